@@ -1,0 +1,297 @@
+"""Benchmark of the hot path: CSR SpMV on MI355X (BASELINE.json metric
+"CSR SpMV GFLOP/s + achieved HBM GB/s (fp64 vs fp32), SuiteSparse set,
+1/2/4/8 GPU").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload big|moderate|NAME]
+    torchrun --nproc-per-node N ... bench.py --gpus N ...      (N > 1, RCCL)
+
+Workload (default "big"): one step = one fp64 y = A x over EACH of the 15
+"big" SuiteSparse matrices (BASELINE config 4; seeded surrogates of the same
+m / stored nnz / structure, since no .mtx data exists offline). With N > 1
+every matrix is row-partitioned (nnz-balanced) across the ranks and each
+SpMV is preceded by the RCCL all-gather of the x slices over xGMI (config 5
+applied to the whole set); total work is fixed => "scaling": "strong".
+Cycling through 3.4 GB of matrices per step also keeps the 256 MB Infinity
+Cache from serving any matrix twice, so the rate is an HBM rate.
+
+value = total GFLOP of all ranks / max-over-ranks wall time of the K steps.
+roofline = the dominant kernel (spmv_tiles, every launch of the step) timed
+with HIP events on the stream it runs on: algorithmic bytes / kernel time
+against 8 TB/s. cpu_baseline = the oracle's OpenMP CSR SpMV (the reference's
+test_spmv.c CPU path, restated) on a bounded sample, rank 0, N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from respasol_amd import csr  # noqa: E402
+from respasol_amd.dist import RowPartitionedSpmv, remap_columns  # noqa: E402
+from respasol_amd.sparse import Handle, SpMat, upload_csr  # noqa: E402
+
+METRIC = "CSR SpMV GFLOP/s + achieved HBM GB/s (fp64 vs fp32), SuiteSparse set, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+class Slice:
+    """One matrix's share on this rank."""
+
+    def __init__(self, name, rank, world, handle, device):
+        self.name = name
+        m = csr.surrogate_rows(name)
+        lens = csr.surrogate_rowlens(name)
+        rowptr = np.zeros(m + 1, np.int64)
+        np.cumsum(lens, out=rowptr[1:])
+        self.m, self.n = m, m
+        self.nnz_global = int(rowptr[-1])
+        self.bounds = csr.partition_rows(rowptr.astype(np.int32), world)
+        r0, r1 = int(self.bounds[rank]), int(self.bounds[rank + 1])
+        self.r0, self.r1 = r0, r1
+        rp, ci, va = csr.surrogate_rows_csr(name, r0, r1)
+        self.host = (rp, ci, va)
+        ci_pad, chunk = remap_columns(ci, self.bounds) if world > 1 else (ci, m)
+        self.n_pad = world * chunk if world > 1 else m
+        self.nnz_local = int(rp[-1])
+        d64 = upload_csr(rp, ci_pad, va, torch.float64, device)
+        self.mat64 = SpMat(handle, *d64, self.n_pad)
+        d32 = upload_csr(rp, ci_pad, va, torch.float32, device)
+        self.mat32 = SpMat(handle, *d32, self.n_pad)
+        x, _ = csr.dlarnv(1, [0, 0, 0, 1], m)
+        self.part64 = RowPartitionedSpmv(self.bounds, rank, torch.float64, device,
+                                         lambda xf, y=None: self.mat64.spmv(xf, y))
+        self.part64.set_local_x(torch.from_numpy(x[r0:r1]).to(device))
+        self.part32 = RowPartitionedSpmv(self.bounds, rank, torch.float32, device,
+                                         lambda xf, y=None: self.mat32.spmv(xf, y))
+        self.part32.set_local_x(torch.from_numpy(x[r0:r1].astype(np.float32)).to(device))
+        self.part64.exchange()
+        self.part32.exchange()
+        self.y64 = torch.empty(max(r1 - r0, 1), dtype=torch.float64, device=device)
+        self.y32 = torch.empty(max(r1 - r0, 1), dtype=torch.float32, device=device)
+
+    def bytes_local(self, elem):
+        """Algorithmic bytes of this rank's SpMV: vals+colidx,
+        rowptr, one read of the replicated x, y write."""
+        ml = self.r1 - self.r0
+        return (elem + 4) * self.nnz_local + 4 * (ml + 1) + elem * self.n + elem * ml
+
+
+def workload_names(w):
+    if w == "big":
+        return csr.surrogate_names(1)
+    if w == "moderate":
+        return csr.surrogate_names(0)
+    return w.split(",")
+
+
+def cpu_baseline(slices, seconds):
+    """Oracle OpenMP fp64 SpMV (test_spmv.c's CPU path restated) over the same
+    matrices, repeated until `seconds` of CPU work; GFLOP/s."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    xs = [csr.dlarnv(1, [0, 0, 0, 1], s.n)[0] for s in slices]
+    for s, x in zip(slices, xs):  # warm (page-in) pass
+        ob.spmv(s.host[0], s.host[1], s.host[2], x, threads=True)
+    flops, t0, passes = 0.0, time.perf_counter(), 0
+    while True:
+        for s, x in zip(slices, xs):
+            ob.spmv(s.host[0], s.host[1], s.host[2], x, threads=True)
+            flops += 2.0 * s.nnz_local
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(flops / el / 1e9, 3), "unit": "GFLOP/s", "cores": ob.lib.oracle_num_threads(),
+            "kind": "port",
+            "sample": f"{passes} full fp64 passes over the {len(slices)}-matrix workload "
+                      f"({el:.1f} s), OpenMP row-parallel CSR, x=dlarnv(1,{{0,0,0,1}})"}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per dominant-kernel launch from a committed rocprofv3 --pmc
+    summary (profiles/*pmc*.json written by scripts/pmc_summary.py), or None."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("workload") == workload and "hbm_bytes_per_launch" in d:
+            best = d["hbm_bytes_per_launch"]
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="big")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--fp32-reps", type=int, default=10)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    handle = Handle()
+    names = workload_names(args.workload)
+
+    t_setup = time.perf_counter()
+    slices = [Slice(n, rank, world, handle, device) for n in names]
+    torch.cuda.synchronize()
+    log(f"setup {time.perf_counter() - t_setup:.1f}s: {len(slices)} matrices, "
+        f"{sum(s.nnz_global for s in slices) / 1e6:.1f} M stored nnz, world={world}")
+
+    stream = torch.cuda.current_stream()
+
+    def step(events=None):
+        for i, s in enumerate(slices):
+            s.part64.exchange()
+            if events is not None:
+                events[i][0].record(stream)
+            s.mat64.spmv(s.part64.x_full, s.y64[: s.r1 - s.r0] if s.r1 > s.r0 else s.y64)
+            if events is not None:
+                events[i][1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+           for _ in slices] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # dominant kernel, this rank: algorithmic bytes / event-timed kernel time
+    kern_ms = sum(ev[k][i][0].elapsed_time(ev[k][i][1]) for k in range(args.steps)
+                  for i in range(len(slices)))
+    launches = args.steps * len(slices)
+    bytes64 = sum(s.bytes_local(8) for s in slices)
+    achieved = bytes64 * args.steps / (kern_ms * 1e-3) / 1e9
+    per_matrix = {s.name: round(sum(ev[k][i][0].elapsed_time(ev[k][i][1]) for k in range(args.steps))
+                                / args.steps * 1e3, 2) for i, s in enumerate(slices)}
+
+    # totals over ranks
+    tot = torch.tensor([float(sum(2.0 * s.nnz_local for s in slices)), float(bytes64)],
+                       dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(tot)
+    flops_step, bytes_step = float(tot[0]), float(tot[1])
+    value = flops_step * args.steps / elapsed / 1e9
+    hbm_gbs = bytes_step * args.steps / elapsed / 1e9
+
+    # fp32 companion measurement (outside the timed region)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for s in slices:
+        s.mat32.spmv(s.part32.x_full, s.y32[: max(s.r1 - s.r0, 1)] if s.r1 > s.r0 else s.y32)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(args.fp32_reps):
+        for s in slices:
+            s.mat32.spmv(s.part32.x_full, s.y32[: s.r1 - s.r0] if s.r1 > s.r0 else s.y32)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms32 = e0.elapsed_time(e1) / args.fp32_reps
+    bytes32 = sum(s.bytes_local(4) for s in slices)
+    fp32 = {"kernel_gflops_rank0": round(sum(2.0 * s.nnz_local for s in slices) / (ms32 * 1e6), 2),
+            "kernel_gbps_rank0": round(bytes32 / (ms32 * 1e6), 1),
+            "ms_per_pass_rank0": round(ms32, 4)}
+
+    # parity spot check of this rank's slice of the largest matrix vs the oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    big = max(slices, key=lambda s: s.nnz_global)
+    xf = big.part64.x_full.cpu().numpy()
+    rp, ci, va = big.host
+    ci_pad = remap_columns(ci, big.bounds)[0] if world > 1 else ci
+    ref = ob.spmv(rp, ci_pad, va, xf, threads=True)
+    got = big.mat64.spmv(big.part64.x_full).cpu().numpy()[: big.r1 - big.r0]
+    bound = ob.spmv_bound(rp, ci_pad, va, xf, 2.0 ** -53)
+    check_ok = bool(np.all(np.abs(got - ref) <= bound))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(slices, args.cpu_seconds)
+
+    if rank == 0:
+        traffic = pmc_traffic(args.workload)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: seeded surrogates of the SuiteSparse matrices (same m, stored nnz, "
+                    "structure family; SURVEY App. A) - no .mtx data offline",
+            "config": {
+                "workload": f"{args.workload}-set CSR SpMV fp64, {len(slices)} matrices per step"
+                            + (", row-partitioned + RCCL all-gather(x)" if world > 1 else ""),
+                "matrices": len(slices),
+                "nnz_stored_total": int(sum(s.nnz_global for s in slices)),
+                "parallelism": f"row-partition x{world}" if world > 1 else "1 GPU",
+            },
+            "hbm_gbps": round(hbm_gbs, 1),
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "rsp_k::spmv_tiles<double,2>",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "avg_launch_us": round(kern_ms / launches * 1e3, 3),
+                "bytes_per_launch_avg": int(bytes64 / len(slices)),
+            },
+            "cpu_baseline": cpu,
+            "fp32": fp32,
+            "per_matrix_us_rank0": per_matrix,
+            "parity_check": "ok" if check_ok else "FAILED",
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not check_ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

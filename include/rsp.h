@@ -1,0 +1,177 @@
+/*
+ * rsp.h — C-ABI of the MI355X (gfx950) sparse operator library `librsp.so`.
+ *
+ * This is the drop-in boundary for the vendor-math layer of ReSpaSol's GPU
+ * drivers: every entry point below replaces one cuSPARSE call (or call family)
+ * made by /root/reference/GPU/spmv.cu or /root/reference/GPU/ilu0.cu, with the
+ * same argument meaning, the same lifecycle (create -> bufferSize ->
+ * analysis -> compute -> zeroPivot -> destroy) and status codes numbered like
+ * cusparseStatus_t so that the drivers' error printing is unchanged.
+ *
+ * Conventions
+ *   - Plain C types only: device pointers are `void*`/typed pointers obtained
+ *     from hipMalloc (or any HIP allocator), sizes are int64_t / size_t, the
+ *     stream is an opaque `void*` holding a hipStream_t (NULL = default stream).
+ *   - CSR with int32 row offsets / column indices, index base 0 (the only form
+ *     the reference uses: GPU/spmv.cu:132-151, GPU/ilu0.cu:122-126).
+ *   - alpha / beta are HOST pointers of the compute type (cuSPARSE default
+ *     pointer mode, GPU/spmv.cu:61-62,77-78).
+ *   - Every call is stream-ordered on the handle's stream; only the calls
+ *     marked "host-blocking" synchronise (as their cuSPARSE counterparts do).
+ *   - No call aborts or exits: failures return a status code.
+ *
+ * Precision: RSP_R_64F / RSP_R_32F select fp64 or fp32 storage AND
+ * accumulation (GPU/spmv.cu:131-162 with and without `#define FLOAT`).
+ * Flush-to-zero (nvcc `-ftz=true`, GPU/Makefile:5) is a handle mode here
+ * (rsp_set_ftz) selecting kernels compiled with fp32 denormal flushing.
+ */
+#ifndef RSP_H
+#define RSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSP_VERSION_MAJOR 0
+#define RSP_VERSION_MINOR 1
+
+/* Numbered exactly like cusparseStatus_t (GPU/spmv.cu:24-29 prints the
+ * integer), so drivers print identical codes. */
+typedef enum {
+    RSP_STATUS_SUCCESS = 0,
+    RSP_STATUS_NOT_INITIALIZED = 1,
+    RSP_STATUS_ALLOC_FAILED = 2,
+    RSP_STATUS_INVALID_VALUE = 3,
+    RSP_STATUS_ARCH_MISMATCH = 4,
+    RSP_STATUS_EXECUTION_FAILED = 6,
+    RSP_STATUS_INTERNAL_ERROR = 7,
+    RSP_STATUS_MATRIX_TYPE_NOT_SUPPORTED = 8,
+    RSP_STATUS_ZERO_PIVOT = 9,
+    RSP_STATUS_NOT_SUPPORTED = 10
+} rsp_status_t;
+
+/* CUDA_R_64F / CUDA_R_32F (GPU/spmv.cu:135,151). */
+typedef enum { RSP_R_64F = 0, RSP_R_32F = 1 } rsp_datatype_t;
+
+/* CUSPARSE_OPERATION_NON_TRANSPOSE / _TRANSPOSE (GPU/ilu0.cu:296,300). */
+typedef enum { RSP_OPERATION_NON_TRANSPOSE = 0, RSP_OPERATION_TRANSPOSE = 1 } rsp_operation_t;
+
+typedef struct rsp_context *rsp_handle_t;       /* cusparseHandle_t       */
+typedef struct rsp_spmat *rsp_spmat_t;          /* cusparseSpMatDescr_t   */
+typedef struct rsp_ilu0_info *rsp_ilu0_info_t;  /* csrilu02Info_t + both csrsv2Info_t */
+
+/* ---------------------------------------------------------------- handle */
+
+/* cusparseCreate (GPU/spmv.cu:128, GPU/ilu0.cu:85). Binds the current HIP
+ * device; fails with ARCH_MISMATCH if it is not gfx950. */
+rsp_status_t rsp_create(rsp_handle_t *handle);
+/* cusparseDestroy (GPU/spmv.cu:282, GPU/ilu0.cu:340). */
+rsp_status_t rsp_destroy(rsp_handle_t handle);
+/* cusparseSetStream. `stream` is a hipStream_t (NULL = default stream). */
+rsp_status_t rsp_set_stream(rsp_handle_t handle, void *stream);
+rsp_status_t rsp_get_stream(rsp_handle_t handle, void **stream);
+/* nvcc -ftz=true (GPU/Makefile:5): fp32 kernels flush denormal inputs and
+ * results to zero when enabled. fp64 is never flushed (as with nvcc). */
+rsp_status_t rsp_set_ftz(rsp_handle_t handle, int enable);
+rsp_status_t rsp_get_ftz(rsp_handle_t handle, int *enable);
+/* cusparseGetErrorString analogue. Never NULL. */
+const char *rsp_get_error_string(rsp_status_t status);
+/* Library version: major*1000 + minor. */
+int rsp_get_version(void);
+
+/* ------------------------------------------------------- CSR descriptor */
+
+/* cusparseCreateCsr(&matA, rows, cols, nnz, offsets, columns, values,
+ * CUSPARSE_INDEX_32I, CUSPARSE_INDEX_32I, CUSPARSE_INDEX_BASE_ZERO, dtype)
+ * (GPU/spmv.cu:132-135,148-151). `nnz` is the caller's count; like cuSPARSE
+ * the kernels use offsets[rows] (the reference passes A.nnz, which exceeds
+ * offsets[rows] for symmetric inputs: SURVEY §0.3). Host-side object only. */
+rsp_status_t rsp_create_csr(rsp_spmat_t *mat, int64_t rows, int64_t cols, int64_t nnz,
+                            void *d_row_offsets, void *d_col_ind, void *d_values,
+                            rsp_datatype_t value_type);
+/* Re-point the values array (e.g. fp64 -> fp32 copy) keeping the analysis. */
+rsp_status_t rsp_csr_set_values(rsp_spmat_t mat, void *d_values, rsp_datatype_t value_type);
+rsp_status_t rsp_destroy_spmat(rsp_spmat_t mat); /* cusparseDestroySpMat (GPU/spmv.cu:279) */
+
+/* ------------------------------------------------------------------ SpMV */
+
+/* cusparseSpMV_bufferSize (GPU/spmv.cu:143-145,159-161). Upper bound on the
+ * workspace rsp_spmv needs; computed from rows/nnz only (no device access). */
+rsp_status_t rsp_spmv_buffer_size(rsp_handle_t handle, rsp_operation_t op, const void *alpha,
+                                  rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
+                                  size_t *buffer_size);
+/* cusparseSpMV_preprocess analogue: builds the row-block schedule of `mat`
+ * into `d_buffer` (host-blocking: reads the row offsets once). rsp_spmv on a
+ * buffer that was not preprocessed for `mat` preprocesses it first. */
+rsp_status_t rsp_spmv_preprocess(rsp_handle_t handle, rsp_operation_t op, const void *alpha,
+                                 rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
+                                 rsp_datatype_t compute_type, void *d_buffer);
+/* cusparseSpMV (GPU/spmv.cu:179-186): y = alpha * A * x + beta * y.
+ * op must be NON_TRANSPOSE (the only form the reference uses). If *beta == 0,
+ * y is write-only. compute_type must equal the matrix value type. Deterministic:
+ * the same inputs give bitwise identical y on every call. */
+rsp_status_t rsp_spmv(rsp_handle_t handle, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
+                      const void *d_x, const void *beta, void *d_y, rsp_datatype_t compute_type,
+                      void *d_buffer);
+
+/* --------------------------------------------------------- ILU(0) + trsv */
+
+/* cusparseCreateCsrilu02Info + 2x cusparseCreateCsrsv2Info (GPU/ilu0.cu:143-150). */
+rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info);
+rsp_status_t rsp_destroy_ilu0_info(rsp_ilu0_info_t info);
+
+/* cusparse?csrilu02_bufferSize / csrsv2_bufferSize (GPU/ilu0.cu:166-186).
+ * The schedule lives in `info` (library-owned), so the external buffer size
+ * is 0; kept for lifecycle parity. */
+rsp_status_t rsp_ilu0_buffer_size(rsp_handle_t handle, int n, int nnz, rsp_datatype_t value_type,
+                                  rsp_ilu0_info_t info, size_t *buffer_size);
+
+/* cusparse?csrilu02_analysis + both csrsv2_analysis (GPU/ilu0.cu:203-252):
+ * diagonal positions, structural-zero detection, level sets of the lower
+ * triangle (factor + L-solve) and of its transpose (L^T-solve), and the
+ * transposed strict-lower index map. `nnz` may exceed offsets[n] (the
+ * reference passes A.nnz, GPU/ilu0.cu:166); offsets[n] is what is analysed.
+ * Host-blocking (reads the pattern once). */
+rsp_status_t rsp_ilu0_analysis(rsp_handle_t handle, int n, int nnz, const int *d_row_offsets,
+                               const int *d_col_ind, rsp_ilu0_info_t info);
+
+/* cusparseXcsrilu02_zeroPivot (GPU/ilu0.cu:222,278). Host-blocking. Returns
+ * RSP_STATUS_ZERO_PIVOT and *position = j (0-based) when A(j,j) is
+ * structurally missing (after analysis) or U(j,j) == 0 (after the numeric
+ * factorisation); the smallest such j is reported. Otherwise SUCCESS, -1. */
+rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t handle, rsp_ilu0_info_t info, int *position);
+
+/* cusparse?csrilu02 (GPU/ilu0.cu:264-268): in-place ILU(0) on the CSR
+ * pattern, IKJ order: for each row i, for each k < i in the pattern
+ * (ascending): a_ik /= u_kk; a_ij -= a_ik * u_kj for j > k in both rows.
+ * value_type selects fp64 or fp32 arithmetic (FTZ per handle mode). */
+rsp_status_t rsp_ilu0_factor(rsp_handle_t handle, rsp_ilu0_info_t info, rsp_datatype_t value_type,
+                             void *d_values);
+
+/* cusparse?csrsv2_solve with desc_L = {LOWER, UNIT} (GPU/ilu0.cu:129-134):
+ *   op == NON_TRANSPOSE: solve L   y = alpha x   (GPU/ilu0.cu:296-298)
+ *   op == TRANSPOSE:     solve L^T y = alpha x   (GPU/ilu0.cu:300-302)
+ * where L is the unit-diagonal strictly-lower part of `d_values` on the
+ * analysed pattern. x and y must not alias. */
+rsp_status_t rsp_trsv_lower_unit(rsp_handle_t handle, rsp_operation_t op, const void *alpha,
+                                 rsp_ilu0_info_t info, rsp_datatype_t value_type,
+                                 const void *d_values, const void *d_x, void *d_y);
+
+/* Extension (off by default): solve with the upper factor
+ * U (non-unit diagonal, upper part incl. diagonal), i.e. the true ILU(0)
+ * apply that the reference's unused desc_U describes (GPU/ilu0.cu:136-141). */
+rsp_status_t rsp_trsv_upper(rsp_handle_t handle, const void *alpha, rsp_ilu0_info_t info,
+                            rsp_datatype_t value_type, const void *d_values, const void *d_x,
+                            void *d_y);
+
+/* Number of dependency levels found by the analysis (L DAG, L^T DAG). */
+rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *levels_upper);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSP_H */

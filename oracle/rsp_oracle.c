@@ -1,0 +1,252 @@
+/*
+ * rsp_oracle.c — TEST INFRASTRUCTURE ONLY (see rsp_oracle.h). CPU
+ * restatement of the reference hot path; never linked into the product.
+ *
+ * Build flags matter: -ffp-contract=off so `s += v * x` is a rounded
+ * product then a rounded sum (the order the GPU tiles reproduce), and fma()
+ * is called explicitly where the restated algorithm fuses (ILU updates and
+ * triangular solves), which the GPU kernels mirror with __builtin_fma.
+ */
+#include "rsp_oracle.h"
+
+#include <limits.h>
+#include <math.h>
+#include <omp.h>
+#include <stdlib.h>
+#include <string.h>
+#include <xmmintrin.h>
+
+static unsigned ftz_enter(int on) {
+    unsigned old = _mm_getcsr();
+    if (on) _mm_setcsr(old | 0x8040u); /* test_pardiso.c:19-24 */
+    return old;
+}
+static void ftz_leave(unsigned old) { _mm_setcsr(old); }
+
+/* ------------------------------------------------------------------ SpMV */
+
+void oracle_spmv_f64(int m, const int *rp, const int *ci, const double *v, const double *x,
+                     double *y) {
+    for (int i = 0; i < m; i++) {
+        double s = 0.0;
+        for (int k = rp[i]; k < rp[i + 1]; k++) s += v[k] * x[ci[k]];
+        y[i] = s;
+    }
+}
+
+void oracle_spmv_f32(int m, const int *rp, const int *ci, const float *v, const float *x,
+                     float *y) {
+    for (int i = 0; i < m; i++) {
+        float s = 0.0f;
+        for (int k = rp[i]; k < rp[i + 1]; k++) s += v[k] * x[ci[k]];
+        y[i] = s;
+    }
+}
+
+void oracle_spmv_f32_ftz(int m, const int *rp, const int *ci, const float *v, const float *x,
+                         float *y) {
+    unsigned old = ftz_enter(1);
+    oracle_spmv_f32(m, rp, ci, v, x, y);
+    ftz_leave(old);
+}
+
+void oracle_spmv_f64_omp(int m, const int *rp, const int *ci, const double *v, const double *x,
+                         double *y) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < m; i++) {
+        double s = 0.0;
+        for (int k = rp[i]; k < rp[i + 1]; k++) s += v[k] * x[ci[k]];
+        y[i] = s;
+    }
+}
+
+void oracle_spmv_f32_omp(int m, const int *rp, const int *ci, const float *v, const float *x,
+                         float *y) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < m; i++) {
+        float s = 0.0f;
+        for (int k = rp[i]; k < rp[i + 1]; k++) s += v[k] * x[ci[k]];
+        y[i] = s;
+    }
+}
+
+int oracle_num_threads(void) { return omp_get_max_threads(); }
+
+/* ---------------------------------------------------------------- ILU(0) */
+
+/* first position in row i with column >= i */
+static int diag_pos(const int *rp, const int *ci, int i) {
+    int lo = rp[i], hi = rp[i + 1];
+    while (lo < hi) {
+        int mid = lo + (hi - lo) / 2;
+        if (ci[mid] < i)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+#define ORACLE_ILU0(T, NAME, FMA)                                                              \
+    static int NAME(int n, const int *rp, const int *ci, T *v, int *zero_pivot) {              \
+        int *dp = (int *)malloc(sizeof(int) * (size_t)(n ? n : 1));                            \
+        int *hd = (int *)malloc(sizeof(int) * (size_t)(n ? n : 1));                            \
+        int *iw = (int *)malloc(sizeof(int) * (size_t)(n ? n : 1));                            \
+        int structural = -1;                                                                   \
+        for (int i = 0; i < n; i++) {                                                          \
+            dp[i] = diag_pos(rp, ci, i);                                                       \
+            hd[i] = dp[i] < rp[i + 1] && ci[dp[i]] == i;                                       \
+            if (!hd[i] && structural < 0) structural = i;                                      \
+            iw[i] = -1;                                                                        \
+        }                                                                                      \
+        *zero_pivot = -1;                                                                      \
+        if (structural >= 0) {                                                                 \
+            free(dp);                                                                          \
+            free(hd);                                                                          \
+            free(iw);                                                                          \
+            return structural;                                                                 \
+        }                                                                                      \
+        for (int i = 0; i < n; i++) {                                                          \
+            for (int p = rp[i]; p < rp[i + 1]; p++) iw[ci[p]] = p;                             \
+            for (int p = rp[i]; p < dp[i]; p++) {                                              \
+                int k = ci[p];                                                                 \
+                T lik = v[p] / v[dp[k]];                                                       \
+                v[p] = lik;                                                                    \
+                for (int q = dp[k] + 1; q < rp[k + 1]; q++) {                                  \
+                    int w = iw[ci[q]];                                                         \
+                    if (w > p) v[w] = FMA(-lik, v[q], v[w]);                                   \
+                }                                                                              \
+            }                                                                                  \
+            if (v[dp[i]] == (T)0 && *zero_pivot < 0) *zero_pivot = i;                          \
+            for (int p = rp[i]; p < rp[i + 1]; p++) iw[ci[p]] = -1;                            \
+        }                                                                                      \
+        free(dp);                                                                              \
+        free(hd);                                                                              \
+        free(iw);                                                                              \
+        return -1;                                                                             \
+    }
+
+ORACLE_ILU0(double, ilu0_d, fma)
+ORACLE_ILU0(float, ilu0_s, fmaf)
+
+int oracle_ilu0_f64(int n, const int *rp, const int *ci, double *v, int *zero_pivot) {
+    return ilu0_d(n, rp, ci, v, zero_pivot);
+}
+
+int oracle_ilu0_f32(int n, const int *rp, const int *ci, float *v, int *zero_pivot, int ftz) {
+    unsigned old = ftz_enter(ftz);
+    int r = ilu0_s(n, rp, ci, v, zero_pivot);
+    ftz_leave(old);
+    return r;
+}
+
+/* ------------------------------------------------------------------ trsv */
+
+#define ORACLE_TRSV(T, SUF, FMA)                                                               \
+    static void lower_n_##SUF(int n, const int *rp, const int *ci, const T *v, T alpha,        \
+                              const T *x, T *y) {                                              \
+        for (int i = 0; i < n; i++) {                                                          \
+            T s = alpha * x[i];                                                                \
+            for (int p = rp[i]; p < rp[i + 1] && ci[p] < i; p++) s = FMA(-v[p], y[ci[p]], s);  \
+            y[i] = s;                                                                          \
+        }                                                                                      \
+    }                                                                                          \
+    static void lower_t_##SUF(int n, const int *rp, const int *ci, const T *v, T alpha,        \
+                              const T *x, T *y) {                                              \
+        for (int i = 0; i < n; i++) y[i] = alpha * x[i];                                       \
+        for (int j = n - 1; j >= 0; j--) {                                                     \
+            const T yj = y[j];                                                                 \
+            for (int p = rp[j]; p < rp[j + 1] && ci[p] < j; p++)                               \
+                y[ci[p]] = FMA(-v[p], yj, y[ci[p]]);                                           \
+        }                                                                                      \
+    }                                                                                          \
+    static void upper_##SUF(int n, const int *rp, const int *ci, const T *v, T alpha,          \
+                            const T *x, T *y) {                                                \
+        for (int i = n - 1; i >= 0; i--) {                                                     \
+            T s = alpha * x[i];                                                                \
+            int d = diag_pos(rp, ci, i);                                                       \
+            int hd = d < rp[i + 1] && ci[d] == i;                                              \
+            for (int p = d + hd; p < rp[i + 1]; p++) s = FMA(-v[p], y[ci[p]], s);              \
+            y[i] = s / (hd ? v[d] : (T)0);                                                     \
+        }                                                                                      \
+    }
+
+ORACLE_TRSV(double, d, fma)
+ORACLE_TRSV(float, s, fmaf)
+
+void oracle_trsv_lower_n_f64(int n, const int *rp, const int *ci, const double *v, double alpha,
+                             const double *x, double *y) {
+    lower_n_d(n, rp, ci, v, alpha, x, y);
+}
+void oracle_trsv_lower_n_f32(int n, const int *rp, const int *ci, const float *v, float alpha,
+                             const float *x, float *y, int ftz) {
+    unsigned old = ftz_enter(ftz);
+    lower_n_s(n, rp, ci, v, alpha, x, y);
+    ftz_leave(old);
+}
+void oracle_trsv_lower_t_f64(int n, const int *rp, const int *ci, const double *v, double alpha,
+                             const double *x, double *y) {
+    lower_t_d(n, rp, ci, v, alpha, x, y);
+}
+void oracle_trsv_lower_t_f32(int n, const int *rp, const int *ci, const float *v, float alpha,
+                             const float *x, float *y, int ftz) {
+    unsigned old = ftz_enter(ftz);
+    lower_t_s(n, rp, ci, v, alpha, x, y);
+    ftz_leave(old);
+}
+void oracle_trsv_upper_f64(int n, const int *rp, const int *ci, const double *v, double alpha,
+                           const double *x, double *y) {
+    upper_d(n, rp, ci, v, alpha, x, y);
+}
+void oracle_trsv_upper_f32(int n, const int *rp, const int *ci, const float *v, float alpha,
+                           const float *x, float *y, int ftz) {
+    unsigned old = ftz_enter(ftz);
+    upper_s(n, rp, ci, v, alpha, x, y);
+    ftz_leave(old);
+}
+
+/* ---------------------------------------------------------------- dlarnv */
+
+/* seed * mult mod 2^48 in 12-bit limbs, exactly as DLARUV's IT1..IT4 chain. */
+static void limb_mul(const int s[4], const int mm[4], int out[4]) {
+    const int P = 4096;
+    int it4 = s[3] * mm[3];
+    int it3 = it4 / P;
+    it4 -= P * it3;
+    it3 += s[2] * mm[3] + s[3] * mm[2];
+    int it2 = it3 / P;
+    it3 -= P * it2;
+    it2 += s[1] * mm[3] + s[2] * mm[2] + s[3] * mm[1];
+    int it1 = it2 / P;
+    it2 -= P * it1;
+    it1 += s[0] * mm[3] + s[1] * mm[2] + s[2] * mm[1] + s[3] * mm[0];
+    it1 %= P;
+    out[0] = it1;
+    out[1] = it2;
+    out[2] = it3;
+    out[3] = it4;
+}
+
+int oracle_dlarnv(int idist, int *iseed, int n, double *x) {
+    if (idist != 1 && idist != 2) return -1;
+    static const int a1[4] = {494, 322, 2508, 2549}; /* DLARUV MM(1,:) */
+    int mm[128][4];
+    memcpy(mm[0], a1, sizeof(a1));
+    for (int i = 1; i < 128; i++) limb_mul(mm[i - 1], a1, mm[i]);
+    const double r = 1.0 / 4096.0;
+    int seed[4] = {iseed[0], iseed[1], iseed[2], iseed[3]};
+    for (int iv = 0; iv < n; iv += 64) { /* DLARNV: LV/2 = 64 per DLARUV call */
+        int il = n - iv < 64 ? n - iv : 64;
+        int last[4] = {seed[0], seed[1], seed[2], seed[3]};
+        for (int i = 0; i < il; i++) {
+            int it[4];
+            limb_mul(seed, mm[i], it);
+            double u = r * ((double)it[0] + r * ((double)it[1] + r * ((double)it[2] + r * (double)it[3])));
+            x[iv + i] = idist == 1 ? u : 2.0 * u - 1.0;
+            memcpy(last, it, sizeof(it));
+        }
+        memcpy(seed, last, sizeof(seed));
+    }
+    memcpy(iseed, seed, sizeof(seed));
+    return 0;
+}

@@ -1,0 +1,659 @@
+// rsp_api.cpp — implementation of include/rsp.h (the C-ABI operator library
+// librsp.so). Host-side planning (SpMV row-block schedule, ILU(0) level sets)
+// plus launches of the kernels in spmv.hip / ilu0.hip. Mirrors the cuSPARSE
+// lifecycle the reference drivers use (GPU/spmv.cu:122-186,
+// GPU/ilu0.cu:82-310); see include/rsp.h for the per-call mapping.
+
+#include "rsp.h"
+
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "rsp_kernels.h"
+
+using rsp::SpmvBlock;
+using rsp::SpmvLongRow;
+using rsp::SpmvTile;
+
+struct rsp_context {
+    int device;
+    hipStream_t stream;
+    int ftz;
+};
+
+struct rsp_spmat {
+    int64_t rows, cols, nnz;
+    int *rowptr;
+    int *colidx;
+    void *vals;
+    rsp_datatype_t type;
+    // schedule state
+    const void *plan_buffer;  // buffer the schedule was written into
+    rsp_datatype_t plan_type;
+    int nblocks, nlong, nslots;
+    size_t off_long, off_part;  // byte offsets inside the buffer
+};
+
+struct rsp_ilu0_info {
+    int analysed;
+    int n, nnz_s;
+    const int *rowptr, *colidx;  // device pattern captured at analysis
+    int structural_zero;         // -1 = none
+    int factored;
+    int *d_dpos, *d_hasdiag;
+    int *d_rows_l, *d_rows_lt, *d_rows_u;
+    int *d_lt_ptr, *d_lt_src, *d_lt_col;
+    int *d_zero;
+    std::vector<int> lev_l, lev_lt, lev_u;  // host level pointers
+};
+
+#define RSP_CHECK_HIP(call)                                                     \
+    do {                                                                        \
+        hipError_t e_ = (call);                                                 \
+        if (e_ != hipSuccess)                                                   \
+            return e_ == hipErrorOutOfMemory ? RSP_STATUS_ALLOC_FAILED          \
+                                             : RSP_STATUS_EXECUTION_FAILED;     \
+    } while (0)
+
+extern "C" {
+
+int rsp_get_version(void) { return RSP_VERSION_MAJOR * 1000 + RSP_VERSION_MINOR; }
+
+const char *rsp_get_error_string(rsp_status_t s) {
+    switch (s) {
+        case RSP_STATUS_SUCCESS: return "RSP_STATUS_SUCCESS";
+        case RSP_STATUS_NOT_INITIALIZED: return "RSP_STATUS_NOT_INITIALIZED";
+        case RSP_STATUS_ALLOC_FAILED: return "RSP_STATUS_ALLOC_FAILED";
+        case RSP_STATUS_INVALID_VALUE: return "RSP_STATUS_INVALID_VALUE";
+        case RSP_STATUS_ARCH_MISMATCH: return "RSP_STATUS_ARCH_MISMATCH";
+        case RSP_STATUS_EXECUTION_FAILED: return "RSP_STATUS_EXECUTION_FAILED";
+        case RSP_STATUS_INTERNAL_ERROR: return "RSP_STATUS_INTERNAL_ERROR";
+        case RSP_STATUS_MATRIX_TYPE_NOT_SUPPORTED: return "RSP_STATUS_MATRIX_TYPE_NOT_SUPPORTED";
+        case RSP_STATUS_ZERO_PIVOT: return "RSP_STATUS_ZERO_PIVOT";
+        case RSP_STATUS_NOT_SUPPORTED: return "RSP_STATUS_NOT_SUPPORTED";
+    }
+    return "RSP_STATUS_UNKNOWN";
+}
+
+rsp_status_t rsp_create(rsp_handle_t *handle) {
+    if (!handle) return RSP_STATUS_INVALID_VALUE;
+    *handle = nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return RSP_STATUS_NOT_INITIALIZED;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return RSP_STATUS_NOT_INITIALIZED;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RSP_STATUS_ARCH_MISMATCH;
+    rsp_context *c = new (std::nothrow) rsp_context;
+    if (!c) return RSP_STATUS_ALLOC_FAILED;
+    c->device = dev;
+    c->stream = nullptr;
+    c->ftz = 0;
+    *handle = c;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_destroy(rsp_handle_t h) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    delete h;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_set_stream(rsp_handle_t h, void *stream) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    h->stream = (hipStream_t)stream;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_get_stream(rsp_handle_t h, void **stream) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!stream) return RSP_STATUS_INVALID_VALUE;
+    *stream = (void *)h->stream;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_set_ftz(rsp_handle_t h, int enable) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    h->ftz = enable ? 1 : 0;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_get_ftz(rsp_handle_t h, int *enable) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!enable) return RSP_STATUS_INVALID_VALUE;
+    *enable = h->ftz;
+    return RSP_STATUS_SUCCESS;
+}
+
+/* ------------------------------------------------------------------ CSR */
+
+rsp_status_t rsp_create_csr(rsp_spmat_t *mat, int64_t rows, int64_t cols, int64_t nnz,
+                            void *d_row_offsets, void *d_col_ind, void *d_values,
+                            rsp_datatype_t value_type) {
+    if (!mat) return RSP_STATUS_INVALID_VALUE;
+    *mat = nullptr;
+    if (rows < 0 || cols < 0 || nnz < 0 || rows > INT_MAX - 1 || cols > INT_MAX || nnz > INT_MAX)
+        return RSP_STATUS_INVALID_VALUE;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    if (!d_row_offsets && rows > 0) return RSP_STATUS_INVALID_VALUE;
+    if ((!d_col_ind || !d_values) && nnz > 0) return RSP_STATUS_INVALID_VALUE;
+    rsp_spmat *a = new (std::nothrow) rsp_spmat;
+    if (!a) return RSP_STATUS_ALLOC_FAILED;
+    memset(a, 0, sizeof(*a));
+    a->rows = rows;
+    a->cols = cols;
+    a->nnz = nnz;
+    a->rowptr = (int *)d_row_offsets;
+    a->colidx = (int *)d_col_ind;
+    a->vals = d_values;
+    a->type = value_type;
+    a->plan_buffer = nullptr;
+    *mat = a;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_csr_set_values(rsp_spmat_t mat, void *d_values, rsp_datatype_t value_type) {
+    if (!mat) return RSP_STATUS_INVALID_VALUE;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    mat->vals = d_values;
+    if (value_type != mat->type) mat->plan_buffer = nullptr;  // tile size depends on type
+    mat->type = value_type;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_destroy_spmat(rsp_spmat_t mat) {
+    if (!mat) return RSP_STATUS_INVALID_VALUE;
+    delete mat;
+    return RSP_STATUS_SUCCESS;
+}
+
+/* ----------------------------------------------------------------- SpMV */
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct SpmvBounds {
+    size_t nblocks, nlong, nslots;
+};
+
+static SpmvBounds spmv_bounds(int64_t rows, int64_t nnz, int cap) {
+    // greedy packing: two consecutive size-closed tiles exceed `cap`, long
+    // rows contribute <= nnz/cap + 1 chunks each side.
+    SpmvBounds b;
+    size_t q = (size_t)(nnz / cap) + 1;
+    b.nlong = q;
+    b.nslots = 2 * q + 1;
+    b.nblocks = 6 * q + (size_t)(rows / rsp::kSpmvMaxRows) + 8;
+    return b;
+}
+
+static size_t spmv_bytes(const SpmvBounds &b, size_t elem, size_t *off_long, size_t *off_part) {
+    size_t o1 = align256(b.nblocks * sizeof(SpmvBlock));
+    size_t o2 = o1 + align256(b.nlong * sizeof(SpmvLongRow));
+    if (off_long) *off_long = o1;
+    if (off_part) *off_part = o2;
+    return o2 + align256(b.nslots * elem);
+}
+
+static int tile_cap(rsp_datatype_t t) {
+    return t == RSP_R_64F ? SpmvTile<double>::kMaxNnz : SpmvTile<float>::kMaxNnz;
+}
+static size_t elem_size(rsp_datatype_t t) { return t == RSP_R_64F ? 8 : 4; }
+
+rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                  rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
+                                  size_t *buffer_size) {
+    (void)alpha;
+    (void)beta;
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!mat || !buffer_size) return RSP_STATUS_INVALID_VALUE;
+    if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
+    if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
+    SpmvBounds b = spmv_bounds(mat->rows, mat->nnz, tile_cap(compute_type));
+    *buffer_size = spmv_bytes(b, elem_size(compute_type), nullptr, nullptr);
+    return RSP_STATUS_SUCCESS;
+}
+
+// Greedy row-block schedule over host row offsets (see spmv.hip header).
+static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock> &blocks,
+                           std::vector<SpmvLongRow> &longrows, int *nslots) {
+    blocks.clear();
+    longrows.clear();
+    int slots = 0;
+    int r = 0;
+    while (r < m) {
+        int len = rp[r + 1] - rp[r];
+        if (len > cap) {
+            SpmvLongRow lr;
+            lr.row = r;
+            lr.first = slots;
+            lr.nchunks = 0;
+            lr.pad = 0;
+            for (int k = rp[r]; k < rp[r + 1]; k += cap) {
+                SpmvBlock b;
+                b.r0 = r;
+                b.r1 = -(slots + 1);
+                b.k0 = k;
+                b.k1 = std::min(k + cap, rp[r + 1]);
+                blocks.push_back(b);
+                slots++;
+                lr.nchunks++;
+            }
+            longrows.push_back(lr);
+            r++;
+            continue;
+        }
+        int start = r, nnz = 0;
+        while (r < m && r - start < rsp::kSpmvMaxRows) {
+            int l = rp[r + 1] - rp[r];
+            if (l > cap || nnz + l > cap) break;
+            nnz += l;
+            r++;
+        }
+        SpmvBlock b;
+        b.r0 = start;
+        b.r1 = r;
+        b.k0 = rp[start];
+        b.k1 = rp[r];
+        blocks.push_back(b);
+    }
+    *nslots = slots;
+    return 0;
+}
+
+rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                 rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
+                                 rsp_datatype_t compute_type, void *d_buffer) {
+    (void)alpha;
+    (void)beta;
+    (void)d_x;
+    (void)d_y;
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!mat) return RSP_STATUS_INVALID_VALUE;
+    if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
+    if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
+    const int m = (int)mat->rows;
+    std::vector<int> rp((size_t)m + 1, 0);
+    if (m > 0) {
+        RSP_CHECK_HIP(hipMemcpyAsync(rp.data(), mat->rowptr, ((size_t)m + 1) * sizeof(int),
+                                     hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
+    if (m > 0 && rp[0] != 0) return RSP_STATUS_INVALID_VALUE;  // base 0 only
+    for (int i = 0; i < m; i++)
+        if (rp[i + 1] < rp[i]) return RSP_STATUS_INVALID_VALUE;
+    // Column indices are gathered unchecked by the kernel: validate them once
+    // here (preprocess is outside the timed loop) so a malformed matrix is an
+    // INVALID_VALUE status, never an out-of-bounds read of x on the GPU.
+    if (m > 0 && rp[(size_t)m] > 0) {
+        if (!mat->colidx) return RSP_STATUS_INVALID_VALUE;
+        std::vector<int> ci((size_t)rp[(size_t)m]);
+        RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), mat->colidx, ci.size() * sizeof(int),
+                                     hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+        const int ncols = (int)mat->cols;
+        for (int c : ci)
+            if ((unsigned)c >= (unsigned)ncols) return RSP_STATUS_INVALID_VALUE;
+    }
+    const int cap = tile_cap(compute_type);
+    std::vector<SpmvBlock> blocks;
+    std::vector<SpmvLongRow> longrows;
+    int nslots = 0;
+    build_spmv_plan(rp.data(), m, cap, blocks, longrows, &nslots);
+    // the caller sized the buffer from mat->nnz; make sure the plan fits
+    SpmvBounds b = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), cap);
+    if (blocks.size() > b.nblocks || longrows.size() > b.nlong || (size_t)nslots > b.nslots)
+        return RSP_STATUS_INVALID_VALUE;
+    if (!blocks.empty() && !d_buffer) return RSP_STATUS_INVALID_VALUE;
+    size_t off_long = 0, off_part = 0;
+    spmv_bytes(b, elem_size(compute_type), &off_long, &off_part);
+    char *buf = (char *)d_buffer;
+    if (!blocks.empty())
+        RSP_CHECK_HIP(hipMemcpyAsync(buf, blocks.data(), blocks.size() * sizeof(SpmvBlock),
+                                     hipMemcpyHostToDevice, h->stream));
+    if (!longrows.empty())
+        RSP_CHECK_HIP(hipMemcpyAsync(buf + off_long, longrows.data(),
+                                     longrows.size() * sizeof(SpmvLongRow), hipMemcpyHostToDevice,
+                                     h->stream));
+    RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    mat->plan_buffer = d_buffer;
+    mat->plan_type = compute_type;
+    mat->nblocks = (int)blocks.size();
+    mat->nlong = (int)longrows.size();
+    mat->nslots = nslots;
+    mat->off_long = off_long;
+    mat->off_part = off_part;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
+                      const void *d_x, const void *beta, void *d_y, rsp_datatype_t compute_type,
+                      void *d_buffer) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!mat || !alpha || !beta) return RSP_STATUS_INVALID_VALUE;
+    if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
+    if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
+    if (mat->rows > 0 && (!d_y || (mat->cols > 0 && !d_x))) return RSP_STATUS_INVALID_VALUE;
+    if (mat->plan_buffer != d_buffer || mat->plan_type != compute_type || mat->plan_buffer == nullptr) {
+        rsp_status_t st =
+            rsp_spmv_preprocess(h, op, alpha, mat, d_x, beta, d_y, compute_type, d_buffer);
+        if (st != RSP_STATUS_SUCCESS) return st;
+    }
+    rsp::SpmvArgs a;
+    a.m = (int)mat->rows;
+    a.rowptr = mat->rowptr;
+    a.colidx = mat->colidx;
+    a.vals = mat->vals;
+    a.x = d_x;
+    a.y = d_y;
+    a.blocks = (const SpmvBlock *)d_buffer;
+    a.nblocks = mat->nblocks;
+    a.longrows = (const SpmvLongRow *)((char *)d_buffer + mat->off_long);
+    a.nlong = mat->nlong;
+    a.partials = (char *)d_buffer + mat->off_part;
+    if (compute_type == RSP_R_64F) {
+        a.alpha = *(const double *)alpha;
+        a.beta = *(const double *)beta;
+    } else {
+        a.alpha = *(const float *)alpha;
+        a.beta = *(const float *)beta;
+    }
+    a.vector_ok = ((((uintptr_t)mat->colidx) | ((uintptr_t)mat->vals)) & 15) == 0;
+    hipError_t e;
+    if (compute_type == RSP_R_64F)
+        e = rsp_k::spmv_f64(a, h->stream);
+    else
+        e = h->ftz ? rsp_k_ftz::spmv_f32(a, h->stream) : rsp_k::spmv_f32(a, h->stream);
+    return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+/* --------------------------------------------------------------- ILU(0) */
+
+static void ilu_free_device(rsp_ilu0_info *f) {
+    int **ptrs[] = {&f->d_dpos,   &f->d_hasdiag, &f->d_rows_l, &f->d_rows_lt, &f->d_rows_u,
+                    &f->d_lt_ptr, &f->d_lt_src,  &f->d_lt_col, &f->d_zero};
+    for (int **p : ptrs) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+}
+
+rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
+    if (!info) return RSP_STATUS_INVALID_VALUE;
+    rsp_ilu0_info *f = new (std::nothrow) rsp_ilu0_info();
+    if (!f) return RSP_STATUS_ALLOC_FAILED;
+    f->analysed = 0;
+    f->structural_zero = -1;
+    f->factored = 0;
+    f->d_dpos = f->d_hasdiag = f->d_rows_l = f->d_rows_lt = f->d_rows_u = nullptr;
+    f->d_lt_ptr = f->d_lt_src = f->d_lt_col = f->d_zero = nullptr;
+    *info = f;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_destroy_ilu0_info(rsp_ilu0_info_t info) {
+    if (!info) return RSP_STATUS_INVALID_VALUE;
+    ilu_free_device(info);
+    delete info;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_ilu0_buffer_size(rsp_handle_t h, int n, int nnz, rsp_datatype_t value_type,
+                                  rsp_ilu0_info_t info, size_t *buffer_size) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!info || !buffer_size || n < 0 || nnz < 0) return RSP_STATUS_INVALID_VALUE;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    *buffer_size = 0;
+    return RSP_STATUS_SUCCESS;
+}
+
+// rows grouped by level (stable: ascending row within a level)
+static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int> &ptr,
+                         std::vector<int> &rows) {
+    ptr.assign((size_t)nlev + 1, 0);
+    for (int v : lev) ptr[(size_t)v + 1]++;
+    for (int l = 0; l < nlev; l++) ptr[(size_t)l + 1] += ptr[(size_t)l];
+    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+    rows.assign(lev.size(), 0);
+    for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
+}
+
+static hipError_t upload(int **dst, const std::vector<int> &v) {
+    size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(int);
+    hipError_t e = hipMalloc((void **)dst, bytes);
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpy(*dst, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice);
+    return e;
+}
+
+rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_offsets,
+                               const int *d_col_ind, rsp_ilu0_info_t f) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!f || n < 0 || nnz < 0 || (n > 0 && !d_row_offsets)) return RSP_STATUS_INVALID_VALUE;
+    ilu_free_device(f);
+    f->analysed = 0;
+    f->factored = 0;
+    f->structural_zero = -1;
+    std::vector<int> rp((size_t)n + 1, 0);
+    if (n > 0) {
+        RSP_CHECK_HIP(hipMemcpyAsync(rp.data(), d_row_offsets, ((size_t)n + 1) * sizeof(int),
+                                     hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
+    if (rp[0] != 0) return RSP_STATUS_INVALID_VALUE;
+    for (int i = 0; i < n; i++)
+        if (rp[(size_t)i + 1] < rp[(size_t)i]) return RSP_STATUS_INVALID_VALUE;
+    const int nnz_s = rp[(size_t)n];
+    if (nnz_s > 0 && !d_col_ind) return RSP_STATUS_INVALID_VALUE;
+    std::vector<int> ci((size_t)nnz_s);
+    if (nnz_s > 0) {
+        RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), d_col_ind, (size_t)nnz_s * sizeof(int),
+                                     hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
+    for (int v : ci)
+        if (v < 0 || v >= n) return RSP_STATUS_INVALID_VALUE;
+    std::vector<int> dpos((size_t)n), hasdiag((size_t)n);
+    for (int i = 0; i < n; i++) {
+        const int *b = ci.data() + rp[(size_t)i], *e = ci.data() + rp[(size_t)i + 1];
+        const int *p = std::lower_bound(b, e, i);
+        dpos[(size_t)i] = (int)(p - ci.data());
+        hasdiag[(size_t)i] = (p != e && *p == i) ? 1 : 0;
+        if (!hasdiag[(size_t)i] && f->structural_zero < 0) f->structural_zero = i;
+    }
+    // levels of the lower DAG (factor + L solve)
+    std::vector<int> lv((size_t)n, 0);
+    int nl = n > 0 ? 1 : 0;
+    for (int i = 0; i < n; i++) {
+        int l = 0;
+        for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) l = std::max(l, lv[(size_t)ci[(size_t)p]] + 1);
+        lv[(size_t)i] = l;
+        nl = std::max(nl, l + 1);
+    }
+    // transposed strict lower: row k lists (j, pos) for l_jk, j descending
+    std::vector<int> ltp((size_t)n + 1, 0);
+    for (int j = 0; j < n; j++)
+        for (int p = rp[(size_t)j]; p < dpos[(size_t)j]; p++) ltp[(size_t)ci[(size_t)p] + 1]++;
+    for (int k = 0; k < n; k++) ltp[(size_t)k + 1] += ltp[(size_t)k];
+    std::vector<int> lts((size_t)ltp[(size_t)n]), ltc((size_t)ltp[(size_t)n]);
+    {
+        std::vector<int> fill(ltp.begin(), ltp.end() - 1);
+        for (int j = n - 1; j >= 0; j--)
+            for (int p = rp[(size_t)j]; p < dpos[(size_t)j]; p++) {
+                int k = ci[(size_t)p];
+                int slot = fill[(size_t)k]++;
+                lts[(size_t)slot] = p;
+                ltc[(size_t)slot] = j;
+            }
+    }
+    // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
+    std::vector<int> lvt((size_t)n, 0);
+    int nlt = n > 0 ? 1 : 0;
+    for (int j = n - 1; j >= 0; j--) {
+        nlt = std::max(nlt, lvt[(size_t)j] + 1);
+        for (int p = rp[(size_t)j]; p < dpos[(size_t)j]; p++) {
+            int k = ci[(size_t)p];
+            lvt[(size_t)k] = std::max(lvt[(size_t)k], lvt[(size_t)j] + 1);
+        }
+    }
+    // levels of the U DAG (extension): row i waits for j > i with u_ij != 0
+    std::vector<int> lvu((size_t)n, 0);
+    int nlu = n > 0 ? 1 : 0;
+    for (int i = n - 1; i >= 0; i--) {
+        int l = 0;
+        for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++)
+            l = std::max(l, lvu[(size_t)ci[(size_t)p]] + 1);
+        lvu[(size_t)i] = l;
+        nlu = std::max(nlu, l + 1);
+    }
+    std::vector<int> rows_l, rows_lt, rows_u;
+    group_levels(lv, nl, f->lev_l, rows_l);
+    group_levels(lvt, nlt, f->lev_lt, rows_lt);
+    group_levels(lvu, nlu, f->lev_u, rows_u);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
+    if (e == hipSuccess) e = upload(&f->d_hasdiag, hasdiag);
+    if (e == hipSuccess) e = upload(&f->d_rows_l, rows_l);
+    if (e == hipSuccess) e = upload(&f->d_rows_lt, rows_lt);
+    if (e == hipSuccess) e = upload(&f->d_rows_u, rows_u);
+    if (e == hipSuccess) e = upload(&f->d_lt_ptr, ltp);
+    if (e == hipSuccess) e = upload(&f->d_lt_src, lts);
+    if (e == hipSuccess) e = upload(&f->d_lt_col, ltc);
+    if (e == hipSuccess) e = hipMalloc((void **)&f->d_zero, sizeof(int));
+    if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
+    if (e != hipSuccess) {
+        ilu_free_device(f);
+        return e == hipErrorOutOfMemory ? RSP_STATUS_ALLOC_FAILED : RSP_STATUS_EXECUTION_FAILED;
+    }
+    f->n = n;
+    f->nnz_s = nnz_s;
+    f->rowptr = d_row_offsets;
+    f->colidx = d_col_ind;
+    f->analysed = 1;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t f, int *levels_lower, int *levels_upper) {
+    if (!f || !f->analysed) return RSP_STATUS_INVALID_VALUE;
+    if (levels_lower) *levels_lower = (int)f->lev_l.size() - 1;
+    if (levels_upper) *levels_upper = (int)f->lev_lt.size() - 1;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *position) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!f || !position) return RSP_STATUS_INVALID_VALUE;
+    *position = -1;
+    if (!f->analysed) return RSP_STATUS_INVALID_VALUE;
+    int pos = f->structural_zero;
+    if (f->factored) {
+        int z = INT_MAX;
+        RSP_CHECK_HIP(hipMemcpyAsync(&z, f->d_zero, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+        if (z != INT_MAX && (pos < 0 || z < pos)) pos = z;
+    }
+    if (pos >= 0) {
+        *position = pos;
+        return RSP_STATUS_ZERO_PIVOT;
+    }
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
+                             void *d_values) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!f || !f->analysed || (f->nnz_s > 0 && !d_values)) return RSP_STATUS_INVALID_VALUE;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    RSP_CHECK_HIP(hipMemsetD32Async(f->d_zero, INT_MAX, 1, h->stream));
+    rsp::IluArgs a;
+    a.n = f->n;
+    a.rowptr = f->rowptr;
+    a.colidx = f->colidx;
+    a.dpos = f->d_dpos;
+    a.hasdiag = f->d_hasdiag;
+    a.vals = d_values;
+    a.zero_pivot = f->d_zero;
+    a.level_rows = f->d_rows_l;
+    a.level_ptr_host = f->lev_l.data();
+    a.nlev = (int)f->lev_l.size() - 1;
+    hipError_t e;
+    if (value_type == RSP_R_64F)
+        e = rsp_k::ilu0_factor_f64(a, h->stream);
+    else
+        e = h->ftz ? rsp_k_ftz::ilu0_factor_f32(a, h->stream) : rsp_k::ilu0_factor_f32(a, h->stream);
+    f->factored = 1;
+    return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype_t t,
+                               const void *vals, const void *x, void *y) {
+    rsp::TrsvArgs a;
+    a.n = f->n;
+    a.rowptr = f->rowptr;
+    a.colidx = f->colidx;
+    a.dpos = f->d_dpos;
+    a.hasdiag = f->d_hasdiag;
+    a.vals = vals;
+    a.x = x;
+    a.y = y;
+    a.alpha = (t == RSP_R_64F) ? *(const double *)alpha : (double)*(const float *)alpha;
+    a.lt_ptr = f->d_lt_ptr;
+    a.lt_src = f->d_lt_src;
+    a.lt_col = f->d_lt_col;
+    a.level_rows = nullptr;
+    a.level_ptr_host = nullptr;
+    a.nlev = 0;
+    return a;
+}
+
+rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                 rsp_ilu0_info_t f, rsp_datatype_t value_type,
+                                 const void *d_values, const void *d_x, void *d_y) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!f || !f->analysed || !alpha) return RSP_STATUS_INVALID_VALUE;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
+    rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
+    hipError_t e;
+    const bool f64 = value_type == RSP_R_64F, ftz = h->ftz != 0;
+    if (op == RSP_OPERATION_NON_TRANSPOSE) {
+        a.level_rows = f->d_rows_l;
+        a.level_ptr_host = f->lev_l.data();
+        a.nlev = (int)f->lev_l.size() - 1;
+        e = f64 ? rsp_k::trsv_lower_n_f64(a, h->stream)
+                : (ftz ? rsp_k_ftz::trsv_lower_n_f32(a, h->stream) : rsp_k::trsv_lower_n_f32(a, h->stream));
+    } else if (op == RSP_OPERATION_TRANSPOSE) {
+        a.level_rows = f->d_rows_lt;
+        a.level_ptr_host = f->lev_lt.data();
+        a.nlev = (int)f->lev_lt.size() - 1;
+        e = f64 ? rsp_k::trsv_lower_t_f64(a, h->stream)
+                : (ftz ? rsp_k_ftz::trsv_lower_t_f32(a, h->stream) : rsp_k::trsv_lower_t_f32(a, h->stream));
+    } else {
+        return RSP_STATUS_INVALID_VALUE;
+    }
+    return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f,
+                            rsp_datatype_t value_type, const void *d_values, const void *d_x,
+                            void *d_y) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!f || !f->analysed || !alpha) return RSP_STATUS_INVALID_VALUE;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
+    rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
+    a.level_rows = f->d_rows_u;
+    a.level_ptr_host = f->lev_u.data();
+    a.nlev = (int)f->lev_u.size() - 1;
+    hipError_t e;
+    if (value_type == RSP_R_64F)
+        e = rsp_k::trsv_upper_f64(a, h->stream);
+    else
+        e = h->ftz ? rsp_k_ftz::trsv_upper_f32(a, h->stream) : rsp_k::trsv_upper_f32(a, h->stream);
+    return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+}  // extern "C"

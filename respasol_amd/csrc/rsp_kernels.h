@@ -1,0 +1,107 @@
+// rsp_kernels.h — internal interface between the C-ABI (rsp_api.cpp) and the
+// HIP kernel translation units. The kernel TUs are compiled twice: once as
+// namespace rsp_k (IEEE fp32 denormals) and once with
+// -fgpu-flush-denormals-to-zero as namespace rsp_k_ftz (the `-ftz=true`
+// build of GPU/Makefile:5). fp64 never flushes, so the FTZ namespace carries
+// fp32 entry points only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsp {
+
+// One entry of the SpMV schedule (built by rsp_spmv_preprocess).
+//   r1 >= 0 : rows [r0, r1) whose entries [k0, k1) fit one workgroup tile;
+//   r1 <  0 : chunk [k0, k1) of long row r0; its partial sum goes to
+//             partials[-(r1 + 1)] and the fixup kernel finishes the row.
+struct alignas(16) SpmvBlock {
+    int r0, r1, k0, k1;
+};
+
+// Long row: partial slots [first, first + nchunks) belong to `row`.
+struct alignas(16) SpmvLongRow {
+    int row, first, nchunks, pad;
+};
+
+// Tile geometry shared by the planner and the kernels.
+constexpr int kSpmvThreads = 256;
+constexpr int kSpmvIter = 4;        // vectors per thread per tile
+constexpr int kSpmvMaxRows = 1024;  // rows per tile (bounds the reduce loop)
+template <typename T>
+struct SpmvTile {
+    static constexpr int kVec = 16 / sizeof(T);                           // 16-B loads
+    static constexpr int kSlots = kSpmvThreads * kSpmvIter * kVec;        // LDS products
+    static constexpr int kMaxNnz = kSlots - (kVec - 1);                   // any alignment fits
+};
+
+struct SpmvArgs {
+    int m;
+    const int *rowptr;
+    const int *colidx;
+    const void *vals;
+    const void *x;
+    void *y;
+    const SpmvBlock *blocks;
+    int nblocks;
+    const SpmvLongRow *longrows;
+    int nlong;
+    void *partials;
+    double alpha, beta;
+    int vector_ok;  // rowptr/colidx/vals 16-B aligned -> vector loads
+};
+
+struct IluArgs {
+    int n;
+    const int *rowptr;
+    const int *colidx;
+    const int *dpos;      // first position with col >= row
+    const int *hasdiag;   // 1 if colidx[dpos[i]] == i
+    void *vals;
+    int *zero_pivot;      // device int, atomicMin target (INT_MAX = none)
+    const int *level_rows;        // rows grouped by level (L DAG)
+    const int *level_ptr_host;    // nlev + 1 offsets, HOST memory
+    int nlev;
+};
+
+struct TrsvArgs {
+    int n;
+    const int *rowptr;
+    const int *colidx;
+    const int *dpos;
+    const int *hasdiag;
+    const void *vals;
+    const void *x;
+    void *y;
+    double alpha;
+    // transposed strict-lower map (op == T): row i lists l_ji for j > i,
+    // j descending: lt_ptr[n+1], lt_src (positions in vals), lt_col (j).
+    const int *lt_ptr;
+    const int *lt_src;
+    const int *lt_col;
+    const int *level_rows;
+    const int *level_ptr_host;
+    int nlev;
+};
+
+}  // namespace rsp
+
+#define RSP_DECLARE_KERNEL_API(NS)                                                              \
+    namespace NS {                                                                              \
+    hipError_t spmv_f32(const rsp::SpmvArgs &a, hipStream_t s);                                 \
+    hipError_t ilu0_factor_f32(const rsp::IluArgs &a, hipStream_t s);                           \
+    hipError_t trsv_lower_n_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
+    hipError_t trsv_lower_t_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
+    hipError_t trsv_upper_f32(const rsp::TrsvArgs &a, hipStream_t s);                           \
+    }
+
+RSP_DECLARE_KERNEL_API(rsp_k)
+RSP_DECLARE_KERNEL_API(rsp_k_ftz)
+
+namespace rsp_k {
+hipError_t spmv_f64(const rsp::SpmvArgs &a, hipStream_t s);
+hipError_t ilu0_factor_f64(const rsp::IluArgs &a, hipStream_t s);
+hipError_t trsv_lower_n_f64(const rsp::TrsvArgs &a, hipStream_t s);
+hipError_t trsv_lower_t_f64(const rsp::TrsvArgs &a, hipStream_t s);
+hipError_t trsv_upper_f64(const rsp::TrsvArgs &a, hipStream_t s);
+}  // namespace rsp_k

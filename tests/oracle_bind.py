@@ -1,0 +1,140 @@
+"""ctypes binding of oracle/build/liboracle.so — the CPU restatement used as
+the parity checker (TEST INFRASTRUCTURE ONLY; see oracle/rsp_oracle.h)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+REF_DUMP = os.path.join(ORACLE_DIR, "_ref", "ref_dump")
+FIXTURES = os.path.join(ROOT, "tests", "golden", "mtx")
+
+
+def _load():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+    lib = C.CDLL(ORACLE_SO)
+    ip, vp = C.POINTER(C.c_int), C.c_void_p
+    for name in ("oracle_spmv_f64", "oracle_spmv_f32", "oracle_spmv_f32_ftz", "oracle_spmv_f64_omp",
+                 "oracle_spmv_f32_omp"):
+        getattr(lib, name).argtypes = [C.c_int, ip, ip, vp, vp, vp]
+        getattr(lib, name).restype = None
+    lib.oracle_num_threads.restype = C.c_int
+    lib.oracle_ilu0_f64.argtypes = [C.c_int, ip, ip, vp, ip]
+    lib.oracle_ilu0_f64.restype = C.c_int
+    lib.oracle_ilu0_f32.argtypes = [C.c_int, ip, ip, vp, ip, C.c_int]
+    lib.oracle_ilu0_f32.restype = C.c_int
+    for n in ("lower_n", "lower_t", "upper"):
+        f = getattr(lib, f"oracle_trsv_{n}_f64")
+        f.argtypes = [C.c_int, ip, ip, vp, C.c_double, vp, vp]
+        f.restype = None
+        f = getattr(lib, f"oracle_trsv_{n}_f32")
+        f.argtypes = [C.c_int, ip, ip, vp, C.c_float, vp, vp, C.c_int]
+        f.restype = None
+    lib.oracle_dlarnv.argtypes = [C.c_int, ip, C.c_int, vp]
+    lib.oracle_dlarnv.restype = C.c_int
+    return lib
+
+
+lib = _load()
+
+
+def _i(a):
+    return np.ascontiguousarray(a, np.int32).ctypes.data_as(C.POINTER(C.c_int))
+
+
+def spmv(rowptr, colidx, vals, x, ftz=False, threads=False):
+    rp = np.ascontiguousarray(rowptr, np.int32)
+    ci = np.ascontiguousarray(colidx, np.int32)
+    v = np.ascontiguousarray(vals)
+    xx = np.ascontiguousarray(x, v.dtype)
+    m = rp.shape[0] - 1
+    y = np.empty(m, v.dtype)
+    if v.dtype == np.float64:
+        fn = lib.oracle_spmv_f64_omp if threads else lib.oracle_spmv_f64
+    else:
+        fn = lib.oracle_spmv_f32_ftz if ftz else (lib.oracle_spmv_f32_omp if threads else lib.oracle_spmv_f32)
+    fn(m, rp.ctypes.data_as(C.POINTER(C.c_int)), ci.ctypes.data_as(C.POINTER(C.c_int)),
+       v.ctypes.data, xx.ctypes.data, y.ctypes.data)
+    return y
+
+
+def ilu0(rowptr, colidx, vals, ftz=False):
+    """Returns (factored values, structural_zero or -1, zero_pivot or -1)."""
+    rp = np.ascontiguousarray(rowptr, np.int32)
+    ci = np.ascontiguousarray(colidx, np.int32)
+    v = np.array(vals, copy=True)
+    n = rp.shape[0] - 1
+    zp = C.c_int(-1)
+    if v.dtype == np.float64:
+        s = lib.oracle_ilu0_f64(n, rp.ctypes.data_as(C.POINTER(C.c_int)),
+                                ci.ctypes.data_as(C.POINTER(C.c_int)), v.ctypes.data, C.byref(zp))
+    else:
+        s = lib.oracle_ilu0_f32(n, rp.ctypes.data_as(C.POINTER(C.c_int)),
+                                ci.ctypes.data_as(C.POINTER(C.c_int)), v.ctypes.data, C.byref(zp),
+                                1 if ftz else 0)
+    return v, s, zp.value
+
+
+def trsv(kind, rowptr, colidx, vals, x, alpha=1.0, ftz=False):
+    """kind in {'lower_n', 'lower_t', 'upper'}."""
+    rp = np.ascontiguousarray(rowptr, np.int32)
+    ci = np.ascontiguousarray(colidx, np.int32)
+    v = np.ascontiguousarray(vals)
+    xx = np.ascontiguousarray(x, v.dtype)
+    n = rp.shape[0] - 1
+    y = np.empty(n, v.dtype)
+    if v.dtype == np.float64:
+        getattr(lib, f"oracle_trsv_{kind}_f64")(n, rp.ctypes.data_as(C.POINTER(C.c_int)),
+                                                ci.ctypes.data_as(C.POINTER(C.c_int)), v.ctypes.data,
+                                                alpha, xx.ctypes.data, y.ctypes.data)
+    else:
+        getattr(lib, f"oracle_trsv_{kind}_f32")(n, rp.ctypes.data_as(C.POINTER(C.c_int)),
+                                                ci.ctypes.data_as(C.POINTER(C.c_int)), v.ctypes.data,
+                                                alpha, xx.ctypes.data, y.ctypes.data, 1 if ftz else 0)
+    return y
+
+
+def dlarnv(idist, seed, n):
+    s = (C.c_int * 4)(*seed)
+    x = np.empty(n, np.float64)
+    assert lib.oracle_dlarnv(idist, s, n, x.ctypes.data) == 0
+    return x, list(s)
+
+
+def spmv_bound(rowptr, colidx, vals, x, eps):
+    """|dy_i| <= (len_i + 2) * eps * sum_j |a_ij x_j|."""
+    rp = np.asarray(rowptr, np.int64)
+    lens = np.diff(rp)
+    absprod = np.abs(np.asarray(vals, np.float64)) * np.abs(np.asarray(x, np.float64)[colidx])
+    rowsum = np.add.reduceat(absprod, rp[:-1]) if absprod.size else np.zeros(len(lens))
+    rowsum = np.where(lens > 0, rowsum, 0.0)
+    return (lens + 2) * eps * rowsum
+
+
+def read_ref_dump(path):
+    b = open(path, "rb").read()
+    h = np.frombuffer(b[:24], np.int32)
+    ok, sym, m, n, nnz, stored = (int(v) for v in h)
+    o = 24
+    rp = np.frombuffer(b[o:o + 4 * (m + 1)], np.int32) if ok else None
+    o += 4 * (m + 1) if ok else 0
+    ci = np.frombuffer(b[o:o + 4 * stored], np.int32) if ok else None
+    o += 4 * stored if ok else 0
+    va = np.frombuffer(b[o:o + 8 * stored], np.float64) if ok else None
+    return dict(ok=ok, sym=sym, m=m, n=n, nnz=nnz, stored=stored, rowptr=rp, colidx=ci, values=va)
+
+
+def ref_load(path, base=0, transpose=0, tmpdir="/tmp"):
+    """Run the reference loader (oracle/_ref/ref_dump) — container only."""
+    out = os.path.join(tmpdir, f"refdump_{os.getpid()}.bin")
+    subprocess.run([REF_DUMP, path, str(base), str(transpose), out], check=True,
+                   capture_output=True)
+    d = read_ref_dump(out)
+    os.remove(out)
+    return d

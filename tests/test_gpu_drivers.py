@@ -1,0 +1,104 @@
+"""The reference-CLI drivers on the GPU (respasol_amd/bin): output format of
+GPU/spmv.cu:202-207,260 and GPU/ilu0.cu:221-226,312-317, results checked
+against the oracle; plus the multi-partition SpMV on one GPU (the N>1
+data path without the collective: every rank's slice computed by the HIP
+kernel on the padded x must reassemble the single-GPU y bitwise)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_bind as ob
+from respasol_amd import csr
+from respasol_amd.dist import padded_layout, remap_columns, unpad
+from respasol_amd.sparse import Handle, SpMat, upload_csr
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "respasol_amd", "bin")
+MTX = os.path.join(ROOT, "tests", "golden", "mtx")
+FLOAT = r"[-+]?\d+\.\d+"
+
+
+def run(*args):
+    r = subprocess.run([os.path.join(BIN, args[0]), *args[1:]], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+@pytest.mark.parametrize("name", ["b1_ss", "bcspwr01", "one"])
+def test_spmv_driver_reference_format(name):
+    out = run("test_spmv", os.path.join(MTX, name + ".mtx"))
+    lines = out.splitlines()
+    assert re.fullmatch(rf"DOUBLE PRECISION SPMV solve time \(microseconds\) = {FLOAT}", lines[0])
+    m = re.fullmatch(r"Error= (\S+)", lines[1])
+    assert m and float(m.group(1)) == 0.0  # GPU y == host y on the fixtures
+    assert len(lines) == 2
+
+
+def test_spmv_driver_fp32_ftz_both_and_stats():
+    out = run("spmv", "surrogate:Serena@0.05", "--prec=both", "--ftz", "--batched", "--stats",
+              "--reps=20")
+    assert "DOUBLE PRECISION SPMV solve time (microseconds) = " in out
+    assert "SINGLE PRECISION SPMV solve time (microseconds) = " in out
+    assert "batched time" in out and "STATS" in out
+    for e in re.findall(r"Error= (\S+)", out):
+        assert float(e) < 1e-5
+
+
+def test_ilu0_driver_reference_format():
+    out = run("test_ilu0", os.path.join(MTX, "bcspwr01.mtx"))
+    pat = (rf"DOUBLE PRECISION SOLVE IN  MILLISECONDS\n Symbolic = {FLOAT}\n Numeric = {FLOAT} \n"
+           rf" Symbolic\+ Numeric = {FLOAT}\n Solve = {FLOAT}\n")
+    assert re.fullmatch(pat, out), out
+
+
+def test_ilu0_driver_structural_zero_exit0():
+    out = run("ilu0", os.path.join(MTX, "b1_ss.mtx"))
+    assert out == "A(0,0) is missing\n"
+
+
+def test_ilu0_driver_dump_matches_oracle(tmp_path):
+    dump = tmp_path / "y.bin"
+    out = run("test_ilu0", "surrogate:thermomech_TK@0.2", "--prec=fp32", "--ftz", f"--dump={dump}")
+    assert out.startswith("SINGLE PRECISION SOLVE IN  MILLISECONDS\n")
+    y = np.fromfile(dump, np.float32)
+    A = csr.surrogate("thermomech_TK", 0.2)
+    v, _, _ = ob.ilu0(A.rowptr, A.colidx, A.values.astype(np.float32), ftz=True)
+    z = ob.trsv("lower_n", A.rowptr, A.colidx, v, np.ones(A.n, np.float32), ftz=True)
+    ref = ob.trsv("lower_t", A.rowptr, A.colidx, v, z, ftz=True)
+    assert np.array_equal(y, ref)
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+def test_partitioned_spmv_single_gpu(P):
+    """Each of P row slices (rank-local surrogate rows, padded column remap)
+    through the HIP kernel; reassembled y == single-GPU y, bitwise."""
+    name, scale = "Hook_1498", 0.05
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    h = Handle()
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
+    y_full = SpMat(h, rp, ci, va, A.n).spmv(torch.from_numpy(x).cuda()).cpu().numpy()
+    bounds = csr.partition_rows(A.rowptr, P)
+    chunk, pos = padded_layout(bounds)
+    x_pad = np.zeros(P * chunk)
+    x_pad[pos] = x
+    xd = torch.from_numpy(x_pad).cuda()
+    ys = []
+    for p in range(P):
+        r0, r1 = int(bounds[p]), int(bounds[p + 1])
+        lrp, lci, lva = csr.surrogate_rows_csr(name, r0, r1, scale)
+        lci_pad, _ = remap_columns(lci, bounds)
+        d = upload_csr(lrp, lci_pad, lva)
+        yp = SpMat(h, *d, P * chunk).spmv(xd)
+        buf = torch.zeros(chunk, dtype=torch.float64, device="cuda")
+        buf[: r1 - r0] = yp
+        ys.append(buf)
+    y = unpad(torch.cat(ys), bounds, chunk).cpu().numpy()
+    assert np.array_equal(y, y_full)
+    h.close()

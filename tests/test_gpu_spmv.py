@@ -1,0 +1,192 @@
+"""GPU parity of the HIP CSR SpMV (librsp.so through the C-ABI) against the
+CPU oracle, on the reference fixtures, surrogates of every structural family
+(including circuit matrices with rows longer than one tile), edge cases and
+full BASELINE-size matrices.
+
+Tolerance: |y_i - y_oracle_i| <= (len_i + 2) * u * sum_j |a_ij x_j|
+with u = 2^-53 (fp64) / 2^-24 (fp32). Rows reduced by a single lane (the
+common short-row case) are summed in the oracle's order and match bitwise;
+the test also asserts run-to-run bitwise determinism."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_bind as ob
+from respasol_amd import csr
+from respasol_amd.sparse import Handle, SpMat, upload_csr
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mtx")
+EPS = {torch.float64: 2.0 ** -53, torch.float32: 2.0 ** -24}
+NP = {torch.float64: np.float64, torch.float32: np.float32}
+
+
+@pytest.fixture(scope="module")
+def handle():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    h = Handle()
+    yield h
+    h.close()
+
+
+def run_gpu(handle, A, x, dtype, ftz=False, alpha=1.0, beta=0.0, y0=None):
+    handle.set_ftz(ftz)
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values, dtype)
+    mat = SpMat(handle, rp, ci, va, A.n, nnz=max(A.nnz, A.nnz_stored))
+    xd = torch.from_numpy(np.ascontiguousarray(x, NP[dtype])).cuda()
+    y = torch.from_numpy(np.ascontiguousarray(y0, NP[dtype])).cuda() if y0 is not None else None
+    out = mat.spmv(xd, y, alpha, beta)
+    torch.cuda.synchronize()
+    res = out.cpu().numpy()
+    out2 = mat.spmv(xd, None, alpha, 0.0) if beta == 0.0 else None
+    torch.cuda.synchronize()
+    handle.set_ftz(False)
+    return res, (out2.cpu().numpy() if out2 is not None else None), mat
+
+
+def check(A, x, dtype, handle, ftz=False):
+    y, y2, mat = run_gpu(handle, A, x, dtype, ftz)
+    v = A.values.astype(NP[dtype])
+    ref = ob.spmv(A.rowptr, A.colidx, v, x.astype(NP[dtype]), ftz=ftz)
+    bound = ob.spmv_bound(A.rowptr, A.colidx, v, x.astype(NP[dtype]), EPS[dtype])
+    err = np.abs(y.astype(np.float64) - ref.astype(np.float64))
+    assert np.all(err <= bound), f"max excess {np.max(err - bound)}"
+    assert np.array_equal(y, y2), "not deterministic"
+    return y, ref
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("name", ["b1_ss", "bcspwr01", "one"] + [
+    "sym_lower", "unsorted_dups", "empty_rows", "rect", "random_300", "pattern_general", "zero_based"])
+def test_fixtures(handle, name, dtype):
+    A = csr.load_matrix_market(os.path.join(GOLD, name + ".mtx"))
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    y, ref = check(A, x, dtype, handle)
+    if name == "one":
+        assert np.array_equal(y, x.astype(NP[dtype]))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("name,scale", [
+    ("2cubes_sphere", 0.2), ("ASIC_320ks", 0.2), ("dc1", 0.3), ("G2_circuit", 0.3),
+    ("ecology2", 0.05), ("crashbasis", 0.2), ("para-10", 0.2), ("ss1", 0.2), ("cage13", 0.05),
+    ("ML_Laplace", 0.05), ("Si87H76", 0.1), ("matrix-new_3", 0.3)])
+def test_surrogates(handle, name, scale, dtype):
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+    check(A, x, dtype, handle)
+
+
+def test_long_rows_exercised(handle):
+    """ASIC_320ks has hub rows far longer than one tile (fp64 2047 / fp32 4093
+    entries): they take the chunked path + fixup kernel."""
+    A = csr.surrogate("ASIC_320ks")
+    assert np.diff(A.rowptr).max() > 4093
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    for dt in (torch.float64, torch.float32):
+        check(A, x, dt, handle)
+
+
+def test_single_dense_row_and_column(handle):
+    n = 10000
+    rows = [np.arange(n, dtype=np.int32)]  # row 0 dense
+    rp = [0, n]
+    cols = [np.arange(n, dtype=np.int32)]
+    for i in range(1, n):
+        cols.append(np.array([0, i], np.int32))  # column 0 dense
+        rp.append(rp[-1] + 2)
+    ci = np.concatenate(cols)
+    rng = np.random.default_rng(3)
+    A = csr.CsrMatrix(0, n, n, len(ci), np.array(rp, np.int32), ci, rng.uniform(-1, 1, len(ci)))
+    x = rng.uniform(-1, 1, n)
+    for dt in (torch.float64, torch.float32):
+        check(A, x, dt, handle)
+    del rows
+
+
+def test_empty_and_tiny(handle):
+    # all-empty rows
+    A = csr.CsrMatrix(0, 5, 5, 0, np.zeros(6, np.int32), np.zeros(0, np.int32), np.zeros(0))
+    y, _, _ = run_gpu(handle, A, np.ones(5), torch.float64)
+    assert np.array_equal(y, np.zeros(5))
+    # 1 x 1
+    A = csr.CsrMatrix(0, 1, 1, 1, np.array([0, 1], np.int32), np.array([0], np.int32), np.array([2.5]))
+    y, _, _ = run_gpu(handle, A, np.array([4.0]), torch.float64)
+    assert y.tolist() == [10.0]
+
+
+def test_alpha_beta(handle):
+    A = csr.surrogate("cfd2", 0.05)
+    rng = np.random.default_rng(1)
+    x = rng.uniform(-1, 1, A.n)
+    y0 = rng.uniform(-1, 1, A.m)
+    y, _, _ = run_gpu(handle, A, x, torch.float64, alpha=2.0, beta=-0.5, y0=y0)
+    ref = 2.0 * ob.spmv(A.rowptr, A.colidx, A.values, x) - 0.5 * y0
+    assert np.allclose(y, ref, rtol=1e-14, atol=1e-13)
+    # beta == 0 must not read y (NaN in y is ignored, cuSPARSE semantics)
+    y, _, _ = run_gpu(handle, A, x, torch.float64, beta=0.0, y0=np.full(A.m, np.nan))
+    assert np.all(np.isfinite(y))
+
+
+def test_unaligned_pointers_scalar_path(handle):
+    """vals/colidx views starting at an odd element disable the 16-B vector
+    loads; the scalar instantiation must give the same result."""
+    A = csr.surrogate("offshore", 0.05)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    ci = torch.zeros(A.nnz_stored + 1, dtype=torch.int32, device="cuda")
+    va = torch.zeros(A.nnz_stored + 1, dtype=torch.float64, device="cuda")
+    ci[1:] = torch.from_numpy(A.colidx).cuda()
+    va[1:] = torch.from_numpy(A.values).cuda()
+    rp = torch.from_numpy(A.rowptr).cuda()
+    mat = SpMat(handle, rp, ci[1:], va[1:], A.n)
+    y = mat.spmv(torch.from_numpy(x).cuda()).cpu().numpy()
+    ref = ob.spmv(A.rowptr, A.colidx, A.values, x)
+    assert np.all(np.abs(y - ref) <= ob.spmv_bound(A.rowptr, A.colidx, A.values, x, EPS[torch.float64]))
+
+
+def test_ftz_flushes_subnormal_products(handle):
+    """fp32 + FTZ (nvcc -ftz=true, GPU/Makefile:5): subnormal inputs/products
+    are zero; without FTZ they survive. Both match the oracle bitwise."""
+    rp = np.array([0, 2, 3], np.int32)
+    ci = np.array([0, 1, 1], np.int32)
+    vals = np.array([1e-39, 2e-39, 1e-20], np.float64)
+    A = csr.CsrMatrix(0, 2, 2, 3, rp, ci, vals)
+    x = np.array([1.0, 1e-20])
+    y_ieee, _, _ = run_gpu(handle, A, x, torch.float32, ftz=False)
+    y_ftz, _, _ = run_gpu(handle, A, x, torch.float32, ftz=True)
+    v32, x32 = vals.astype(np.float32), x.astype(np.float32)
+    assert np.array_equal(y_ieee, ob.spmv(rp, ci, v32, x32))
+    assert np.array_equal(y_ftz, ob.spmv(rp, ci, v32, x32, ftz=True))
+    assert y_ieee[0] != 0 and y_ftz[0] == 0 and y_ftz[1] == 0
+
+
+def test_ftz_stress_surrogate(handle):
+    from respasol_amd._lib import SURR_FTZ_STRESS
+    A = csr.surrogate("cfd2", 0.1, flags=SURR_FTZ_STRESS)
+    x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+    check(A, x, torch.float32, handle, ftz=True)
+
+
+@pytest.mark.parametrize("name", ["Serena", "ML_Laplace", "Transport"])
+def test_full_size_big_set(handle, name):
+    """BASELINE config 4 sizes (full surrogate) fp64 against the oracle, plus
+    linearity A(2x + z) = 2Ax + Az as a size-independent property."""
+    A = csr.surrogate(name)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    y, ref = check(A, x, torch.float64, handle)
+    z, _ = csr.dlarnv(1, [1, 2, 3, 5], A.n)
+    yz, _, _ = run_gpu(handle, A, z, torch.float64)
+    ylin, _, _ = run_gpu(handle, A, 2 * x + z, torch.float64)
+    assert np.allclose(ylin, 2 * y + yz, rtol=1e-12, atol=1e-10)
+
+
+def test_invalid_inputs_are_status_codes(handle):
+    from respasol_amd import RspError
+    rp = torch.tensor([0, 2], dtype=torch.int32, device="cuda")
+    ci = torch.tensor([0, 7], dtype=torch.int32, device="cuda")  # column 7 >= n = 2
+    va = torch.ones(2, dtype=torch.float64, device="cuda")
+    with pytest.raises(RspError) as e:
+        SpMat(handle, rp, ci, va, 2)
+    assert e.value.status == 3

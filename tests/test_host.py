@@ -1,0 +1,169 @@
+"""Host-side product logic that needs no GPU: the C-ABI libraries load and
+export every symbol declared in include/*.h, the surrogate generator's
+contracts, the row partitioner, and the CPU reference-CLI driver."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from respasol_amd import _lib, csr
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+BIN = os.path.join(ROOT, "respasol_amd", "bin")
+
+
+def header_functions(path):
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    return sorted(set(re.findall(r"\b([A-Za-z_]\w*)\s*\(", text)) - {
+        "if", "sizeof", "defined", "return", "while", "for"} - {"extern"})
+
+
+@pytest.mark.parametrize("header,lib,protos", [
+    ("rsp.h", "rsp", _lib.RSP_PROTOS), ("rsp_host.h", "host", _lib.HOST_PROTOS)])
+def test_every_declared_symbol_is_exported_and_bound(header, lib, protos):
+    funcs = [f for f in header_functions(os.path.join(ROOT, "include", header))
+             if f.startswith(("rsp_", "load"))]
+    assert funcs, header
+    L = getattr(_lib, lib)
+    for f in funcs:
+        assert hasattr(L, f), f"{f} declared in {header} but not exported"
+        assert f in protos, f"{f} has no ctypes prototype"
+    assert set(protos) <= set(funcs)
+
+
+def test_native_version_and_error_strings():
+    import respasol_amd
+    assert respasol_amd.native_version() == 1
+    assert _lib.rsp.rsp_get_error_string(9) == b"RSP_STATUS_ZERO_PIVOT"
+
+
+def test_library_has_gfx950_code_object():
+    so = os.path.join(_lib.LIB_DIR, "librsp.so")
+    blob = open(so, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"gfx90a" not in blob  # gfx950 only
+
+
+# ------------------------------------------------------------ surrogates
+
+@pytest.mark.parametrize("name", ["Serena", "ASIC_320ks", "G2_circuit", "ecology2", "cage13",
+                                  "ML_Laplace", "af_shell2", "Si87H76"])
+def test_surrogate_contract(name):
+    info = csr.surrogate_info(name)
+    A = csr.surrogate(name, 0.02)
+    rows = np.repeat(np.arange(A.m), np.diff(A.rowptr))
+    # sorted, unique columns per row; diagonal present
+    d = np.diff(A.colidx)
+    newrow = np.diff(rows) != 0
+    assert np.all((d > 0) | newrow)
+    diag = A.colidx == rows
+    assert np.bincount(rows[diag], minlength=A.m).min() == 1
+    if info["symmetric"]:
+        assert np.all(A.colidx <= rows)
+    # strict row diagonal dominance over the stored row
+    absrow = np.bincount(rows, weights=np.abs(A.values), minlength=A.m)
+    assert np.all(A.values[diag] * 2 > absrow)
+    # row-local: any slice equals the same rows of the whole matrix
+    r0, r1 = A.m // 3, A.m // 3 + A.m // 4
+    rp, ci, va = csr.surrogate_rows_csr(name, r0, r1, 0.02)
+    s, e = A.rowptr[r0], A.rowptr[r1]
+    assert np.array_equal(rp, A.rowptr[r0:r1 + 1] - s)
+    assert np.array_equal(ci, A.colidx[s:e])
+    assert np.array_equal(va, A.values[s:e])
+
+
+def test_surrogate_sizes_match_catalog():
+    for name in csr.surrogate_names():
+        info = csr.surrogate_info(name)
+        lens = csr.surrogate_rowlens(name)
+        assert len(lens) == info["m"]
+        assert abs(int(lens.sum()) - info["nnz_target"]) <= 1e-3 * info["nnz_target"], name
+    assert len(csr.surrogate_names(0)) == 21 and len(csr.surrogate_names(1)) == 15
+
+
+def test_surrogate_ftz_stress_has_fp32_subnormals():
+    A = csr.surrogate("cfd2", 0.02, flags=_lib.SURR_FTZ_STRESS)
+    v32 = A.values.astype(np.float32)
+    sub = (v32 != 0) & (np.abs(v32) < np.finfo(np.float32).tiny)
+    assert sub.sum() > 0
+
+
+def test_custom_surrogate_spec():
+    A = csr.surrogate("stencil3d:1000:7000:G")
+    assert A.m == 1000 and abs(A.nnz_stored - 7000) < 100
+
+
+# ------------------------------------------------------------ partition
+
+def test_partition_rows_balanced():
+    A = csr.surrogate("ASIC_320ks", 0.05)
+    for P in (1, 2, 3, 4, 8):
+        b = csr.partition_rows(A.rowptr, P)
+        assert b[0] == 0 and b[-1] == A.m and np.all(np.diff(b) >= 0)
+        nnz = A.rowptr[b[1:]] - A.rowptr[b[:-1]]
+        assert nnz.sum() == A.nnz_stored
+        assert nnz.max() <= A.nnz_stored / P + np.diff(A.rowptr).max()
+    b = csr.partition_rows(np.array([0, 1, 2], np.int32), 4)  # P > m
+    assert b.tolist()[0] == 0 and b.tolist()[-1] == 2
+
+
+# ------------------------------------------------------------ CPU driver
+
+def test_cpu_driver_csv_schema(tmp_path):
+    out = tmp_path / "bench.csv"
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    for f in ("b1_ss", "bcspwr01", "one"):
+        r = subprocess.run([os.path.join(BIN, "test_spmv_cpu"), os.path.join(GOLD, "mtx", f + ".mtx"),
+                            str(out)], env=env, capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+    r = subprocess.run([os.path.join(BIN, "test_spmv_cpu"),
+                        os.path.join(tmp_path, "matrix-new_3.mtx"), str(out)], env=env,
+                       capture_output=True, text=True)
+    assert r.returncode != 0  # missing file exits non-zero (reference: exit(-1))
+    lines = out.read_text().splitlines()
+    assert len(lines) == 4
+    for line, name in zip(lines, ("b1_ss", "bcspwr01", "one")):
+        f = line.split(",")
+        assert f[0] == "2" and f[1] == name and f[-1] == ""
+        float(f[2]), float(f[3])
+        assert float(f[4]) < 1e-6  # fp32-vs-fp64 mean difference
+    # the missing-file run wrote only the thread field before exiting
+    assert lines[3] == "2,"
+
+
+def test_cpu_driver_name_regex(tmp_path):
+    # (\w+)\.mtx keeps only the word run: matrix-new_3 -> new_3 (test_spmv.c:57-62)
+    src = os.path.join(GOLD, "mtx", "one.mtx")
+    dst = tmp_path / "matrix-new_3.mtx"
+    dst.write_text(open(src).read())
+    out = tmp_path / "o.csv"
+    subprocess.run([os.path.join(BIN, "test_spmv_cpu"), str(dst), str(out)], check=True,
+                   env=dict(os.environ, OMP_NUM_THREADS="1"), capture_output=True)
+    assert out.read_text().split(",")[1] == "new_3"
+
+
+def test_cpu_driver_error_matches_oracle(tmp_path):
+    """err column = mean |y64 - y32| with x = dlarnv(1,{0,0,0,1}) (test_spmv.c:200-208)."""
+    out = tmp_path / "o.csv"
+    spec = "surrogate:cfd2@0.05"
+    subprocess.run([os.path.join(BIN, "test_spmv_cpu"), spec, str(out)], check=True,
+                   env=dict(os.environ, OMP_NUM_THREADS="3"), capture_output=True)
+    err = float(out.read_text().split(",")[4])
+    A = csr.surrogate("cfd2", 0.05)
+    x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+    y64 = ob.spmv(A.rowptr, A.colidx, A.values, x)
+    y32 = ob.spmv(A.rowptr, A.colidx, A.values.astype(np.float32), x.astype(np.float32))
+    ref = np.abs(y64 - y32.astype(np.float64)).mean()
+    assert err == pytest.approx(ref, rel=1e-5)
+
+
+def test_gpu_drivers_usage_without_args():
+    for exe in ("test_spmv", "test_ilu0", "spmv", "ilu0", "test_spmv_cpu"):
+        r = subprocess.run([os.path.join(BIN, exe)], capture_output=True, text=True)
+        assert r.returncode == 255 and "Usage examples" in r.stderr

@@ -1,0 +1,135 @@
+"""Loader parity: respasol_amd's Matrix-Market loader vs the REFERENCE loader
+(ReadMatrixMarket/loadMatrixMarket.cpp:47-253), byte for byte.
+
+* committed dumps of the reference loader (tests/golden/ref_csr, made by
+  tests/golden/make_golden.py from oracle/_ref/ref_dump) — always run;
+* a live differential run against oracle/_ref/ref_dump on randomly generated
+  files — runs where the reference build exists (the build container).
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from respasol_amd import csr
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+MANIFEST = json.load(open(os.path.join(GOLD, "manifest.json")))
+
+
+def _same(A, d):
+    return ((A.is_symmetric, A.m, A.n, A.nnz) == (d["sym"], d["m"], d["n"], d["nnz"])
+            and np.array_equal(A.rowptr, d["rowptr"]) and np.array_equal(A.colidx, d["colidx"])
+            and np.array_equal(A.values.view(np.uint64), d["values"].view(np.uint64)))
+
+
+@pytest.mark.parametrize("entry", MANIFEST, ids=lambda e: f"{e['file']}-b{e['base']}-t{e['transpose']}")
+def test_loader_matches_reference_dump(entry):
+    d = ob.read_ref_dump(os.path.join(GOLD, entry["dump"]))
+    path = os.path.join(GOLD, "mtx", entry["file"])
+    if not d["ok"]:
+        with pytest.raises(csr.LoadError):
+            csr.load_matrix_market(path, entry["base"], entry["transpose"])
+        return
+    A = csr.load_matrix_market(path, entry["base"], entry["transpose"])
+    assert _same(A, d)
+
+
+def test_symmetric_quirk_bcspwr01():
+    """stored triangle only in the CSR, nnz = expanded count."""
+    A = csr.load_matrix_market(os.path.join(GOLD, "mtx", "bcspwr01.mtx"))
+    assert (A.m, A.nnz, A.nnz_stored) == (39, 131, 85)
+    rows = np.repeat(np.arange(A.m), np.diff(A.rowptr))
+    assert np.all(A.colidx <= rows)  # no upper entries
+    assert np.all(A.values == 1.0)   # pattern -> 1.0
+
+
+def test_b1_ss_rows():
+    A = csr.load_matrix_market(os.path.join(GOLD, "mtx", "b1_ss.mtx"))
+    kat = json.load(open(os.path.join(GOLD, "kat.json")))["b1_ss"]
+    r0 = list(zip(A.colidx[A.rowptr[0]:A.rowptr[1]].tolist(), A.values[A.rowptr[0]:A.rowptr[1]].tolist()))
+    r1 = list(zip(A.colidx[A.rowptr[1]:A.rowptr[2]].tolist(), A.values[A.rowptr[1]:A.rowptr[2]].tolist()))
+    assert r0 == [tuple(p) for p in kat["row0"]]
+    assert r1 == [tuple(p) for p in kat["row1"]]
+
+
+def test_full_symmetric_extension():
+    A = csr.load_matrix_market(os.path.join(GOLD, "mtx", "bcspwr01.mtx"), full_symmetric=True)
+    assert A.nnz_stored == A.nnz == 131
+    dense = np.zeros((A.m, A.n))
+    for i in range(A.m):
+        dense[i, A.colidx[A.rowptr[i]:A.rowptr[i + 1]]] = A.values[A.rowptr[i]:A.rowptr[i + 1]]
+    assert np.array_equal(dense, dense.T)
+
+
+def test_loader_errors_and_buffer():
+    with pytest.raises(csr.LoadError) as e:
+        csr.load_matrix_market("/nonexistent/file.mtx")
+    assert e.value.status == 1
+    A = csr.load_matrix_market_text("%%MatrixMarket matrix coordinate real general\n2 2 2\n1 1 3\n2 2 4\n")
+    assert A.rowptr.tolist() == [0, 1, 2] and A.values.tolist() == [3.0, 4.0]
+
+
+def test_row_qsort_matches_reference_order():
+    """Duplicate columns keep the order the reference's quicksort leaves
+    (loadMatrixMarket.cpp:5-26) — pinned through the unsorted_dups dump."""
+    d = ob.read_ref_dump(os.path.join(GOLD, "ref_csr", "unsorted_dups_b0_t0.bin"))
+    A = csr.load_matrix_market(os.path.join(GOLD, "mtx", "unsorted_dups.mtx"))
+    assert np.array_equal(A.values, d["values"])
+    assert np.any(np.diff(A.colidx) == 0)  # the file really has duplicates
+
+
+def _random_mtx(rnd: random.Random) -> str:
+    m, n = rnd.randint(1, 40), rnd.randint(1, 40)
+    field = rnd.choice(["real", "pattern", "integer", "complex"])
+    sym = rnd.choice(["general", "symmetric"]) if field != "complex" else "general"
+    if sym == "symmetric":
+        n = m
+    k = rnd.randint(m + 1, 4 * m + 8)
+    lines = []
+    for _ in range(k):
+        i, j = rnd.randint(1, m), rnd.randint(1, n)
+        if sym == "symmetric" and rnd.random() < 0.85 and j > i:
+            i, j = j, i
+        if field == "pattern":
+            lines.append(f"{i} {j}")
+        elif field == "integer":
+            lines.append(f"{i} {j} {rnd.randint(-999, 999)}")
+        elif field == "complex":
+            lines.append(f"{i} {j} {rnd.uniform(-5, 5):.6e} {rnd.uniform(-1, 1)}")
+        else:
+            lines.append(f"{i} {j} {rnd.uniform(-1e3, 1e3):.17g}")
+    return f"%%MatrixMarket matrix coordinate {field} {sym}\n% random\n{m} {n} {k}\n" + "\n".join(lines) + "\n"
+
+
+@pytest.mark.skipif(not os.path.exists(ob.REF_DUMP), reason="reference loader build (oracle/_ref) not present")
+def test_loader_differential_vs_reference_build(tmp_path):
+    rnd = random.Random(20241218)
+    for t in range(60):
+        p = tmp_path / f"r{t}.mtx"
+        p.write_text(_random_mtx(rnd))
+        for base in (0, 1):
+            tr = t % 2
+            d = ob.ref_load(str(p), base, tr, str(tmp_path))
+            assert d["ok"] == 1
+            A = csr.load_matrix_market(str(p), base, tr)
+            assert _same(A, d), (t, base)
+
+
+def test_binary_cache_roundtrip(tmp_path):
+    import ctypes as C
+    from respasol_amd._lib import CSRStruct, host
+    path = os.path.join(GOLD, "mtx", "bcspwr01.mtx")
+    s = CSRStruct()
+    assert host.rsp_mm_load(path.encode(), C.byref(s), 0, 0, 2) == 0
+    out = str(tmp_path / "c.bin").encode()
+    assert host.rsp_csr_save(out, C.byref(s)) == 0
+    t = CSRStruct()
+    assert host.rsp_csr_load(out, C.byref(t)) == 0
+    assert (t.m, t.n, t.nnz, t.isSymmetric) == (s.m, s.n, s.nnz, s.isSymmetric)
+    assert [t.rowptr[i] for i in range(t.m + 1)] == [s.rowptr[i] for i in range(s.m + 1)]
+    host.rsp_csr_free(C.byref(s))
+    host.rsp_csr_free(C.byref(t))
