@@ -72,6 +72,32 @@ void oracle_spmv_f32_omp(int m, const int *rp, const int *ci, const float *v, co
 
 int oracle_num_threads(void) { return omp_get_max_threads(); }
 
+/* Canonical 8-way order of the GPU tiles (spmv.hip): partial p_j sums the
+ * row's products e = j, j+8, j+16, ... (e counted from the row start) in
+ * increasing e; y = ((p0+p4)+(p2+p6)) + ((p1+p5)+(p3+p7)). The kernels give
+ * this bit-for-bit for every row that fits one tile, whatever the tiling,
+ * lanes-per-row or row partition (rows longer than a tile are chunked and
+ * checked against the bound instead). */
+#define ORACLE_W8(T, NAME)                                                                     \
+    void NAME(int m, const int *rp, const int *ci, const T *v, const T *x, T *y) {             \
+        for (int i = 0; i < m; i++) {                                                          \
+            T p[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                                 \
+            for (int k = rp[i]; k < rp[i + 1]; k++) p[(k - rp[i]) & 7] += v[k] * x[ci[k]];     \
+            for (int h = 4; h >= 1; h >>= 1)                                                   \
+                for (int t = 0; t < h; t++) p[t] = p[t] + p[t + h];                            \
+            y[i] = p[0];                                                                       \
+        }                                                                                      \
+    }
+ORACLE_W8(double, oracle_spmv_w8_f64)
+ORACLE_W8(float, oracle_spmv_w8_f32)
+
+void oracle_spmv_w8_f32_ftz(int m, const int *rp, const int *ci, const float *v, const float *x,
+                            float *y) {
+    unsigned old = ftz_enter(1);
+    oracle_spmv_w8_f32(m, rp, ci, v, x, y);
+    ftz_leave(old);
+}
+
 /* ---------------------------------------------------------------- ILU(0) */
 
 /* first position in row i with column >= i */

@@ -44,6 +44,15 @@ void oracle_spmv_f64_omp(int m, const int *rowptr, const int *colidx, const doub
 void oracle_spmv_f32_omp(int m, const int *rowptr, const int *colidx, const float *vals,
                          const float *x, float *y);
 int oracle_num_threads(void);
+/* Same products, canonical 8-way interleaved summation order (the order the
+ * GPU tiles use): p_j = sum of products e = j (mod 8) from the row start, in
+ * order; y = ((p0+p4)+(p2+p6)) + ((p1+p5)+(p3+p7)). */
+void oracle_spmv_w8_f64(int m, const int *rowptr, const int *colidx, const double *vals,
+                        const double *x, double *y);
+void oracle_spmv_w8_f32(int m, const int *rowptr, const int *colidx, const float *vals,
+                        const float *x, float *y);
+void oracle_spmv_w8_f32_ftz(int m, const int *rowptr, const int *colidx, const float *vals,
+                            const float *x, float *y);
 
 /* In-place ILU(0), IKJ, fma updates (cusparse?csrilu02, GPU/ilu0.cu:264-268).
  * Returns the first structurally missing diagonal (>= 0) without factoring,

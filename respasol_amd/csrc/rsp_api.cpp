@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 #include <limits.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -24,6 +25,7 @@ struct rsp_context {
     int device;
     hipStream_t stream;
     int ftz;
+    int spmv_variant;  // RSP_SPMV_VARIANT (tuning knob, default 0)
 };
 
 struct rsp_spmat {
@@ -36,6 +38,7 @@ struct rsp_spmat {
     const void *plan_buffer;  // buffer the schedule was written into
     rsp_datatype_t plan_type;
     int nblocks, nlong, nslots;
+    int nnz_s;                  // rowptr[rows] seen by the preprocess
     size_t off_long, off_part;  // byte offsets inside the buffer
 };
 
@@ -93,6 +96,8 @@ rsp_status_t rsp_create(rsp_handle_t *handle) {
     c->device = dev;
     c->stream = nullptr;
     c->ftz = 0;
+    const char *v = getenv("RSP_SPMV_VARIANT");
+    c->spmv_variant = v ? atoi(v) : 0;
     *handle = c;
     return RSP_STATUS_SUCCESS;
 }
@@ -324,6 +329,7 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     mat->nblocks = (int)blocks.size();
     mat->nlong = (int)longrows.size();
     mat->nslots = nslots;
+    mat->nnz_s = m > 0 ? rp[(size_t)m] : 0;
     mat->off_long = off_long;
     mat->off_part = off_part;
     return RSP_STATUS_SUCCESS;
@@ -362,6 +368,8 @@ rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp
         a.beta = *(const float *)beta;
     }
     a.vector_ok = ((((uintptr_t)mat->colidx) | ((uintptr_t)mat->vals)) & 15) == 0;
+    a.nnz = mat->nnz_s;
+    a.variant = h->spmv_variant;
     hipError_t e;
     if (compute_type == RSP_R_64F)
         e = rsp_k::spmv_f64(a, h->stream);

@@ -27,7 +27,7 @@ struct alignas(16) SpmvLongRow {
 // Tile geometry shared by the planner and the kernels.
 constexpr int kSpmvThreads = 256;
 constexpr int kSpmvIter = 4;        // vectors per thread per tile
-constexpr int kSpmvMaxRows = 1024;  // rows per tile (bounds the reduce loop)
+constexpr int kSpmvMaxRows = 512;   // rows per tile (row offsets staged in LDS)
 template <typename T>
 struct SpmvTile {
     static constexpr int kVec = 16 / sizeof(T);                           // 16-B loads
@@ -48,7 +48,9 @@ struct SpmvArgs {
     int nlong;
     void *partials;
     double alpha, beta;
-    int vector_ok;  // rowptr/colidx/vals 16-B aligned -> vector loads
+    int nnz;        // rowptr[m]: tiles touching the last partial vector go scalar
+    int vector_ok;  // colidx/vals 16-B aligned -> vector loads
+    int variant;    // bit 0: non-temporal vals/colidx loads
 };
 
 struct IluArgs {

@@ -5,17 +5,20 @@
 // Schedule ("row-block" tiles, built on the host by rsp_spmv_preprocess):
 // consecutive rows are packed into tiles of at most SpmvTile<T>::kMaxNnz
 // entries (<= kSpmvMaxRows rows); one 256-thread workgroup per tile.
-//   1. stream: every thread issues kSpmvIter 16-byte loads of colidx and vals
-//      (fully coalesced, 1 KiB per wave-instruction for vals), gathers
-//      x[col] and writes the products into LDS (16 KiB per tile);
-//   2. reduce: L = 1..64 lanes per row (power of two chosen from the tile's
-//      rows and average row length) sum the row's products from LDS and
-//      combine with wave shuffles; lane 0 writes y.
-// Rows longer than a tile are split into tile-sized chunks whose partial sums
-// a tiny fixup kernel adds in chunk order. Every summation order is fixed, so
-// results are bitwise reproducible run to run (cuSPARSE ALG_DEFAULT is not).
-// With L == 1 (the common case for short rows) each row is summed
-// sequentially in column order, i.e. bit-identical to the CPU oracle.
+//   1. stream: each thread issues all of its 16-byte colidx/vals loads for
+//      the tile back to back (predicated, no per-element branches, so every
+//      load is in flight before the first wait), then all its x[col] gathers,
+//      then writes the products into LDS (16 KiB per tile);
+//   2. reduce: L = 1, 2, 4 or 8 lanes per row sum the row's products from
+//      LDS in the CANONICAL 8-WAY ORDER — partial p_j adds the products
+//      e = j, j+8, ... (e counted from the row start) in order, then
+//      y = ((p0+p4)+(p2+p6)) + ((p1+p5)+(p3+p7)) — which every L realises
+//      exactly (local tree stages for offsets >= L, shuffles below). So y is
+//      bitwise independent of how rows are packed into tiles or split over
+//      GPUs, and equal to the oracle's oracle_spmv_w8_* bit for bit.
+// Rows longer than a tile are cut into tile-sized chunks (relative to the row
+// start); each chunk is reduced by all 256 threads in a fixed tree and a tiny
+// fixup kernel adds the chunk partials in order. Everything is deterministic.
 //
 // Roofline: HBM-bound, no MFMA (no dense contraction). Algorithmic bytes per
 // call: (sizeof(T)+4)*nnz_s + 4*(m+1) + sizeof(T)*(n + m) (+ sizeof(T)*m if
@@ -34,12 +37,11 @@
 
 namespace RSP_KNS {
 
+using rsp::kSpmvThreads;
 using rsp::SpmvArgs;
 using rsp::SpmvBlock;
 using rsp::SpmvLongRow;
 using rsp::SpmvTile;
-using rsp::kSpmvIter;
-using rsp::kSpmvThreads;
 
 template <typename T, int N>
 struct VecT;
@@ -53,11 +55,6 @@ struct VecT<float, 4> {
     typedef float __attribute__((ext_vector_type(4))) V;
     typedef int __attribute__((ext_vector_type(4))) I;
 };
-template <typename T>
-struct VecT<T, 1> {
-    typedef T V;
-    typedef int I;
-};
 
 // Logical tile for workgroup `bid`: each of the 8 XCDs (round-robin dispatch)
 // gets a contiguous run of tiles, so neighbouring row blocks — which gather
@@ -69,125 +66,176 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
     return start + idx;
 }
 
-template <typename T>
-__device__ __forceinline__ T wave_sum_group(T v, int width) {
-    // butterfly over the low log2(width) lane bits (width <= 64, power of 2)
-    for (int off = width >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+template <bool NT, typename P>
+__device__ __forceinline__ P ld(const P *p) {
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
 }
 
-// Stream the tile's [k0, k1) entries with 16-B loads starting at the aligned
-// element kb = k0 & ~(VW-1); products land in lds[e - kb]. Returns this
-// thread's running sum of its products in element order (used by long-row
-// chunks; ignored by normal tiles).
-template <typename T, int VW, bool kStore>
-__device__ __forceinline__ T stream_tile(const int *__restrict__ colidx,
-                                         const T *__restrict__ vals, const T *__restrict__ x,
-                                         int k0, int k1, T *lds) {
+// Products of entries [k0, k1) into lds[e - kb], kb = k0 rounded down to the
+// vector width. Every load is unpredicated: a vector past k1 re-reads the
+// tile's last vector (an L1 hit), so the loads, then the gathers, issue back
+// to back with no exec-masked blocks between them (a predicated load makes
+// hipcc drain vmcnt before each later gather). Partial vectors at either end
+// touch in-bounds neighbours whose LDS slots are never read. Requires a
+// non-empty tile whose last vector does not straddle the end of the arrays
+// (the caller takes stream_products_scalar otherwise).
+template <typename T, bool NT>
+__device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
+                                                const T *__restrict__ vals,
+                                                const T *__restrict__ x, int kb, int k1,
+                                                T *__restrict__ lds) {
+    constexpr int VW = 16 / sizeof(T);
+    constexpr int IT = SpmvTile<T>::kSlots / (kSpmvThreads * VW);
     typedef typename VecT<T, VW>::V V;
     typedef typename VecT<T, VW>::I I;
     const int tid = threadIdx.x;
-    const int kb = k0 & ~(VW - 1);
-    int c[kSpmvIter][VW];
-    T v[kSpmvIter][VW];
+    const int last = (k1 - 1) & ~(VW - 1);
+    I ci[IT];
+    V vv[IT];
 #pragma unroll
-    for (int it = 0; it < kSpmvIter; ++it) {
-        const int e = kb + (it * kSpmvThreads + tid) * VW;
-        if (e >= k0 && e + VW <= k1) {
-            if constexpr (VW == 1) {
-                c[it][0] = colidx[e];
-                v[it][0] = vals[e];
-            } else {
-                const I ci = *reinterpret_cast<const I *>(colidx + e);
-                const V vi = *reinterpret_cast<const V *>(vals + e);
-#pragma unroll
-                for (int j = 0; j < VW; ++j) {
-                    c[it][j] = ci[j];
-                    v[it][j] = vi[j];
-                }
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < VW; ++j) {
-                const int ej = e + j;
-                const bool ok = ej >= k0 && ej < k1;
-                c[it][j] = ok ? colidx[ej] : -1;
-                v[it][j] = ok ? vals[ej] : T(0);
-            }
-        }
+    for (int it = 0; it < IT; ++it) {
+        const int e = min(kb + (it * kSpmvThreads + tid) * VW, last);
+        ci[it] = ld<NT>(reinterpret_cast<const I *>(colidx + e));
     }
-    T acc = T(0);
 #pragma unroll
-    for (int it = 0; it < kSpmvIter; ++it) {
-        const int e = kb + (it * kSpmvThreads + tid) * VW;
-#pragma unroll
-        for (int j = 0; j < VW; ++j) {
-            if (c[it][j] >= 0) {
-                const T p = v[it][j] * x[c[it][j]];
-                if constexpr (kStore)
-                    lds[e + j - kb] = p;
-                else
-                    acc += p;
-            }
-        }
+    for (int it = 0; it < IT; ++it) {
+        const int e = min(kb + (it * kSpmvThreads + tid) * VW, last);
+        vv[it] = ld<NT>(reinterpret_cast<const V *>(vals + e));
     }
-    return acc;
+    // keep the scheduler from splitting the load and gather bursts: two
+    // memory round trips per tile, not one per vector
+    __builtin_amdgcn_sched_barrier(0);
+    T xv[IT][VW];
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int j = 0; j < VW; ++j) xv[it][j] = x[ci[it][j]];
+    __builtin_amdgcn_sched_barrier(0);
+    // every slot (it*256 + tid)*VW lies inside the tile's LDS image, so the
+    // stores are unpredicated too; slots at or past k1 - kb are never read
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        V p;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) p[j] = vv[it][j] * xv[it][j];
+        *reinterpret_cast<V *>(lds + (it * kSpmvThreads + tid) * VW) = p;
+    }
 }
 
-template <typename T, int VW>
-__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
-    const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
-    const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
-    T *__restrict__ partials, T alpha, T beta, int beta_nonzero) {
-    __shared__ T lds[SpmvTile<T>::kSlots];
-    __shared__ T wsum[kSpmvThreads / 64];
-    const int b = xcd_swizzle(blockIdx.x, nblocks);
-    const SpmvBlock blk = blocks[b];
+// Element-wise variant for a tile that touches the end of the arrays (at
+// most one per call) or unaligned arrays.
+template <typename T>
+__device__ __forceinline__ void stream_products_scalar(const int *__restrict__ colidx,
+                                                       const T *__restrict__ vals,
+                                                       const T *__restrict__ x, int k0, int kb,
+                                                       int k1, T *lds) {
+    for (int e = kb + (int)threadIdx.x; e < k1; e += kSpmvThreads)
+        if (e >= k0) lds[e - kb] = vals[e] * x[colidx[e]];
+}
+
+// Rows [r0, r0 + nrows) of a tile, L lanes per row, canonical 8-way order.
+template <typename T, int L>
+__device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int r0, int nrows,
+                                            int kb, T *__restrict__ y, T alpha, T beta,
+                                            int beta_nonzero) {
+    constexpr int NA = 8 / L;                  // partials held per lane
+    constexpr int NG = kSpmvThreads / L;       // row groups per pass
     const int tid = threadIdx.x;
-
-    if (blk.r1 < 0) {
-        // chunk of a long row: per-thread sums -> wave butterfly -> LDS -> slot
-        T s = stream_tile<T, VW, false>(colidx, vals, x, blk.k0, blk.k1, lds);
-        s = wave_sum_group(s, 64);
-        if ((tid & 63) == 0) wsum[tid >> 6] = s;
-        __syncthreads();
-        if (tid == 0) {
-            T t = T(0);
-#pragma unroll
-            for (int w = 0; w < kSpmvThreads / 64; ++w) t += wsum[w];
-            partials[-(blk.r1 + 1)] = t;
-        }
-        return;
-    }
-
-    stream_tile<T, VW, true>(colidx, vals, x, blk.k0, blk.k1, lds);
-    __syncthreads();
-
-    const int r0 = blk.r0, nrows = blk.r1 - blk.r0;
-    const int kb = blk.k0 & ~(VW - 1);
-    const int nnz = blk.k1 - blk.k0;
-    // lanes per row: power of two <= 64 such that every lane still sums >= 4
-    // products of an average row and the groups fit the workgroup. Tiles of
-    // short rows (avg < 8) keep L = 1: sequential column order per row, i.e.
-    // bit-identical to the CPU oracle.
-    int L = 1;
-    while (L < 64 && 2 * L * nrows <= kSpmvThreads && 8 * L * nrows <= nnz) L <<= 1;
-    const int g = tid / L, lane = tid & (L - 1), ngroups = kSpmvThreads / L;
-    // groups of one wave share a trip count within +-1, and all lanes of a
-    // group stay convergent for the shuffles.
-    for (int rr = g; rr - g < nrows; rr += ngroups) {
+    const int g = tid / L, lane = tid & (L - 1);
+    for (int rr = g; rr - g < nrows; rr += NG) {  // same trip count for all groups
         const bool active = rr < nrows;
-        T s = T(0);
+        T acc[NA];
+#pragma unroll
+        for (int t = 0; t < NA; ++t) acc[t] = T(0);
         if (active) {
-            const int a = rowptr[r0 + rr] - kb, e = rowptr[r0 + rr + 1] - kb;
-            for (int k = a + lane; k < e; k += L) s += lds[k];
+            const int a1 = rp_lds[rr + 1] - kb;
+            for (int base = rp_lds[rr] - kb + lane; base < a1; base += 8) {
+#pragma unroll
+                for (int t = 0; t < NA; ++t) {
+                    const int k = base + t * L;  // partial (lane + t*L) of the row
+                    if (k < a1) acc[t] += lds[k];
+                }
+            }
         }
-        if (L > 1) s = wave_sum_group(s, L);
+        // tree stages whose pair offset (4, 2, 1) is a multiple of L: local
+#pragma unroll
+        for (int h = NA / 2; h >= 1; h >>= 1)
+#pragma unroll
+            for (int t = 0; t < h; ++t) acc[t] = acc[t] + acc[t + h];
+        T s = acc[0];
+        // remaining stages across the L lanes of the group
+#pragma unroll
+        for (int off = L / 2; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
         if (active && lane == 0) {
             T out = alpha * s;
             if (beta_nonzero) out += beta * y[r0 + rr];
             y[r0 + rr] = out;
         }
+    }
+}
+
+template <typename T, bool NT>
+__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
+    const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
+    const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
+    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok) {
+    constexpr int VW = 16 / sizeof(T);
+    __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
+    __shared__ T wsum[kSpmvThreads / 64];
+    __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
+    constexpr int RPQ = (rsp::kSpmvMaxRows + kSpmvThreads) / kSpmvThreads;
+    const int b = xcd_swizzle(blockIdx.x, nblocks);
+    const SpmvBlock blk = blocks[b];
+    const int tid = threadIdx.x;
+    const int k0 = blk.k0, k1 = blk.k1;
+    // the tile's row offsets, loaded ahead of the stream and parked in LDS
+    // after it, so the reduce never waits on global memory
+    const int nrows = blk.r1 - blk.r0;
+    const int nrows_ld = nrows > 0 ? nrows : 0;  // long-row chunks: r1 < 0
+    int rpv[RPQ];
+#pragma unroll
+    for (int q = 0; q < RPQ; ++q)  // unpredicated (clamped) so nothing waits here
+        rpv[q] = rowptr[blk.r0 + min(tid + q * kSpmvThreads, nrows_ld)];
+    // vectors may be used unless the tile reaches the last, partial vector
+    const bool vec = vector_ok && k1 > k0 && k1 <= (nnz & ~(VW - 1));
+    const int kb = vec ? (k0 & ~(VW - 1)) : k0;
+    if (vec)
+        stream_products<T, NT>(colidx, vals, x, kb, k1, lds);
+    else
+        stream_products_scalar<T>(colidx, vals, x, k0, kb, k1, lds);
+#pragma unroll
+    for (int q = 0; q < RPQ; ++q) {
+        const int i = tid + q * kSpmvThreads;
+        if (i <= nrows) rp_lds[i] = rpv[q];
+    }
+    __syncthreads();
+
+    if (blk.r1 < 0) {
+        // chunk of a long row: thread t sums chunk elements t, t+256, ...
+        // (relative to the chunk start), then a fixed butterfly + wave order
+        T s = T(0);
+        for (int e = (k0 - kb) + tid; e < k1 - kb; e += kSpmvThreads) s += lds[e];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
+        if ((tid & 63) == 0) wsum[tid >> 6] = s;
+        __syncthreads();
+        if (tid == 0) partials[-(blk.r1 + 1)] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        return;
+    }
+
+    const int r0 = blk.r0, nnzt = k1 - k0;
+    // lanes per row: power of two <= 8 such that each lane still sums >= 4
+    // products of an average row and the groups fit the workgroup
+    int L = 1;
+    while (L < 8 && 2 * L * nrows <= kSpmvThreads && 8 * L * nrows <= nnzt) L <<= 1;
+    switch (L) {
+        case 1: reduce_rows<T, 1>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
+        case 2: reduce_rows<T, 2>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
+        case 4: reduce_rows<T, 4>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
+        default: reduce_rows<T, 8>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
     }
 }
 
@@ -209,29 +257,27 @@ __global__ __launch_bounds__(64) void spmv_longrow_fixup(const SpmvLongRow *__re
 
 template <typename T>
 static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
-    if (a.nblocks > 0) {
-        const T alpha = (T)a.alpha, beta = (T)a.beta;
-        const int bnz = a.beta != 0.0;
-        if (a.vector_ok)
-            hipLaunchKernelGGL((spmv_tiles<T, SpmvTile<T>::kVec>), dim3(a.nblocks),
-                               dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx, (const T *)a.vals,
-                               (const T *)a.x, (T *)a.y, a.blocks, a.nblocks, (T *)a.partials,
-                               alpha, beta, bnz);
-        else
-            hipLaunchKernelGGL((spmv_tiles<T, 1>), dim3(a.nblocks), dim3(kSpmvThreads), 0, s,
-                               a.rowptr, a.colidx, (const T *)a.vals, (const T *)a.x, (T *)a.y,
-                               a.blocks, a.nblocks, (T *)a.partials, alpha, beta, bnz);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        if (a.nlong > 0) {
-            hipLaunchKernelGGL((spmv_longrow_fixup<T>), dim3((a.nlong + 63) / 64), dim3(64), 0, s,
-                               a.longrows, a.nlong, (const T *)a.partials, (T *)a.y, alpha, beta,
-                               bnz);
-            e = hipGetLastError();
-        }
-        return e;
+    if (a.nblocks <= 0) return hipSuccess;
+    const T alpha = (T)a.alpha, beta = (T)a.beta;
+    const int bnz = a.beta != 0.0;
+    if (a.variant & 1)
+        hipLaunchKernelGGL((spmv_tiles<T, true>), dim3(a.nblocks), dim3(kSpmvThreads), 0, s,
+                           a.rowptr, a.colidx, (const T *)a.vals, (const T *)a.x, (T *)a.y,
+                           a.blocks, a.nblocks, (T *)a.partials, alpha, beta, bnz, a.nnz,
+                           a.vector_ok);
+    else
+        hipLaunchKernelGGL((spmv_tiles<T, false>), dim3(a.nblocks), dim3(kSpmvThreads), 0, s,
+                           a.rowptr, a.colidx, (const T *)a.vals, (const T *)a.x, (T *)a.y,
+                           a.blocks, a.nblocks, (T *)a.partials, alpha, beta, bnz, a.nnz,
+                           a.vector_ok);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (a.nlong > 0) {
+        hipLaunchKernelGGL((spmv_longrow_fixup<T>), dim3((a.nlong + 63) / 64), dim3(64), 0, s,
+                           a.longrows, a.nlong, (const T *)a.partials, (T *)a.y, alpha, beta, bnz);
+        e = hipGetLastError();
     }
-    return hipSuccess;
+    return e;
 }
 
 hipError_t spmv_f32(const SpmvArgs &a, hipStream_t s) { return launch_spmv<float>(a, s); }

@@ -21,7 +21,8 @@ def _load():
     lib = C.CDLL(ORACLE_SO)
     ip, vp = C.POINTER(C.c_int), C.c_void_p
     for name in ("oracle_spmv_f64", "oracle_spmv_f32", "oracle_spmv_f32_ftz", "oracle_spmv_f64_omp",
-                 "oracle_spmv_f32_omp"):
+                 "oracle_spmv_f32_omp", "oracle_spmv_w8_f64", "oracle_spmv_w8_f32",
+                 "oracle_spmv_w8_f32_ftz"):
         getattr(lib, name).argtypes = [C.c_int, ip, ip, vp, vp, vp]
         getattr(lib, name).restype = None
     lib.oracle_num_threads.restype = C.c_int
@@ -48,14 +49,19 @@ def _i(a):
     return np.ascontiguousarray(a, np.int32).ctypes.data_as(C.POINTER(C.c_int))
 
 
-def spmv(rowptr, colidx, vals, x, ftz=False, threads=False):
+def spmv(rowptr, colidx, vals, x, ftz=False, threads=False, order="seq"):
+    """order="seq": column order per row (the reference semantics);
+    order="w8": the canonical 8-way interleaved order of the GPU tiles."""
     rp = np.ascontiguousarray(rowptr, np.int32)
     ci = np.ascontiguousarray(colidx, np.int32)
     v = np.ascontiguousarray(vals)
     xx = np.ascontiguousarray(x, v.dtype)
     m = rp.shape[0] - 1
     y = np.empty(m, v.dtype)
-    if v.dtype == np.float64:
+    if order == "w8":
+        fn = (lib.oracle_spmv_w8_f64 if v.dtype == np.float64
+              else (lib.oracle_spmv_w8_f32_ftz if ftz else lib.oracle_spmv_w8_f32))
+    elif v.dtype == np.float64:
         fn = lib.oracle_spmv_f64_omp if threads else lib.oracle_spmv_f64
     else:
         fn = lib.oracle_spmv_f32_ftz if ftz else (lib.oracle_spmv_f32_omp if threads else lib.oracle_spmv_f32)
@@ -105,6 +111,9 @@ def dlarnv(idist, seed, n):
     x = np.empty(n, np.float64)
     assert lib.oracle_dlarnv(idist, s, n, x.ctypes.data) == 0
     return x, list(s)
+
+
+TILE_CAP = {np.dtype(np.float64): 2047, np.dtype(np.float32): 4093}  # SpmvTile<T>::kMaxNnz
 
 
 def spmv_bound(rowptr, colidx, vals, x, eps):

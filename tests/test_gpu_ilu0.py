@@ -123,12 +123,27 @@ def test_true_lu_extension(handle, dtype):
     compare(A, dtype, handle, x=x, true_lu=True)
 
 
+def _levels(rowptr, colidx, transpose):
+    n = len(rowptr) - 1
+    lev = np.zeros(n, np.int64)
+    order = range(n - 1, -1, -1) if transpose else range(n)
+    for i in order:
+        row = colidx[rowptr[i]:rowptr[i + 1]]
+        low = row[row < i]
+        if transpose:
+            if low.size:
+                np.maximum.at(lev, low, lev[i] + 1)
+        elif low.size:
+            lev[i] = lev[low].max() + 1
+    return int(lev.max()) + 1
+
+
 def test_levels_reported(handle):
-    A = csr.surrogate("ecology2", 0.01)  # 5-point grid: levels ~ 2*sqrt(n)
+    A = csr.surrogate("ecology2", 0.01)
     il = compare(A, torch.float64, handle)
     lo, up = il.levels()
-    side = int(np.ceil(np.sqrt(A.m)))
-    assert side <= lo <= 2 * side + 1 and lo == up
+    assert lo == _levels(A.rowptr, A.colidx, False)
+    assert up == _levels(A.rowptr, A.colidx, True)
 
 
 def test_full_size_moderate(handle):
