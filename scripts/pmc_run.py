@@ -1,0 +1,70 @@
+"""Workload for the rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE are
+collected in separate runs, guide §rocprofv3).
+
+1. calibration: y = D x with a 32 M-row DIAGONAL matrix (fp64). Every byte
+   is streamed exactly once (vals 8 B + colidx 4 B + rowptr 4 B + x 8 B read,
+   y 8 B written per row), so its FETCH_SIZE/WRITE_SIZE give the counter's
+   bytes-per-unit for this kernel's access pattern (the gfx950 FETCH_SIZE
+   under-count of wide loads, MI355X_MICROARCH.md §HBM);
+2. the bench workload: `--passes` cycles of fp64 SpMV over every matrix of
+   the set (the same order as bench.py, so no matrix is cache-resident).
+scripts/pmc_summary.py turns the two CSVs into profiles/<tag>_pmc.json.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from respasol_amd import csr  # noqa: E402
+from respasol_amd.sparse import Handle, SpMat, upload_csr  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--set", default="big")
+    ap.add_argument("--passes", type=int, default=3)
+    ap.add_argument("--calib-rows", type=int, default=32 << 20)
+    ap.add_argument("--meta", default="")
+    args = ap.parse_args()
+    h = Handle()
+    n = args.calib_rows
+    rp = torch.arange(n + 1, dtype=torch.int32, device="cuda")
+    ci = torch.arange(n, dtype=torch.int32, device="cuda")
+    va = torch.rand(n, dtype=torch.float64, device="cuda")
+    x = torch.rand(n, dtype=torch.float64, device="cuda")
+    y = torch.empty(n, dtype=torch.float64, device="cuda")
+    D = SpMat(h, rp, ci, va, n)
+    for _ in range(3):
+        D.spmv(x, y)
+    torch.cuda.synchronize()
+    calib = {"rows": n, "read_bytes": n * (8 + 4 + 4 + 8) + 4, "write_bytes": n * 8, "launches": 3}
+    del D, rp, ci, va, x, y
+    names = csr.surrogate_names(1 if args.set == "big" else 0)
+    mats = []
+    for name in names:
+        A = csr.surrogate(name)
+        d = upload_csr(A.rowptr, A.colidx, A.values)
+        xx = torch.from_numpy(csr.dlarnv(1, [0, 0, 0, 1], A.n)[0]).cuda()
+        mats.append((name, A.spmv_bytes(8), SpMat(h, *d, A.n), xx,
+                     torch.empty(A.m, dtype=torch.float64, device="cuda")))
+        del A
+    for _ in range(args.passes):
+        for name, b, M, xx, yy in mats:
+            M.spmv(xx, yy)
+    torch.cuda.synchronize()
+    if args.meta:
+        with open(args.meta, "w") as f:
+            json.dump({"calibration": calib, "set": args.set, "passes": args.passes,
+                       "matrices": [{"name": n_, "grid": int(M.buffer.numel()), "alg_bytes": b}
+                                    for n_, b, M, _, _ in mats]}, f)
+
+
+if __name__ == "__main__":
+    main()

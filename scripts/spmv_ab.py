@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dtype", default="f64")
+    ap.add_argument("--mode", default="cycled", choices=["cycled", "hot"],
+                    help="cycled: one call per matrix per pass over the set (cache-cold, like "
+                         "bench.py); hot: --reps back-to-back calls of one matrix")
     args = ap.parse_args()
     dt = torch.float64 if args.dtype == "f64" else torch.float32
     elem = 8 if dt == torch.float64 else 4
@@ -64,16 +67,27 @@ def main():
     copy_gbs = 2 * src.numel() * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
     del src, dst
     times = {(n, v): [] for n, *_ in mats for v in variants}
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in mats]
     for _ in range(args.rounds):
         for v in variants:
-            for n, _b, _f, per, x, y in mats:
-                per[v].spmv(x, y)  # warm this matrix's schedule, not its cache
-                e0.record()
-                for _ in range(args.reps):
+            if args.mode == "hot":
+                for n, _b, _f, per, x, y in mats:
                     per[v].spmv(x, y)
-                e1.record()
-                torch.cuda.synchronize()
-                times[(n, v)].append(e0.elapsed_time(e1) / args.reps * 1e3)
+                    e0.record()
+                    for _ in range(args.reps):
+                        per[v].spmv(x, y)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    times[(n, v)].append(e0.elapsed_time(e1) / args.reps * 1e3)
+            else:
+                for _ in range(args.reps):
+                    for (n, _b, _f, per, x, y), (a, b) in zip(mats, evs):
+                        a.record()
+                        per[v].spmv(x, y)
+                        b.record()
+                    torch.cuda.synchronize()
+                    for (n, *_), (a, b) in zip(mats, evs):
+                        times[(n, v)].append(a.elapsed_time(b) * 1e3)
     print(f"device copy (read+write) {copy_gbs:.0f} GB/s")
     tot = {v: 0.0 for v in variants}
     totb = sum(b for _, b, *_ in mats)
