@@ -50,7 +50,7 @@ struct SpmvArgs {
     double alpha, beta;
     int nnz;        // rowptr[m]: tiles touching the last partial vector go scalar
     int vector_ok;  // colidx/vals 16-B aligned -> vector loads
-    int variant;    // bit 0: non-temporal vals/colidx loads
+    int variant;    // bit 0: default-policy (not non-temporal) vals/colidx loads
 };
 
 struct IluArgs {

@@ -260,7 +260,10 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
     const T alpha = (T)a.alpha, beta = (T)a.beta;
     const int bnz = a.beta != 0.0;
-    if (a.variant & 1)
+    // vals/colidx are read once per call: non-temporal loads keep them from
+    // evicting x (measured +2% fp64 / +7.5% fp32 on the cache-cold big set);
+    // variant bit 0 restores default-policy loads for A/B runs
+    if (!(a.variant & 1))
         hipLaunchKernelGGL((spmv_tiles<T, true>), dim3(a.nblocks), dim3(kSpmvThreads), 0, s,
                            a.rowptr, a.colidx, (const T *)a.vals, (const T *)a.x, (T *)a.y,
                            a.blocks, a.nblocks, (T *)a.partials, alpha, beta, bnz, a.nnz,
