@@ -26,6 +26,7 @@ struct rsp_context {
     hipStream_t stream;
     int ftz;
     int spmv_variant;  // RSP_SPMV_VARIANT (tuning knob, default 0)
+    int num_cus;
 };
 
 struct rsp_spmat {
@@ -98,6 +99,7 @@ rsp_status_t rsp_create(rsp_handle_t *handle) {
     c->ftz = 0;
     const char *v = getenv("RSP_SPMV_VARIANT");
     c->spmv_variant = v ? atoi(v) : 0;
+    c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     *handle = c;
     return RSP_STATUS_SUCCESS;
 }
@@ -370,6 +372,7 @@ rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp
     a.vector_ok = ((((uintptr_t)mat->colidx) | ((uintptr_t)mat->vals)) & 15) == 0;
     a.nnz = mat->nnz_s;
     a.variant = h->spmv_variant;
+    a.num_cus = h->num_cus;
     hipError_t e;
     if (compute_type == RSP_R_64F)
         e = rsp_k::spmv_f64(a, h->stream);

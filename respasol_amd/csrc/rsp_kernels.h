@@ -50,7 +50,9 @@ struct SpmvArgs {
     double alpha, beta;
     int nnz;        // rowptr[m]: tiles touching the last partial vector go scalar
     int vector_ok;  // colidx/vals 16-B aligned -> vector loads
-    int variant;    // bit 0: default-policy (not non-temporal) vals/colidx loads
+    int variant;    // bit 0: default-policy (not non-temporal) vals/colidx loads;
+                    // bit 1: persistent pipelined kernel
+    int num_cus;    // compute units of the device (persistent grid sizing)
 };
 
 struct IluArgs {

@@ -239,6 +239,150 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent, software-pipelined form of spmv_tiles: gridDim.x workgroups,
+// each walking a contiguous run of `tpw` tiles (XCD-swizzled so each XCD owns
+// a contiguous eighth of the matrix). The colidx/vals/row-offset loads of
+// tile t+1 are issued before tile t is reduced, so the HBM stream of a
+// workgroup stays busy through its reduce phase and there is no per-tile
+// dispatch. Same arithmetic and summation order as spmv_tiles.
+
+template <typename T>
+struct TileRegs {
+    static constexpr int VW = 16 / sizeof(T);
+    static constexpr int IT = SpmvTile<T>::kSlots / (kSpmvThreads * VW);
+    static constexpr int RPQ = (rsp::kSpmvMaxRows + kSpmvThreads) / kSpmvThreads;
+    typename VecT<T, VW>::I ci[IT];
+    typename VecT<T, VW>::V vv[IT];
+    int rpv[RPQ];
+};
+
+// Issue the loads of one tile (vector path only; the scalar path loads in
+// finish). Returns the tile's vector flag.
+template <typename T, bool NT>
+__device__ __forceinline__ bool issue_tile(const SpmvBlock &blk, const int *__restrict__ rowptr,
+                                           const int *__restrict__ colidx,
+                                           const T *__restrict__ vals, int nnz, int vector_ok,
+                                           TileRegs<T> &r) {
+    typedef TileRegs<T> R;
+    typedef typename VecT<T, R::VW>::I I;
+    typedef typename VecT<T, R::VW>::V V;
+    const int tid = threadIdx.x;
+    const int nrows = blk.r1 - blk.r0;
+    const int nrows_ld = nrows > 0 ? nrows : 0;
+#pragma unroll
+    for (int q = 0; q < R::RPQ; ++q) r.rpv[q] = rowptr[blk.r0 + min(tid + q * kSpmvThreads, nrows_ld)];
+    const bool vec = vector_ok && blk.k1 > blk.k0 && blk.k1 <= (nnz & ~(R::VW - 1));
+    if (vec) {
+        const int kb = blk.k0 & ~(R::VW - 1);
+        const int last = (blk.k1 - 1) & ~(R::VW - 1);
+#pragma unroll
+        for (int it = 0; it < R::IT; ++it)
+            r.ci[it] = ld<NT>(reinterpret_cast<const I *>(colidx + min(kb + (it * kSpmvThreads + tid) * R::VW, last)));
+#pragma unroll
+        for (int it = 0; it < R::IT; ++it)
+            r.vv[it] = ld<NT>(reinterpret_cast<const V *>(vals + min(kb + (it * kSpmvThreads + tid) * R::VW, last)));
+    }
+    return vec;
+}
+
+// Gathers + products into LDS (+ row offsets); returns kb.
+template <typename T>
+__device__ __forceinline__ int finish_tile(const SpmvBlock &blk, bool vec,
+                                           const int *__restrict__ colidx,
+                                           const T *__restrict__ vals, const T *__restrict__ x,
+                                           const TileRegs<T> &r, T *__restrict__ lds, int *rp_lds) {
+    typedef TileRegs<T> R;
+    typedef typename VecT<T, R::VW>::V V;
+    const int tid = threadIdx.x;
+    int kb;
+    if (vec) {
+        kb = blk.k0 & ~(R::VW - 1);
+        T xv[R::IT][R::VW];
+#pragma unroll
+        for (int it = 0; it < R::IT; ++it)
+#pragma unroll
+            for (int j = 0; j < R::VW; ++j) xv[it][j] = x[r.ci[it][j]];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int it = 0; it < R::IT; ++it) {
+            V p;
+#pragma unroll
+            for (int j = 0; j < R::VW; ++j) p[j] = r.vv[it][j] * xv[it][j];
+            *reinterpret_cast<V *>(lds + (it * kSpmvThreads + tid) * R::VW) = p;
+        }
+    } else {
+        kb = blk.k0;
+        stream_products_scalar<T>(colidx, vals, x, blk.k0, kb, blk.k1, lds);
+    }
+    const int nrows = blk.r1 - blk.r0;
+#pragma unroll
+    for (int q = 0; q < R::RPQ; ++q) {
+        const int i = tid + q * kSpmvThreads;
+        if (i <= nrows) rp_lds[i] = r.rpv[q];
+    }
+    return kb;
+}
+
+template <typename T>
+__device__ __forceinline__ void reduce_tile(const SpmvBlock &blk, int kb, const T *lds,
+                                            const int *rp_lds, T *wsum, T *__restrict__ y,
+                                            T *__restrict__ partials, T alpha, T beta,
+                                            int beta_nonzero) {
+    const int tid = threadIdx.x;
+    if (blk.r1 < 0) {
+        T s = T(0);
+        for (int e = (blk.k0 - kb) + tid; e < blk.k1 - kb; e += kSpmvThreads) s += lds[e];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
+        if ((tid & 63) == 0) wsum[tid >> 6] = s;
+        __syncthreads();
+        if (tid == 0) partials[-(blk.r1 + 1)] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        return;
+    }
+    const int r0 = blk.r0, nrows = blk.r1 - blk.r0, nnzt = blk.k1 - blk.k0;
+    int L = 1;
+    while (L < 8 && 2 * L * nrows <= kSpmvThreads && 8 * L * nrows <= nnzt) L <<= 1;
+    switch (L) {
+        case 1: reduce_rows<T, 1>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
+        case 2: reduce_rows<T, 2>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
+        case 4: reduce_rows<T, 4>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
+        default: reduce_rows<T, 8>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
+    }
+}
+
+template <typename T, bool NT>
+__global__ __launch_bounds__(kSpmvThreads) void spmv_persistent(
+    const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
+    const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
+    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, int tpw) {
+    __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
+    __shared__ T wsum[kSpmvThreads / 64];
+    __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
+    const int w = xcd_swizzle(blockIdx.x, gridDim.x);
+    int t = w * tpw;
+    const int tend = min(nblocks, t + tpw);
+    if (t >= tend) return;
+    TileRegs<T> r;
+    SpmvBlock blk = blocks[t];
+    bool vec = issue_tile<T, NT>(blk, rowptr, colidx, vals, nnz, vector_ok, r);
+    for (; t < tend; ++t) {
+        const int kb = finish_tile<T>(blk, vec, colidx, vals, x, r, lds, rp_lds);
+        __syncthreads();
+        SpmvBlock nblk = blk;
+        bool nvec = false;
+        if (t + 1 < tend) {  // prefetch the next tile under this tile's reduce
+            nblk = blocks[t + 1];
+            nvec = issue_tile<T, NT>(nblk, rowptr, colidx, vals, nnz, vector_ok, r);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        reduce_tile<T>(blk, kb, lds, rp_lds, wsum, y, partials, alpha, beta, beta_nonzero);
+        __syncthreads();
+        blk = nblk;
+        vec = nvec;
+    }
+}
+
 // y[row] = alpha * sum(partials of the row, chunk order) (+ beta*y[row]).
 template <typename T>
 __global__ __launch_bounds__(64) void spmv_longrow_fixup(const SpmvLongRow *__restrict__ lr,
@@ -260,6 +404,23 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
     const T alpha = (T)a.alpha, beta = (T)a.beta;
     const int bnz = a.beta != 0.0;
+    if (a.variant & 2) {
+        // persistent: one workgroup per resident slot (occupancy query x CUs;
+        // performance only — a non-resident workgroup would just run late),
+        // tiles shared out in contiguous runs
+        auto kern = (a.variant & 1) ? spmv_persistent<T, false> : spmv_persistent<T, true>;
+        static int occ[2] = {0, 0};
+        int &o = occ[a.variant & 1];
+        if (o == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, kSpmvThreads, 0) !=
+                           hipSuccess || o < 1))
+            o = 1;
+        const int grid = min(a.nblocks, o * a.num_cus);
+        const int tpw = (a.nblocks + grid - 1) / grid;
+        const int g = (a.nblocks + tpw - 1) / tpw;
+        hipLaunchKernelGGL(kern, dim3(g), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
+                           (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks,
+                           (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok, tpw);
+    } else
     // vals/colidx are read once per call: non-temporal loads keep them from
     // evicting x (measured +2% fp64 / +7.5% fp32 on the cache-cold big set);
     // variant bit 0 restores default-policy loads for A/B runs
