@@ -146,15 +146,21 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fp32-reps", type=int, default=10)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    dev = local % max(torch.cuda.device_count(), 1)  # == local on a full node
+    torch.cuda.set_device(dev)
+    device = torch.device("cuda", dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
     handle = Handle()
     names = workload_names(args.workload)
 
@@ -287,6 +293,9 @@ def main():
                 "matrices": len(slices),
                 "nnz_stored_total": int(sum(s.nnz_global for s in slices)),
                 "parallelism": f"row-partition x{world}" if world > 1 else "1 GPU",
+                "collective": (f"all_gather_into_tensor over {args.dist_backend}"
+                               + (" (RCCL, xGMI)" if args.dist_backend == "nccl" else " (rehearsal)"))
+                if world > 1 else None,
             },
             "hbm_gbps": round(hbm_gbs, 1),
             "roofline": {

@@ -78,8 +78,16 @@ class RowPartitionedSpmv:
 
     def exchange(self) -> None:
         """all_gather the x slices into the replicated x (in place)."""
-        if self.P > 1:
-            dist.all_gather_into_tensor(self.x_full, self.x_local, group=self.group)
+        if self.P <= 1:
+            return
+        if self.x_full.is_cuda and dist.get_backend(self.group) == "gloo":
+            # rehearsal path (gloo on a GPU box): stage through host memory
+            host = self.x_full.cpu()
+            dist.all_gather_into_tensor(host, host[self.rank * self.chunk:(self.rank + 1) * self.chunk].clone(),
+                                        group=self.group)
+            self.x_full.copy_(host)
+            return
+        dist.all_gather_into_tensor(self.x_full, self.x_local, group=self.group)
 
     def step(self, y_local: torch.Tensor | None = None) -> torch.Tensor:
         self.exchange()
@@ -90,7 +98,11 @@ class RowPartitionedSpmv:
         buf = torch.zeros(max(self.P * self.chunk, 1), dtype=y_local.dtype, device=y_local.device)
         pad = torch.zeros(max(self.chunk, 1), dtype=y_local.dtype, device=y_local.device)
         pad[: self.m_local].copy_(y_local[: self.m_local])
-        if self.P > 1:
+        if self.P > 1 and buf.is_cuda and dist.get_backend(self.group) == "gloo":
+            host = buf.cpu()
+            dist.all_gather_into_tensor(host, pad[: self.chunk].cpu(), group=self.group)
+            buf.copy_(host)
+        elif self.P > 1:
             dist.all_gather_into_tensor(buf, pad[: self.chunk], group=self.group)
         else:
             buf[: self.chunk].copy_(pad[: self.chunk])
