@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from respasol_amd import csr  # noqa: E402
-from respasol_amd.dist import RowPartitionedSpmv, remap_columns  # noqa: E402
+from respasol_amd.dist import HaloExchange, HaloSlice, RowPartitionedSpmv, remap_columns  # noqa: E402
 from respasol_amd.sparse import Handle, SpMat, upload_csr  # noqa: E402
 
 METRIC = "CSR SpMV GFLOP/s + achieved HBM GB/s (fp64 vs fp32), SuiteSparse set, 1/2/4/8 GPU"
@@ -51,9 +51,10 @@ def log(*a):
 
 
 class Slice:
-    """One matrix's share on this rank."""
+    """One matrix's share on this rank: its rows [r0, r1) (nnz-balanced split),
+    generated locally, with the column layout of the chosen exchange."""
 
-    def __init__(self, name, rank, world, handle, device):
+    def __init__(self, name, rank, world, handle, device, exchange):
         self.name = name
         m = csr.surrogate_rows(name)
         lens = csr.surrogate_rowlens(name)
@@ -64,32 +65,49 @@ class Slice:
         self.bounds = csr.partition_rows(rowptr.astype(np.int32), world)
         r0, r1 = int(self.bounds[rank]), int(self.bounds[rank + 1])
         self.r0, self.r1 = r0, r1
+        self.m_local = r1 - r0
         rp, ci, va = csr.surrogate_rows_csr(name, r0, r1)
-        self.host = (rp, ci, va)
-        ci_pad, chunk = remap_columns(ci, self.bounds) if world > 1 else (ci, m)
-        self.n_pad = world * chunk if world > 1 else m
         self.nnz_local = int(rp[-1])
-        d64 = upload_csr(rp, ci_pad, va, torch.float64, device)
-        self.mat64 = SpMat(handle, *d64, self.n_pad)
-        d32 = upload_csr(rp, ci_pad, va, torch.float32, device)
-        self.mat32 = SpMat(handle, *d32, self.n_pad)
-        x, _ = csr.dlarnv(1, [0, 0, 0, 1], m)
-        self.part64 = RowPartitionedSpmv(self.bounds, rank, torch.float64, device,
-                                         lambda xf, y=None: self.mat64.spmv(xf, y))
-        self.part64.set_local_x(torch.from_numpy(x[r0:r1]).to(device))
-        self.part32 = RowPartitionedSpmv(self.bounds, rank, torch.float32, device,
-                                         lambda xf, y=None: self.mat32.spmv(xf, y))
-        self.part32.set_local_x(torch.from_numpy(x[r0:r1].astype(np.float32)).to(device))
-        self.part64.exchange()
-        self.part32.exchange()
-        self.y64 = torch.empty(max(r1 - r0, 1), dtype=torch.float64, device=device)
-        self.y32 = torch.empty(max(r1 - r0, 1), dtype=torch.float32, device=device)
+        self.x_global_slice = csr.dlarnv(1, [0, 0, 0, 1], m)[0][r0:r1]
+        self.mode = exchange if world > 1 else "none"
+        if self.mode == "halo":
+            self.halo = HaloSlice(ci, self.bounds, rank)
+            ci_dev, self.n_x = self.halo.colidx_ext, self.halo.n_ext
+        elif self.mode == "allgather":
+            ci_dev, chunk = remap_columns(ci, self.bounds)
+            self.n_x = world * chunk
+        else:
+            ci_dev, self.n_x = ci, m
+        self.host = (rp, ci_dev, va)
+        self.mat64 = SpMat(handle, *upload_csr(rp, ci_dev, va, torch.float64, device), self.n_x)
+        self.mat32 = SpMat(handle, *upload_csr(rp, ci_dev, va, torch.float32, device), self.n_x)
+        self.y64 = torch.empty(max(self.m_local, 1), dtype=torch.float64, device=device)
+        self.y32 = torch.empty(max(self.m_local, 1), dtype=torch.float32, device=device)
+        if self.mode != "halo":  # replicated x (padded layout for the all-gather)
+            self.part64 = RowPartitionedSpmv(self.bounds, rank, torch.float64, device, None)
+            self.part32 = RowPartitionedSpmv(self.bounds, rank, torch.float32, device, None)
+            self.part64.set_local_x(torch.from_numpy(self.x_global_slice).to(device))
+            self.part32.set_local_x(torch.from_numpy(self.x_global_slice.astype(np.float32)).to(device))
+            self.part64.exchange()
+            self.part32.exchange()
+
+    def bind_halo(self, i, ex64, ex32):
+        self.i, self.ex64, self.ex32 = i, ex64, ex32
+        ex64.x_local(i).copy_(torch.from_numpy(self.x_global_slice))
+        ex32.x_local(i).copy_(torch.from_numpy(self.x_global_slice.astype(np.float32)))
+
+    def x64(self):
+        return self.ex64.x_ext(self.i) if self.mode == "halo" else self.part64.x_full
+
+    def x32(self):
+        return self.ex32.x_ext(self.i) if self.mode == "halo" else self.part32.x_full
 
     def bytes_local(self, elem):
         """Algorithmic bytes of this rank's SpMV: vals+colidx,
-        rowptr, one read of the replicated x, y write."""
-        ml = self.r1 - self.r0
-        return (elem + 4) * self.nnz_local + 4 * (ml + 1) + elem * self.n + elem * ml
+        rowptr, one read of the x the slice references (n at N = 1, the
+        replicated x for the all-gather, local + halo for the halo exchange),
+        y write."""
+        return (elem + 4) * self.nnz_local + 4 * (self.m_local + 1) + elem * self.n_x + elem * self.m_local
 
 
 def workload_names(w):
@@ -146,6 +164,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fp32-reps", type=int, default=10)
+    ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"],
+                    help="N>1 x exchange: halo-only all_to_all (default) or full all-gather")
+    ap.add_argument("--no-bucket", action="store_true",
+                    help="halo mode: one exchange per matrix instead of one per step")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
@@ -165,20 +187,37 @@ def main():
     names = workload_names(args.workload)
 
     t_setup = time.perf_counter()
-    slices = [Slice(n, rank, world, handle, device) for n in names]
+    slices = [Slice(n, rank, world, handle, device, args.exchange) for n in names]
+    exchanges64, exchanges32 = [], []
+    if world > 1 and args.exchange == "halo":
+        groups = [[i] for i in range(len(slices))] if args.no_bucket else [list(range(len(slices)))]
+        for g in groups:
+            ex64 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float64, device, handle)
+            ex32 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float32, device, handle)
+            for j, i in enumerate(g):
+                slices[i].bind_halo(j, ex64, ex32)
+            ex64.exchange()
+            ex32.exchange()
+            exchanges64.append((g, ex64))
+            exchanges32.append((g, ex32))
     torch.cuda.synchronize()
     log(f"setup {time.perf_counter() - t_setup:.1f}s: {len(slices)} matrices, "
         f"{sum(s.nnz_global for s in slices) / 1e6:.1f} M stored nnz, world={world}")
 
     stream = torch.cuda.current_stream()
 
+    first_of = {g[0]: ex for g, ex in exchanges64}  # halo: exchange before a group's first SpMV
+
     def step(exchange=True, events=None):
         for i, s in enumerate(slices):
             if exchange:
-                s.part64.exchange()
+                if s.mode == "allgather":
+                    s.part64.exchange()
+                elif i in first_of:
+                    first_of[i].exchange()
             if events is not None:
                 events[i][0].record(stream)
-            s.mat64.spmv(s.part64.x_full, s.y64[: s.r1 - s.r0] if s.r1 > s.r0 else s.y64)
+            s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
             if events is not None:
                 events[i][1].record(stream)
 
@@ -241,12 +280,12 @@ def main():
     # fp32 companion measurement (outside the timed region)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for s in slices:
-        s.mat32.spmv(s.part32.x_full, s.y32[: max(s.r1 - s.r0, 1)] if s.r1 > s.r0 else s.y32)
+        s.mat32.spmv(s.x32(), s.y32[: s.m_local] if s.m_local else s.y32)
     torch.cuda.synchronize()
     e0.record(stream)
     for _ in range(args.fp32_reps):
         for s in slices:
-            s.mat32.spmv(s.part32.x_full, s.y32[: s.r1 - s.r0] if s.r1 > s.r0 else s.y32)
+            s.mat32.spmv(s.x32(), s.y32[: s.m_local] if s.m_local else s.y32)
     e1.record(stream)
     torch.cuda.synchronize()
     ms32 = e0.elapsed_time(e1) / args.fp32_reps
@@ -259,20 +298,25 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind as ob
     big = max(slices, key=lambda s: s.nnz_global)
-    xf = big.part64.x_full.cpu().numpy()
-    rp, ci, va = big.host
-    ci_pad = remap_columns(ci, big.bounds)[0] if world > 1 else ci
-    ref = ob.spmv(rp, ci_pad, va, xf, threads=True)
-    got = big.mat64.spmv(big.part64.x_full).cpu().numpy()[: big.r1 - big.r0]
-    bound = ob.spmv_bound(rp, ci_pad, va, xf, 2.0 ** -53)
-    check_ok = bool(np.all(np.abs(got - ref) <= bound))
+    xf = big.x64().cpu().numpy()
+    rp, ci_dev, va = big.host
+    ref = ob.spmv(rp, ci_dev, va, xf, threads=True)
+    got = big.mat64.spmv(big.x64()).cpu().numpy()[: big.m_local]
+    bound = ob.spmv_bound(rp, ci_dev, va, xf, 2.0 ** -53)
+    # the exchanged x must hold exactly the global x entries the slice references
+    ok_x = True
+    if big.mode == "halo":
+        xg = csr.dlarnv(1, [0, 0, 0, 1], big.n)[0]
+        cols = np.concatenate([c for c in big.halo.recv_cols])
+        ok_x = np.array_equal(xf[big.m_local:], xg[cols]) and np.array_equal(xf[: big.m_local], xg[big.r0:big.r1])
+    check_ok = bool(np.all(np.abs(got - ref) <= bound)) and ok_x
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(slices, args.cpu_seconds)
 
     if rank == 0:
-        traffic = pmc_traffic(args.workload)
+        traffic = pmc_traffic(args.workload) if world == 1 else None  # PMC run was N = 1
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -289,13 +333,18 @@ def main():
                     "structure family; SURVEY App. A) - no .mtx data offline",
             "config": {
                 "workload": f"{args.workload}-set CSR SpMV fp64, {len(slices)} matrices per step"
-                            + (", row-partitioned + RCCL all-gather(x)" if world > 1 else ""),
+                            + (f", row-partitioned + RCCL {args.exchange} exchange of x" if world > 1 else ""),
                 "matrices": len(slices),
                 "nnz_stored_total": int(sum(s.nnz_global for s in slices)),
                 "parallelism": f"row-partition x{world}" if world > 1 else "1 GPU",
-                "collective": (f"all_gather_into_tensor over {args.dist_backend}"
+                "collective": (("halo all_to_all_single" + ("" if args.no_bucket else
+                                 " (one per step, bucketed over the matrices)")
+                                 if args.exchange == "halo" else "all_gather_into_tensor")
+                               + f" over {args.dist_backend}"
                                + (" (RCCL, xGMI)" if args.dist_backend == "nccl" else " (rehearsal)"))
                 if world > 1 else None,
+                "halo_bytes_per_step_rank0": (sum(ex.bytes_per_exchange for _, ex in exchanges64)
+                                              if exchanges64 else None),
             },
             "hbm_gbps": round(hbm_gbs, 1),
             "roofline": {

@@ -167,6 +167,18 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t handle, const void *alpha, rsp_ilu0_inf
                             rsp_datatype_t value_type, const void *d_values, const void *d_x,
                             void *d_y);
 
+/* ------------------------------------------------ multi-GPU halo exchange */
+
+/* Indexed gather dst[i] = src[idx[i]] for i < n (value_type elements). The
+ * pack / unpack step of the row-partitioned SpMV's halo exchange (SURVEY
+ * §8e-f): pack the x entries peers need into an RCCL send buffer, and unpack
+ * the received halo into each slice's extended x. idx must be in range. */
+rsp_status_t rsp_gather(rsp_handle_t handle, rsp_datatype_t value_type, int64_t n,
+                        const int64_t *d_idx, const void *d_src, void *d_dst);
+/* Indexed scatter dst[idx[i]] = src[i] for i < n (idx without duplicates). */
+rsp_status_t rsp_scatter(rsp_handle_t handle, rsp_datatype_t value_type, int64_t n,
+                         const int64_t *d_idx, const void *d_src, void *d_dst);
+
 /* Number of dependency levels found by the analysis (L DAG, L^T DAG). */
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *levels_upper);
 

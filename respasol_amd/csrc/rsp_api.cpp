@@ -381,6 +381,24 @@ rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
 }
 
+rsp_status_t rsp_gather(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, const int64_t *d_idx,
+                        const void *d_src, void *d_dst) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    if (n < 0 || (n > 0 && (!d_idx || !d_src || !d_dst))) return RSP_STATUS_INVALID_VALUE;
+    hipError_t e = rsp_k::gather(value_type == RSP_R_64F ? 8 : 4, n, d_idx, d_src, d_dst, h->stream);
+    return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+rsp_status_t rsp_scatter(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, const int64_t *d_idx,
+                         const void *d_src, void *d_dst) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    if (n < 0 || (n > 0 && (!d_idx || !d_src || !d_dst))) return RSP_STATUS_INVALID_VALUE;
+    hipError_t e = rsp_k::scatter(value_type == RSP_R_64F ? 8 : 4, n, d_idx, d_src, d_dst, h->stream);
+    return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
 /* --------------------------------------------------------------- ILU(0) */
 
 static void ilu_free_device(rsp_ilu0_info *f) {

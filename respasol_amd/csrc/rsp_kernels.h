@@ -103,6 +103,10 @@ RSP_DECLARE_KERNEL_API(rsp_k)
 RSP_DECLARE_KERNEL_API(rsp_k_ftz)
 
 namespace rsp_k {
+hipError_t gather(int elem_bytes, int64_t n, const int64_t *idx, const void *src, void *dst,
+                  hipStream_t s);
+hipError_t scatter(int elem_bytes, int64_t n, const int64_t *idx, const void *src, void *dst,
+                   hipStream_t s);
 hipError_t spmv_f64(const rsp::SpmvArgs &a, hipStream_t s);
 hipError_t ilu0_factor_f64(const rsp::IluArgs &a, hipStream_t s);
 hipError_t trsv_lower_n_f64(const rsp::TrsvArgs &a, hipStream_t s);

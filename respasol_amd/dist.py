@@ -107,3 +107,146 @@ class RowPartitionedSpmv:
         else:
             buf[: self.chunk].copy_(pad[: self.chunk])
         return unpad(buf, self.bounds, self.chunk)
+
+
+# ----------------------------------------------------------------- halo exchange
+#
+# The all-gather above moves all of x to every rank: 8*n*(P-1)/P bytes per
+# rank per SpMV, ~10 MB for Serena at P = 8 against ~11 us of kernel time.
+# A row block of a banded / mesh matrix references only a thin "halo" of
+# columns outside its own range, so each rank needs just those x entries
+# (SURVEY §8f rank 2). Layout per slice: x_ext = [x_local (m_local) | halo (H)],
+# halo ordered by (owner rank, column); the slice's column indices are remapped
+# once (own column j -> j - r0, halo column -> m_local + position). One
+# exchange = pack (gather the entries each peer asked for) -> all_to_all_single
+# with per-peer split sizes -> unpack (scatter into each x_ext). Several slices
+# (one per matrix) share ONE all_to_all per step ("bucketed": fewer, larger
+# collectives — on xGMI the per-call latency, not bandwidth, dominates these
+# small halos). pack/unpack are librsp kernels (rsp_gather / rsp_scatter) on
+# the GPU; CPU tensors (gloo tests) use torch indexing.
+
+
+class HaloSlice:
+    """Halo analysis of one rank's row slice (global column indices)."""
+
+    def __init__(self, colidx: np.ndarray, bounds: np.ndarray, rank: int):
+        self.bounds = np.asarray(bounds, np.int64)
+        self.P = len(self.bounds) - 1
+        self.rank = rank
+        self.r0, self.r1 = int(self.bounds[rank]), int(self.bounds[rank + 1])
+        self.m_local = self.r1 - self.r0
+        ci = np.asarray(colidx, np.int64)
+        cols = np.unique(ci)
+        remote = cols[(cols < self.r0) | (cols >= self.r1)]
+        owner = np.searchsorted(self.bounds, remote, side="right") - 1
+        self.recv_cols = [remote[owner == p] for p in range(self.P)]  # sorted per owner
+        self.recv_counts = np.array([len(c) for c in self.recv_cols], np.int64)
+        self.H = int(remote.size)
+        local = (ci >= self.r0) & (ci < self.r1)
+        ext = np.empty_like(ci)
+        ext[local] = ci[local] - self.r0
+        ext[~local] = self.m_local + np.searchsorted(remote, ci[~local])
+        if self.m_local + self.H > np.iinfo(np.int32).max:
+            raise ValueError("extended x does not fit int32 indices")
+        self.colidx_ext = ext.astype(np.int32)
+        self.n_ext = self.m_local + self.H
+        self.send_local: list[np.ndarray] | None = None  # filled by HaloExchange
+
+    def halo_offsets(self) -> np.ndarray:
+        """Start of each owner's block inside the halo."""
+        return np.concatenate([[0], np.cumsum(self.recv_counts)[:-1]]).astype(np.int64)
+
+
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group) -> None:
+    if out.is_cuda and dist.get_backend(group) == "gloo":  # rehearsal path
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(host, inp.cpu(), list(out_splits), list(in_splits), group=group)
+        out.copy_(host)
+        return
+    dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=group)
+
+
+class HaloExchange:
+    """Bucketed halo exchange for the slices of several matrices on one rank.
+
+    Setup is collective (every rank constructs it with its slices in the same
+    order). `arena` holds every slice's x_ext back to back; `x_ext(i)` is slice
+    i's view, `x_local(i)` its owned part. `exchange()` refreshes every halo
+    with one all_to_all_single."""
+
+    def __init__(self, slices: list[HaloSlice], rank: int, world: int, dtype: torch.dtype,
+                 device, handle=None, group=None):
+        self.slices, self.rank, self.P, self.group = slices, rank, world, group
+        self.dtype, self.device, self.handle = dtype, torch.device(device), handle
+        self.offsets = np.concatenate([[0], np.cumsum([s.n_ext for s in slices])]).astype(np.int64)
+        self.arena = torch.zeros(max(int(self.offsets[-1]), 1), dtype=dtype, device=self.device)
+        # 1) who wants what: counts then the requested global columns
+        idx_dev = self.device if (self.device.type == "cuda" and
+                                  dist.get_backend(group) != "gloo") else torch.device("cpu")
+        want = np.stack([s.recv_counts for s in slices], axis=0) if slices else np.zeros((0, world), np.int64)
+        send_cnt = torch.empty(len(slices) * world, dtype=torch.int64, device=idx_dev)
+        # element [i*P + p] on rank r = how many columns slice i of rank r wants from p;
+        # transpose through all_to_all so rank p learns the counts it must send.
+        req = torch.from_numpy(np.ascontiguousarray(want.T.reshape(-1))).to(idx_dev)  # [p][i]
+        dist.all_to_all_single(send_cnt, req, [len(slices)] * world, [len(slices)] * world, group=group)
+        send_counts = send_cnt.cpu().numpy().reshape(world, len(slices))  # [q][i]: q wants from me
+        req_cols = np.concatenate([np.concatenate([s.recv_cols[p] for s in slices]) if slices
+                                   else np.zeros(0, np.int64) for p in range(world)]).astype(np.int64)
+        in_split = [int(want[:, p].sum()) for p in range(world)]
+        out_split = [int(send_counts[q].sum()) for q in range(world)]
+        asked = torch.empty(sum(out_split), dtype=torch.int64, device=idx_dev)
+        dist.all_to_all_single(asked, torch.from_numpy(req_cols).to(idx_dev), out_split, in_split,
+                               group=group)
+        asked = asked.cpu().numpy()
+        # 2) pack index: for dest q, slice i: positions of the asked columns in my arena
+        pack, pos = [], 0
+        for q in range(world):
+            for i, s in enumerate(slices):
+                c = int(send_counts[q, i])
+                cols = asked[pos:pos + c]
+                pos += c
+                if c and (cols.min() < s.r0 or cols.max() >= s.r1):
+                    raise RuntimeError("halo request outside the owner's rows")
+                pack.append(self.offsets[i] + (cols - s.r0))
+        self.send_split = out_split
+        self.recv_split = in_split
+        # 3) unpack index: data from source p arrives ordered (slice i, column)
+        unpack = []
+        for p in range(world):
+            for i, s in enumerate(slices):
+                c = int(s.recv_counts[p])
+                start = self.offsets[i] + s.m_local + s.halo_offsets()[p]
+                unpack.append(np.arange(start, start + c, dtype=np.int64))
+        cat = lambda a: np.concatenate(a) if a else np.zeros(0, np.int64)  # noqa: E731
+        self.pack_idx = torch.from_numpy(cat(pack)).to(self.device)
+        self.unpack_idx = torch.from_numpy(cat(unpack)).to(self.device)
+        self.sendbuf = torch.empty(max(self.pack_idx.numel(), 1), dtype=dtype, device=self.device)
+        self.recvbuf = torch.empty(max(self.unpack_idx.numel(), 1), dtype=dtype, device=self.device)
+
+    def x_ext(self, i: int) -> torch.Tensor:
+        return self.arena[int(self.offsets[i]):int(self.offsets[i + 1])]
+
+    def x_local(self, i: int) -> torch.Tensor:
+        return self.arena[int(self.offsets[i]):int(self.offsets[i]) + self.slices[i].m_local]
+
+    @property
+    def bytes_per_exchange(self) -> int:
+        return int(self.pack_idx.numel() + self.unpack_idx.numel()) * self.arena.element_size()
+
+    def exchange(self) -> None:
+        if self.P <= 1:
+            return
+        n_send, n_recv = self.pack_idx.numel(), self.unpack_idx.numel()
+        if self.device.type == "cuda":
+            from .sparse import gather, scatter
+            if n_send:
+                gather(self.handle, self.pack_idx, self.arena, self.sendbuf)
+            _a2a(self.recvbuf[:n_recv], self.sendbuf[:n_send], self.recv_split, self.send_split,
+                 self.group)
+            if n_recv:
+                scatter(self.handle, self.unpack_idx, self.recvbuf, self.arena)
+        else:  # CPU tensors: gloo tests of the host logic
+            self.sendbuf[:n_send] = self.arena[self.pack_idx]
+            dist.all_to_all_single(self.recvbuf[:n_recv], self.sendbuf[:n_send],
+                                   list(self.recv_split), list(self.send_split), group=self.group)
+            self.arena[self.unpack_idx] = self.recvbuf[:n_recv]

@@ -202,4 +202,20 @@ class Ilu0:
             pass
 
 
-__all__ = ["Handle", "SpMat", "Ilu0", "upload_csr", "RspError"]
+def gather(handle: Handle, idx: torch.Tensor, src: torch.Tensor, dst: torch.Tensor) -> None:
+    """dst[i] = src[idx[i]] (rsp_gather; idx int64, all on the device)."""
+    if idx.dtype != torch.int64 or src.dtype != dst.dtype or dst.numel() < idx.numel():
+        raise ValueError("gather: bad arguments")
+    check(rsp.rsp_gather(handle.ptr, _DT[src.dtype], idx.numel(), _ptr(idx), _ptr(src), _ptr(dst)),
+          "rsp_gather")
+
+
+def scatter(handle: Handle, idx: torch.Tensor, src: torch.Tensor, dst: torch.Tensor) -> None:
+    """dst[idx[i]] = src[i] (rsp_scatter; idx int64 without duplicates)."""
+    if idx.dtype != torch.int64 or src.dtype != dst.dtype or src.numel() < idx.numel():
+        raise ValueError("scatter: bad arguments")
+    check(rsp.rsp_scatter(handle.ptr, _DT[src.dtype], idx.numel(), _ptr(idx), _ptr(src), _ptr(dst)),
+          "rsp_scatter")
+
+
+__all__ = ["Handle", "SpMat", "Ilu0", "upload_csr", "gather", "scatter", "RspError"]

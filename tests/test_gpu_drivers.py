@@ -102,3 +102,37 @@ def test_partitioned_spmv_single_gpu(P):
     y = unpad(torch.cat(ys), bounds, chunk).cpu().numpy()
     assert np.array_equal(y, y_full)
     h.close()
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_halo_partitioned_spmv_single_gpu(P):
+    """Halo layout (x_ext = [own rows | referenced remote columns], remapped
+    column indices) through the HIP kernel for each of P slices: the
+    concatenated y equals the single-GPU y bitwise; pack/unpack via
+    rsp_gather / rsp_scatter reproduce the host-built x_ext."""
+    from respasol_amd.dist import HaloSlice
+    from respasol_amd.sparse import gather, scatter
+    name, scale = "Serena", 0.05
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+    h = Handle()
+    y_full = SpMat(h, *upload_csr(A.rowptr, A.colidx, A.values), A.n).spmv(
+        torch.from_numpy(x).cuda()).cpu().numpy()
+    bounds = csr.partition_rows(A.rowptr, P)
+    xd = torch.from_numpy(x).cuda()
+    ys = []
+    for p in range(P):
+        r0, r1 = int(bounds[p]), int(bounds[p + 1])
+        rp, ci, va = csr.surrogate_rows_csr(name, r0, r1, scale)
+        hs = HaloSlice(ci, bounds, p)
+        cols = np.concatenate([np.arange(r0, r1)] + hs.recv_cols).astype(np.int64)
+        idx = torch.from_numpy(cols).cuda()
+        x_ext = torch.empty(hs.n_ext, dtype=torch.float64, device="cuda")
+        gather(h, idx, xd, x_ext)                      # pack: global x -> x_ext
+        back = torch.zeros_like(xd)
+        scatter(h, idx, x_ext, back)                   # unpack: x_ext -> global slots
+        assert np.array_equal(back.cpu().numpy()[cols], x[cols])
+        assert np.array_equal(x_ext.cpu().numpy(), x[cols])
+        ys.append(SpMat(h, *upload_csr(rp, hs.colidx_ext, va), hs.n_ext).spmv(x_ext).cpu().numpy())
+    assert np.array_equal(np.concatenate(ys), y_full)
+    h.close()
