@@ -1,0 +1,104 @@
+"""BASELINE config 3: level-scheduled ILU(0) factor + L / L^T solves on the
+21 moderate matrices (surrogates), fp64 and fp32+FTZ, on one MI355X, with
+the oracle's sequential CPU time beside it and a bitwise parity check.
+
+    python scripts/bench_ilu0.py [--set moderate] [--reps 3] [--json out.json]
+
+Times (ms): analysis (host-side level sets, wall clock), factor and solve
+(L then L^T, the reference's "Solve", GPU/ilu0.cu:284-310) as HIP event
+pairs, median of --reps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_bind as ob  # noqa: E402  (checker + CPU reference time)
+from respasol_amd import csr  # noqa: E402
+from respasol_amd.sparse import Handle, Ilu0, upload_csr  # noqa: E402
+
+
+def run_one(h, A, dt, ftz, reps):
+    npdt = np.float64 if dt == torch.float64 else np.float32
+    h.set_ftz(ftz)
+    rp, ci, va0 = upload_csr(A.rowptr, A.colidx, A.values, dt)
+    il = Ilu0(h, rp, ci)
+    t0 = time.perf_counter()
+    il.analysis()
+    t_an = (time.perf_counter() - t0) * 1e3
+    assert il.zero_pivot() == -1
+    lev = il.levels()
+    x = torch.ones(A.n, dtype=dt, device="cuda")
+    tf, ts = [], []
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for _ in range(reps):
+        va = va0.clone()
+        torch.cuda.synchronize()
+        e[0].record()
+        il.factor(va)
+        e[1].record()
+        z = il.solve_lower(va, x)
+        y = il.solve_lower(va, z, transpose=True)
+        e[2].record()
+        torch.cuda.synchronize()
+        tf.append(e[0].elapsed_time(e[1]))
+        ts.append(e[1].elapsed_time(e[2]))
+    zp = il.zero_pivot()
+    # parity (bitwise) and the sequential CPU time of the same arithmetic
+    t0 = time.perf_counter()
+    rv, _, rzp = ob.ilu0(A.rowptr, A.colidx, A.values.astype(npdt), ftz=ftz)
+    t_cf = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    rz = ob.trsv("lower_n", A.rowptr, A.colidx, rv, np.ones(A.n, npdt), ftz=ftz)
+    ry = ob.trsv("lower_t", A.rowptr, A.colidx, rv, rz, ftz=ftz)
+    t_cs = (time.perf_counter() - t0) * 1e3
+    ok = (zp == rzp and np.array_equal(va.cpu().numpy(), rv) and np.array_equal(y.cpu().numpy(), ry))
+    h.set_ftz(False)
+    return {"analysis_ms": round(t_an, 3), "factor_ms": round(statistics.median(tf), 4),
+            "solve_ms": round(statistics.median(ts), 4), "levels_L": lev[0], "levels_LT": lev[1],
+            "cpu_factor_ms": round(t_cf, 3), "cpu_solve_ms": round(t_cs, 3), "bitwise_ok": bool(ok)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--set", default="moderate")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+    names = csr.surrogate_names(0 if args.set == "moderate" else 1) if args.set in ("moderate", "big") \
+        else args.set.split(",")
+    h = Handle()
+    out = []
+    print(f"{'matrix':16s} {'n':>8s} {'nnz_s':>9s} {'lvL':>5s} {'lvT':>5s} | "
+          f"{'fp64 fac':>9s} {'solve':>8s} | {'fp32ftz fac':>11s} {'solve':>8s} | "
+          f"{'cpu fac':>8s} {'cpu slv':>8s} ok")
+    for name in names:
+        A = csr.surrogate(name)
+        r64 = run_one(h, A, torch.float64, False, args.reps)
+        r32 = run_one(h, A, torch.float32, True, args.reps)
+        row = {"matrix": name, "n": A.m, "nnz_s": A.nnz_stored, "fp64": r64, "fp32_ftz": r32}
+        out.append(row)
+        print(f"{name:16s} {A.m:8d} {A.nnz_stored:9d} {r64['levels_L']:5d} {r64['levels_LT']:5d} | "
+              f"{r64['factor_ms']:9.3f} {r64['solve_ms']:8.3f} | {r32['factor_ms']:11.3f} "
+              f"{r32['solve_ms']:8.3f} | {r64['cpu_factor_ms']:8.2f} {r64['cpu_solve_ms']:8.2f} "
+              f"{r64['bitwise_ok'] and r32['bitwise_ok']}", flush=True)
+    tot = lambda k, p: sum(r[p][k] for r in out)  # noqa: E731
+    print(f"TOTAL fp64 factor {tot('factor_ms', 'fp64'):.2f} ms solve {tot('solve_ms', 'fp64'):.2f} ms; "
+          f"fp32+ftz factor {tot('factor_ms', 'fp32_ftz'):.2f} solve {tot('solve_ms', 'fp32_ftz'):.2f}; "
+          f"cpu(1 thread) factor {tot('cpu_factor_ms', 'fp64'):.1f} solve {tot('cpu_solve_ms', 'fp64'):.1f}")
+    if args.json:
+        json.dump(out, open(args.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
