@@ -72,29 +72,53 @@ void oracle_spmv_f32_omp(int m, const int *rp, const int *ci, const float *v, co
 
 int oracle_num_threads(void) { return omp_get_max_threads(); }
 
-/* Canonical 8-way order of the GPU tiles (spmv.hip): partial p_j sums the
- * row's products e = j, j+8, j+16, ... (e counted from the row start) in
- * increasing e; y = ((p0+p4)+(p2+p6)) + ((p1+p5)+(p3+p7)). The kernels give
- * this bit-for-bit for every row that fits one tile, whatever the tiling,
- * lanes-per-row or row partition (rows longer than a tile are chunked and
- * checked against the bound instead). */
-#define ORACLE_W8(T, NAME)                                                                     \
-    void NAME(int m, const int *rp, const int *ci, const T *v, const T *x, T *y) {             \
+/* Canonical summation order of the GPU SpMV (spmv.hip), a function of the
+ * row alone (independent of tiling, lanes per row and row partition):
+ *  - rows of <= 256 products: partial p_j sums the products e = j, j+8, ...
+ *    (e counted from the row start) in order; y = ((p0+p4)+(p2+p6)) +
+ *    ((p1+p5)+(p3+p7));
+ *  - longer rows: cut into chunks of `cap` products from the row start
+ *    (cap = 2047 fp64 / 4093 fp32, the tile capacity); in a chunk, q_t sums
+ *    products t, t+256, ... in order (t < 256), each group of 64 q's is
+ *    combined by a xor-butterfly tree (stride 32, 16, ..., 1) and the four
+ *    results as (w0+w1)+(w2+w3); the chunks are added in order from 0. */
+#define ORACLE_CANON(T, NAME)                                                                  \
+    void NAME(int m, const int *rp, const int *ci, const T *v, const T *x, T *y, int cap) {    \
         for (int i = 0; i < m; i++) {                                                          \
-            T p[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                                 \
-            for (int k = rp[i]; k < rp[i + 1]; k++) p[(k - rp[i]) & 7] += v[k] * x[ci[k]];     \
-            for (int h = 4; h >= 1; h >>= 1)                                                   \
-                for (int t = 0; t < h; t++) p[t] = p[t] + p[t + h];                            \
-            y[i] = p[0];                                                                       \
+            const int a = rp[i], len = rp[i + 1] - rp[i];                                      \
+            if (len <= 256) {                                                                  \
+                T p[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                             \
+                for (int k = a; k < a + len; k++) p[(k - a) & 7] += v[k] * x[ci[k]];           \
+                for (int h = 4; h >= 1; h >>= 1)                                               \
+                    for (int t = 0; t < h; t++) p[t] = p[t] + p[t + h];                        \
+                y[i] = p[0];                                                                   \
+                continue;                                                                      \
+            }                                                                                  \
+            T row = 0;                                                                         \
+            for (int c0 = 0; c0 < len; c0 += cap) {                                            \
+                const int c1 = c0 + cap < len ? c0 + cap : len;                                \
+                T q[256];                                                                      \
+                for (int t = 0; t < 256; t++) q[t] = 0;                                        \
+                for (int e = c0; e < c1; e++) q[(e - c0) & 255] += v[a + e] * x[ci[a + e]];     \
+                T w[4];                                                                        \
+                for (int g = 0; g < 4; g++) {                                                  \
+                    T *qq = q + 64 * g;                                                        \
+                    for (int o = 32; o >= 1; o >>= 1)                                          \
+                        for (int l = 0; l < o; l++) qq[l] = qq[l] + qq[l + o];                 \
+                    w[g] = qq[0];                                                              \
+                }                                                                              \
+                row += (w[0] + w[1]) + (w[2] + w[3]);                                          \
+            }                                                                                  \
+            y[i] = row;                                                                        \
         }                                                                                      \
     }
-ORACLE_W8(double, oracle_spmv_w8_f64)
-ORACLE_W8(float, oracle_spmv_w8_f32)
+ORACLE_CANON(double, oracle_spmv_canon_f64)
+ORACLE_CANON(float, oracle_spmv_canon_f32)
 
-void oracle_spmv_w8_f32_ftz(int m, const int *rp, const int *ci, const float *v, const float *x,
-                            float *y) {
+void oracle_spmv_canon_f32_ftz(int m, const int *rp, const int *ci, const float *v, const float *x,
+                               float *y, int cap) {
     unsigned old = ftz_enter(1);
-    oracle_spmv_w8_f32(m, rp, ci, v, x, y);
+    oracle_spmv_canon_f32(m, rp, ci, v, x, y, cap);
     ftz_leave(old);
 }
 

@@ -44,15 +44,16 @@ void oracle_spmv_f64_omp(int m, const int *rowptr, const int *colidx, const doub
 void oracle_spmv_f32_omp(int m, const int *rowptr, const int *colidx, const float *vals,
                          const float *x, float *y);
 int oracle_num_threads(void);
-/* Same products, canonical 8-way interleaved summation order (the order the
- * GPU tiles use): p_j = sum of products e = j (mod 8) from the row start, in
- * order; y = ((p0+p4)+(p2+p6)) + ((p1+p5)+(p3+p7)). */
-void oracle_spmv_w8_f64(int m, const int *rowptr, const int *colidx, const double *vals,
-                        const double *x, double *y);
-void oracle_spmv_w8_f32(int m, const int *rowptr, const int *colidx, const float *vals,
-                        const float *x, float *y);
-void oracle_spmv_w8_f32_ftz(int m, const int *rowptr, const int *colidx, const float *vals,
-                            const float *x, float *y);
+/* Same products in the CANONICAL summation order of the GPU SpMV (see
+ * rsp_oracle.c): 8-way interleave + fixed tree for rows of <= 256 products,
+ * chunked (cap = tile capacity: 2047 fp64 / 4093 fp32) 256-way interleave +
+ * wave butterflies for longer rows. The GPU result equals this bit for bit. */
+void oracle_spmv_canon_f64(int m, const int *rowptr, const int *colidx, const double *vals,
+                           const double *x, double *y, int cap);
+void oracle_spmv_canon_f32(int m, const int *rowptr, const int *colidx, const float *vals,
+                           const float *x, float *y, int cap);
+void oracle_spmv_canon_f32_ftz(int m, const int *rowptr, const int *colidx, const float *vals,
+                               const float *x, float *y, int cap);
 
 /* In-place ILU(0), IKJ, fma updates (cusparse?csrilu02, GPU/ilu0.cu:264-268).
  * Returns the first structurally missing diagonal (>= 0) without factoring,

@@ -189,11 +189,14 @@ struct SpmvBounds {
 static SpmvBounds spmv_bounds(int64_t rows, int64_t nnz, int cap) {
     // greedy packing: two consecutive size-closed tiles exceed `cap`, long
     // rows contribute <= nnz/cap + 1 chunks each side.
+    // + every row longer than kSpmvLongRow may sit in a tile of its own and
+    // close the tile before it: <= 2 * nnz / kSpmvLongRow extra tiles.
     SpmvBounds b;
     size_t q = (size_t)(nnz / cap) + 1;
+    size_t l = (size_t)(nnz / rsp::kSpmvLongRow) + 1;
     b.nlong = q;
     b.nslots = 2 * q + 1;
-    b.nblocks = 6 * q + (size_t)(rows / rsp::kSpmvMaxRows) + 8;
+    b.nblocks = 6 * q + 2 * l + (size_t)(rows / rsp::kSpmvMaxRows) + 8;
     return b;
 }
 
@@ -225,6 +228,8 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void
 }
 
 // Greedy row-block schedule over host row offsets (see spmv.hip header).
+// Rows longer than kSpmvLongRow get tiles of their own (one per tile-sized
+// chunk); the others are packed into tiles of <= cap entries / kSpmvMaxRows.
 static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock> &blocks,
                            std::vector<SpmvLongRow> &longrows, int *nslots) {
     blocks.clear();
@@ -233,7 +238,17 @@ static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock>
     int r = 0;
     while (r < m) {
         int len = rp[r + 1] - rp[r];
-        if (len > cap) {
+        if (len > rsp::kSpmvLongRow) {
+            if (len <= cap) {  // one chunk: reduced and written in place
+                SpmvBlock b;
+                b.r0 = r;
+                b.r1 = rsp::kSpmvWholeRow;
+                b.k0 = rp[r];
+                b.k1 = rp[r + 1];
+                blocks.push_back(b);
+                r++;
+                continue;
+            }
             SpmvLongRow lr;
             lr.row = r;
             lr.first = slots;
@@ -256,7 +271,7 @@ static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock>
         int start = r, nnz = 0;
         while (r < m && r - start < rsp::kSpmvMaxRows) {
             int l = rp[r + 1] - rp[r];
-            if (l > cap || nnz + l > cap) break;
+            if (l > rsp::kSpmvLongRow || nnz + l > cap) break;
             nnz += l;
             r++;
         }

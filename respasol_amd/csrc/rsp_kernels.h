@@ -12,9 +12,13 @@
 namespace rsp {
 
 // One entry of the SpMV schedule (built by rsp_spmv_preprocess).
-//   r1 >= 0 : rows [r0, r1) whose entries [k0, k1) fit one workgroup tile;
-//   r1 <  0 : chunk [k0, k1) of long row r0; its partial sum goes to
-//             partials[-(r1 + 1)] and the fixup kernel finishes the row.
+//   r1 >= 0       : rows [r0, r1) whose entries [k0, k1) fit one workgroup tile
+//                   (every row <= kSpmvLongRow entries);
+//   r1 == INT_MIN : the whole long row r0 (kSpmvLongRow < len <= tile cap),
+//                   reduced by the 256 threads and written to y directly;
+//   other r1 < 0  : chunk [k0, k1) of a row longer than a tile; its partial
+//                   goes to partials[-(r1 + 1)] and the fixup kernel adds the
+//                   chunks in order.
 struct alignas(16) SpmvBlock {
     int r0, r1, k0, k1;
 };
@@ -28,6 +32,8 @@ struct alignas(16) SpmvLongRow {
 constexpr int kSpmvThreads = 256;
 constexpr int kSpmvIter = 4;        // vectors per thread per tile
 constexpr int kSpmvMaxRows = 512;   // rows per tile (row offsets staged in LDS)
+constexpr int kSpmvLongRow = 256;   // rows longer than this get the 256-thread tree
+constexpr int kSpmvWholeRow = -2147483647 - 1;  // SpmvBlock::r1 marker (INT_MIN)
 template <typename T>
 struct SpmvTile {
     static constexpr int kVec = 16 / sizeof(T);                           // 16-B loads

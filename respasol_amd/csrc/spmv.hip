@@ -177,6 +177,36 @@ __device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int
     }
 }
 
+// A long row (or one tile-sized chunk of it) in LDS slots [a, e): thread t
+// sums slots a+t, a+t+256, ... in order, each wave combines its 64 sums with
+// a xor-butterfly (32, 16, ..., 1), and the four wave sums are added as
+// (w0+w1)+(w2+w3) — the canonical order for rows longer than kSpmvLongRow
+// (oracle_spmv_canon_*). A whole row is written to y; a chunk goes to its
+// partial slot for the in-order fixup.
+template <typename T>
+__device__ __forceinline__ void reduce_long(const T *lds, int a, int e, T *wsum,
+                                            const SpmvBlock &blk, T *__restrict__ y,
+                                            T *__restrict__ partials, T alpha, T beta,
+                                            int beta_nonzero) {
+    const int tid = threadIdx.x;
+    T s = T(0);
+    for (int k = a + tid; k < e; k += kSpmvThreads) s += lds[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
+    if ((tid & 63) == 0) wsum[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) {
+        const T t = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        if (blk.r1 == rsp::kSpmvWholeRow) {
+            T out = alpha * t;
+            if (beta_nonzero) out += beta * y[blk.r0];
+            y[blk.r0] = out;
+        } else {
+            partials[-(blk.r1 + 1)] = t;
+        }
+    }
+}
+
 template <typename T, bool NT>
 __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
@@ -214,15 +244,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     __syncthreads();
 
     if (blk.r1 < 0) {
-        // chunk of a long row: thread t sums chunk elements t, t+256, ...
-        // (relative to the chunk start), then a fixed butterfly + wave order
-        T s = T(0);
-        for (int e = (k0 - kb) + tid; e < k1 - kb; e += kSpmvThreads) s += lds[e];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
-        if ((tid & 63) == 0) wsum[tid >> 6] = s;
-        __syncthreads();
-        if (tid == 0) partials[-(blk.r1 + 1)] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        reduce_long(lds, k0 - kb, k1 - kb, wsum, blk, y, partials, alpha, beta, beta_nonzero);
         return;
     }
 
@@ -329,15 +351,9 @@ __device__ __forceinline__ void reduce_tile(const SpmvBlock &blk, int kb, const 
                                             const int *rp_lds, T *wsum, T *__restrict__ y,
                                             T *__restrict__ partials, T alpha, T beta,
                                             int beta_nonzero) {
-    const int tid = threadIdx.x;
     if (blk.r1 < 0) {
-        T s = T(0);
-        for (int e = (blk.k0 - kb) + tid; e < blk.k1 - kb; e += kSpmvThreads) s += lds[e];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
-        if ((tid & 63) == 0) wsum[tid >> 6] = s;
-        __syncthreads();
-        if (tid == 0) partials[-(blk.r1 + 1)] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+        reduce_long(lds, blk.k0 - kb, blk.k1 - kb, wsum, blk, y, partials, alpha, beta,
+                    beta_nonzero);
         return;
     }
     const int r0 = blk.r0, nrows = blk.r1 - blk.r0, nnzt = blk.k1 - blk.k0;

@@ -21,9 +21,11 @@ def _load():
     lib = C.CDLL(ORACLE_SO)
     ip, vp = C.POINTER(C.c_int), C.c_void_p
     for name in ("oracle_spmv_f64", "oracle_spmv_f32", "oracle_spmv_f32_ftz", "oracle_spmv_f64_omp",
-                 "oracle_spmv_f32_omp", "oracle_spmv_w8_f64", "oracle_spmv_w8_f32",
-                 "oracle_spmv_w8_f32_ftz"):
+                 "oracle_spmv_f32_omp"):
         getattr(lib, name).argtypes = [C.c_int, ip, ip, vp, vp, vp]
+        getattr(lib, name).restype = None
+    for name in ("oracle_spmv_canon_f64", "oracle_spmv_canon_f32", "oracle_spmv_canon_f32_ftz"):
+        getattr(lib, name).argtypes = [C.c_int, ip, ip, vp, vp, vp, C.c_int]
         getattr(lib, name).restype = None
     lib.oracle_num_threads.restype = C.c_int
     lib.oracle_ilu0_f64.argtypes = [C.c_int, ip, ip, vp, ip]
@@ -51,17 +53,20 @@ def _i(a):
 
 def spmv(rowptr, colidx, vals, x, ftz=False, threads=False, order="seq"):
     """order="seq": column order per row (the reference semantics);
-    order="w8": the canonical 8-way interleaved order of the GPU tiles."""
+    order="canon": the canonical order of the GPU kernels (bit-exact target)."""
     rp = np.ascontiguousarray(rowptr, np.int32)
     ci = np.ascontiguousarray(colidx, np.int32)
     v = np.ascontiguousarray(vals)
     xx = np.ascontiguousarray(x, v.dtype)
     m = rp.shape[0] - 1
     y = np.empty(m, v.dtype)
-    if order == "w8":
-        fn = (lib.oracle_spmv_w8_f64 if v.dtype == np.float64
-              else (lib.oracle_spmv_w8_f32_ftz if ftz else lib.oracle_spmv_w8_f32))
-    elif v.dtype == np.float64:
+    if order == "canon":
+        fn = (lib.oracle_spmv_canon_f64 if v.dtype == np.float64
+              else (lib.oracle_spmv_canon_f32_ftz if ftz else lib.oracle_spmv_canon_f32))
+        fn(m, rp.ctypes.data_as(C.POINTER(C.c_int)), ci.ctypes.data_as(C.POINTER(C.c_int)),
+           v.ctypes.data, xx.ctypes.data, y.ctypes.data, TILE_CAP[v.dtype])
+        return y
+    if v.dtype == np.float64:
         fn = lib.oracle_spmv_f64_omp if threads else lib.oracle_spmv_f64
     else:
         fn = lib.oracle_spmv_f32_ftz if ftz else (lib.oracle_spmv_f32_omp if threads else lib.oracle_spmv_f32)
