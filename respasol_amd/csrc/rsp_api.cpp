@@ -50,10 +50,15 @@ struct rsp_ilu0_info {
     int structural_zero;         // -1 = none
     int factored;
     int *d_dpos, *d_hasdiag;
-    int *d_rows_l, *d_rows_lt, *d_rows_u;
     int *d_lt_ptr, *d_lt_src, *d_lt_col;
     int *d_zero;
-    std::vector<int> lev_l, lev_lt, lev_u;  // host level pointers
+    // one level set per DAG: L (factor + L solve), L^T, U
+    struct Dag {
+        std::vector<int> ptr;                  // host level pointers
+        int *d_rows = nullptr, *d_ptr = nullptr;
+        std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
+    } L, LT, U;
+    std::vector<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
 };
 
 #define RSP_CHECK_HIP(call)                                                     \
@@ -417,8 +422,9 @@ rsp_status_t rsp_scatter(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, c
 /* --------------------------------------------------------------- ILU(0) */
 
 static void ilu_free_device(rsp_ilu0_info *f) {
-    int **ptrs[] = {&f->d_dpos,   &f->d_hasdiag, &f->d_rows_l, &f->d_rows_lt, &f->d_rows_u,
-                    &f->d_lt_ptr, &f->d_lt_src,  &f->d_lt_col, &f->d_zero};
+    int **ptrs[] = {&f->d_dpos,     &f->d_hasdiag, &f->L.d_rows,  &f->L.d_ptr,
+                    &f->LT.d_rows,  &f->LT.d_ptr,  &f->U.d_rows,  &f->U.d_ptr,
+                    &f->d_lt_ptr,   &f->d_lt_src,  &f->d_lt_col,  &f->d_zero};
     for (int **p : ptrs) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
@@ -432,7 +438,7 @@ rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
     f->analysed = 0;
     f->structural_zero = -1;
     f->factored = 0;
-    f->d_dpos = f->d_hasdiag = f->d_rows_l = f->d_rows_lt = f->d_rows_u = nullptr;
+    f->d_dpos = f->d_hasdiag = nullptr;
     f->d_lt_ptr = f->d_lt_src = f->d_lt_col = f->d_zero = nullptr;
     *info = f;
     return RSP_STATUS_SUCCESS;
@@ -463,6 +469,21 @@ static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int>
     std::vector<int> fill(ptr.begin(), ptr.end() - 1);
     rows.assign(lev.size(), 0);
     for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
+}
+
+// Consecutive levels of at most thin_max rows form one thin run (one
+// single-workgroup launch); the other levels are launched one by one.
+static std::vector<rsp::LevelSeg> make_segs(const std::vector<int> &ptr, int thin_max) {
+    std::vector<rsp::LevelSeg> segs;
+    const int nlev = (int)ptr.size() - 1;
+    for (int l = 0; l < nlev; l++) {
+        const int thin = (ptr[(size_t)l + 1] - ptr[(size_t)l]) <= thin_max ? 1 : 0;
+        if (!segs.empty() && segs.back().thin == thin && segs.back().le == l)
+            segs.back().le = l + 1;
+        else
+            segs.push_back({l, l + 1, thin});
+    }
+    return segs;
 }
 
 static hipError_t upload(int **dst, const std::vector<int> &v) {
@@ -554,15 +575,22 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         nlu = std::max(nlu, l + 1);
     }
     std::vector<int> rows_l, rows_lt, rows_u;
-    group_levels(lv, nl, f->lev_l, rows_l);
-    group_levels(lvt, nlt, f->lev_lt, rows_lt);
-    group_levels(lvu, nlu, f->lev_u, rows_u);
+    group_levels(lv, nl, f->L.ptr, rows_l);
+    group_levels(lvt, nlt, f->LT.ptr, rows_lt);
+    group_levels(lvu, nlu, f->U.ptr, rows_u);
+    f->L.segs = make_segs(f->L.ptr, rsp::kThinSolveRows);
+    f->LT.segs = make_segs(f->LT.ptr, rsp::kThinSolveRows);
+    f->U.segs = make_segs(f->U.ptr, rsp::kThinSolveRows);
+    f->fac_segs = make_segs(f->L.ptr, rsp::kThinFactorRows);
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
     if (e == hipSuccess) e = upload(&f->d_hasdiag, hasdiag);
-    if (e == hipSuccess) e = upload(&f->d_rows_l, rows_l);
-    if (e == hipSuccess) e = upload(&f->d_rows_lt, rows_lt);
-    if (e == hipSuccess) e = upload(&f->d_rows_u, rows_u);
+    if (e == hipSuccess) e = upload(&f->L.d_rows, rows_l);
+    if (e == hipSuccess) e = upload(&f->L.d_ptr, f->L.ptr);
+    if (e == hipSuccess) e = upload(&f->LT.d_rows, rows_lt);
+    if (e == hipSuccess) e = upload(&f->LT.d_ptr, f->LT.ptr);
+    if (e == hipSuccess) e = upload(&f->U.d_rows, rows_u);
+    if (e == hipSuccess) e = upload(&f->U.d_ptr, f->U.ptr);
     if (e == hipSuccess) e = upload(&f->d_lt_ptr, ltp);
     if (e == hipSuccess) e = upload(&f->d_lt_src, lts);
     if (e == hipSuccess) e = upload(&f->d_lt_col, ltc);
@@ -582,8 +610,8 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
 
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t f, int *levels_lower, int *levels_upper) {
     if (!f || !f->analysed) return RSP_STATUS_INVALID_VALUE;
-    if (levels_lower) *levels_lower = (int)f->lev_l.size() - 1;
-    if (levels_upper) *levels_upper = (int)f->lev_lt.size() - 1;
+    if (levels_lower) *levels_lower = (int)f->L.ptr.size() - 1;
+    if (levels_upper) *levels_upper = (int)f->LT.ptr.size() - 1;
     return RSP_STATUS_SUCCESS;
 }
 
@@ -606,6 +634,17 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
     return RSP_STATUS_SUCCESS;
 }
 
+static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<rsp::LevelSeg> &segs) {
+    rsp::LevelPlan p;
+    p.rows = d.d_rows;
+    p.ptr_dev = d.d_ptr;
+    p.ptr_host = d.ptr.data();
+    p.nlev = (int)d.ptr.size() - 1;
+    p.segs = segs.data();
+    p.nseg = (int)segs.size();
+    return p;
+}
+
 rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
                              void *d_values) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
@@ -620,9 +659,7 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.hasdiag = f->d_hasdiag;
     a.vals = d_values;
     a.zero_pivot = f->d_zero;
-    a.level_rows = f->d_rows_l;
-    a.level_ptr_host = f->lev_l.data();
-    a.nlev = (int)f->lev_l.size() - 1;
+    a.plan = level_plan(f->L, f->fac_segs);
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::ilu0_factor_f64(a, h->stream);
@@ -647,9 +684,7 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.lt_ptr = f->d_lt_ptr;
     a.lt_src = f->d_lt_src;
     a.lt_col = f->d_lt_col;
-    a.level_rows = nullptr;
-    a.level_ptr_host = nullptr;
-    a.nlev = 0;
+    a.plan = level_plan(f->L, f->L.segs);
     return a;
 }
 
@@ -664,15 +699,10 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
     hipError_t e;
     const bool f64 = value_type == RSP_R_64F, ftz = h->ftz != 0;
     if (op == RSP_OPERATION_NON_TRANSPOSE) {
-        a.level_rows = f->d_rows_l;
-        a.level_ptr_host = f->lev_l.data();
-        a.nlev = (int)f->lev_l.size() - 1;
         e = f64 ? rsp_k::trsv_lower_n_f64(a, h->stream)
                 : (ftz ? rsp_k_ftz::trsv_lower_n_f32(a, h->stream) : rsp_k::trsv_lower_n_f32(a, h->stream));
     } else if (op == RSP_OPERATION_TRANSPOSE) {
-        a.level_rows = f->d_rows_lt;
-        a.level_ptr_host = f->lev_lt.data();
-        a.nlev = (int)f->lev_lt.size() - 1;
+        a.plan = level_plan(f->LT, f->LT.segs);
         e = f64 ? rsp_k::trsv_lower_t_f64(a, h->stream)
                 : (ftz ? rsp_k_ftz::trsv_lower_t_f32(a, h->stream) : rsp_k::trsv_lower_t_f32(a, h->stream));
     } else {
@@ -689,9 +719,7 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
-    a.level_rows = f->d_rows_u;
-    a.level_ptr_host = f->lev_u.data();
-    a.nlev = (int)f->lev_u.size() - 1;
+    a.plan = level_plan(f->U, f->U.segs);
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::trsv_upper_f64(a, h->stream);

@@ -61,6 +61,27 @@ struct SpmvArgs {
     int num_cus;    // compute units of the device (persistent grid sizing)
 };
 
+// Level schedule of one dependency DAG. Rows are grouped by level
+// (rows[ptr[l] .. ptr[l+1])); `segs` (host) cover the levels in order, each
+// {lev_begin, lev_end, thin}: a thin segment is a run of small levels that
+// one 1024-thread workgroup walks with __syncthreads() between levels (one
+// launch for the whole run); a fat segment is one launch per level.
+struct LevelSeg {
+    int lb, le, thin;
+};
+struct LevelPlan {
+    const int *rows;      // device
+    const int *ptr_dev;   // device, nlev + 1
+    const int *ptr_host;  // host, nlev + 1
+    int nlev;
+    const LevelSeg *segs; // host
+    int nseg;
+};
+constexpr int kThinThreads = 1024;  // workgroup of a thin segment
+constexpr int kIluWaves = 4;        // rows per 256-thread workgroup (fat factor levels)
+constexpr int kThinSolveRows = 2048;  // solve levels this small run inside a thin segment
+constexpr int kThinFactorRows = 64;   // factor levels (a wave per row: 16 rows per pass)
+
 struct IluArgs {
     int n;
     const int *rowptr;
@@ -69,9 +90,7 @@ struct IluArgs {
     const int *hasdiag;   // 1 if colidx[dpos[i]] == i
     void *vals;
     int *zero_pivot;      // device int, atomicMin target (INT_MAX = none)
-    const int *level_rows;        // rows grouped by level (L DAG)
-    const int *level_ptr_host;    // nlev + 1 offsets, HOST memory
-    int nlev;
+    LevelPlan plan;       // L DAG, factor thresholds
 };
 
 struct TrsvArgs {
@@ -89,9 +108,7 @@ struct TrsvArgs {
     const int *lt_ptr;
     const int *lt_src;
     const int *lt_col;
-    const int *level_rows;
-    const int *level_ptr_host;
-    int nlev;
+    LevelPlan plan;
 };
 
 }  // namespace rsp
