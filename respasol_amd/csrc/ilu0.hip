@@ -19,6 +19,9 @@
 // Arithmetic (identical in the CPU oracle, so results are bitwise equal):
 //   factor, row i, k ascending over its lower entries:
 //       l_ik = a_ik / u_kk;  a_ij = fma(-l_ik, u_kj, a_ij) for j > k in row k ∩ row i
+//   evaluated in pull form: every position applies its own precomputed update
+//   list in k order (same fma sequence per position), so the positions of a
+//   row run in parallel lanes except where l_ij needs an l_ik of its own row.
 //   L   y = alpha x : y_i = fma(-l_ij, y_j, ...) over j ascending, from alpha*x_i
 //   L^T y = alpha x : y_i = fma(-l_ji, y_j, ...) over j DESCENDING, from alpha*x_i
 //   U   y = alpha x : y_i = (alpha*x_i - sum_j>i u_ij y_j) / u_ii, j ascending
@@ -44,196 +47,264 @@ using rsp::kThinThreads;
 using rsp::LevelPlan;
 using rsp::TrsvArgs;
 
-// position of column j in the sorted range cols[lo, hi), or -1
-__device__ __forceinline__ int find_col(const int *__restrict__ cols, int lo, int hi, int j) {
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const int c = cols[mid];
-        if (c == j) return mid;
-        if (c < j)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return -1;
-}
-
 // ------------------------------------------------------------ per-row work
 
-// ILU(0) of row i by one wave (lane = 0..63).
-template <typename T>
-__device__ __forceinline__ void factor_row(int i, int lane, const int *__restrict__ rowptr,
-                                           const int *__restrict__ colidx,
-                                           const int *__restrict__ dpos,
-                                           const int *__restrict__ hasdiag, T *vals,
-                                           int *zero_pivot) {
-    const int rs = rowptr[i], re = rowptr[i + 1], di = dpos[i];
-    for (int p = rs; p < di; ++p) {
-        const int k = colidx[p];
-        const T ukk = hasdiag[k] ? vals[dpos[k]] : T(0);
-        const T lik = vals[p] / ukk;
-        // row k's upper part, lanes in parallel; each j hits a distinct a_ij
-        const int q0 = dpos[k] + hasdiag[k], q1 = rowptr[k + 1];
-        for (int q = q0 + lane; q < q1; q += 64) {
-            const int pos = find_col(colidx, p + 1, re, colidx[q]);
-            if (pos >= 0) vals[pos] = __builtin_fma(-lik, vals[q], vals[pos]);
+// s - sum_p v_p y_p as a serial fma chain over p = p0 .. p1-1, ascending.
+// The operands of B consecutive terms are loaded together (clamped,
+// unpredicated) so the loads of a batch overlap instead of serialising
+// behind each fma; B is picked per DAG from its mean chain length so short
+// rows do not pay for dead loads.
+template <typename T, int B, typename FV, typename FY>
+__device__ __forceinline__ T fma_chain(T s, int p0, int p1, FV vat, FY yat) {
+    const int n = p1 - p0;
+    for (int b0 = 0; b0 < n; b0 += B) {
+        T v[B], y[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int p = p0 + min(b0 + b, n - 1);
+            v[b] = vat(p);
+            y[b] = yat(p);
         }
-        if (lane == 0) vals[p] = lik;
-        // make this step's stores visible to the wave's next loads
-        __threadfence_block();
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (b0 + b < n) s = __builtin_fma(-v[b], y[b], s);
     }
-    if (lane == 0 && hasdiag[i] && vals[di] == T(0)) atomicMin(zero_pivot, i);
+    return s;
 }
 
-template <typename T>
-__device__ __forceinline__ void lower_n_row(int i, const int *__restrict__ rowptr,
-                                            const int *__restrict__ colidx,
-                                            const int *__restrict__ dpos,
-                                            const T *__restrict__ vals, const T *__restrict__ x,
-                                            T *y, T alpha) {
-    T s = alpha * x[i];
-    const int e = dpos[i];
-    for (int p = rowptr[i]; p < e; ++p) s = __builtin_fma(-vals[p], y[colidx[p]], s);
-    y[i] = s;
+// One position of the factor, pull form: v = a_p - sum_k l_ik u_kj over the
+// position's update list (k ascending, one fma each — the same sequence of
+// roundings as the IKJ loop).
+template <typename T, int B>
+__device__ __forceinline__ T factor_entry(const IluArgs &a, const T *vals, int p) {
+    const int *ul = a.upd_l, *uu = a.upd_u;
+    return fma_chain<T, B>(vals[p], a.upd_ptr[p], a.upd_ptr[p + 1],
+                           [&](int u) { return vals[ul[u]]; },
+                           [&](int u) { return vals[uu[u]]; });
 }
 
-template <typename T>
-__device__ __forceinline__ void lower_t_row(int i, const int *__restrict__ lt_ptr,
-                                            const int *__restrict__ lt_src,
-                                            const int *__restrict__ lt_col,
-                                            const T *__restrict__ vals, const T *__restrict__ x,
-                                            T *y, T alpha) {
-    T s = alpha * x[i];
-    for (int q = lt_ptr[i]; q < lt_ptr[i + 1]; ++q)
-        s = __builtin_fma(-vals[lt_src[q]], y[lt_col[q]], s);
-    y[i] = s;
+// ILU(0) of row i by the 64 lanes of a wave: lower positions stage by stage
+// (a stage's positions depend only on earlier stages of the row and on
+// earlier rows), l_ij = v / u_jj, then every upper position at once.
+template <typename T, int B>
+__device__ __forceinline__ void factor_row(const IluArgs &a, int i, int lane) {
+    T *vals = (T *)a.vals;
+    const int rs = a.rowptr[i], re = a.rowptr[i + 1], di = a.dpos[i];
+    for (int s = rs; s < di;) {
+        const int e = a.lend[s];
+        for (int x = s + lane; x < e; x += 64) {
+            const int p = a.lord[x];
+            const int k = a.colidx[p];
+            const T ukk = a.hasdiag[k] ? vals[a.dpos[k]] : T(0);
+            vals[p] = factor_entry<T, B>(a, vals, p) / ukk;
+        }
+        // this stage's l_ik visible to the next stage's lanes
+        __threadfence_block();
+        s = e;
+    }
+    for (int p = di + lane; p < re; p += 64) {
+        const T v = factor_entry<T, B>(a, vals, p);
+        vals[p] = v;
+        if (p == di && a.hasdiag[i] && v == T(0)) atomicMin(a.zero_pivot, i);
+    }
 }
 
-template <typename T>
-__device__ __forceinline__ void upper_row(int i, const int *__restrict__ rowptr,
-                                          const int *__restrict__ colidx,
-                                          const int *__restrict__ dpos,
-                                          const int *__restrict__ hasdiag,
-                                          const T *__restrict__ vals, const T *__restrict__ x, T *y,
-                                          T alpha) {
-    T s = alpha * x[i];
-    const int d = dpos[i], hd = hasdiag[i];
-    for (int p = d + hd; p < rowptr[i + 1]; ++p) s = __builtin_fma(-vals[p], y[colidx[p]], s);
-    y[i] = s / (hd ? vals[d] : T(0));
+// Triangular solve of one row task. kind: 0 = L (op N), 1 = L^T (op T), 2 = U.
+// The structural operands of the first B terms (and x_i, u_ii) are fetched
+// by solve_fetch — for a thin run one level AHEAD, while the previous level
+// computes — so a level's critical path is only its y loads.
+template <typename T, int B>
+struct SolvePre {
+    rsp::RowTask t;
+    T xv, dv;
+    T v[B];
+    int c[B];
+};
+
+__device__ __forceinline__ rsp::RowTask load_task(const TrsvArgs &a, int slot, bool ok) {
+    rsp::RowTask t;
+    t.i = -1;
+    if (ok) t = a.plan.tasks[slot];
+    return t;
+}
+
+template <typename T, int KIND, int B>
+__device__ __forceinline__ void solve_fetch(const TrsvArgs &a, const rsp::RowTask &t, SolvePre<T, B> &f) {
+    f.t = t;
+    if (t.i < 0) return;
+    const T *vals = (const T *)a.vals;
+    f.xv = ((const T *)a.x)[t.i];
+    f.dv = (KIND == 2 && t.d >= 0) ? vals[t.d] : T(0);
+    const int n = t.p1 - t.p0;
+    if (n <= 0) return;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int q = t.p0 + min(b, n - 1);
+        if constexpr (KIND == 1) {
+            f.c[b] = a.lt_col[q];
+            f.v[b] = vals[a.lt_src[q]];
+        } else {
+            f.c[b] = a.colidx[q];
+            f.v[b] = vals[q];
+        }
+    }
+}
+
+template <typename T, int KIND, int B>
+__device__ __forceinline__ void solve_compute(const TrsvArgs &a, const SolvePre<T, B> &f, T alpha) {
+    if (f.t.i < 0) return;
+    const T *vals = (const T *)a.vals;
+    T *y = (T *)a.y;
+    T s = alpha * f.xv;
+    const int n = f.t.p1 - f.t.p0;
+    if (n > 0) {
+        T yy[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) yy[b] = y[f.c[b]];
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (b < n) s = __builtin_fma(-f.v[b], yy[b], s);
+        if (n > B) {
+            if constexpr (KIND == 1) {
+                const int *src = a.lt_src, *col = a.lt_col;
+                s = fma_chain<T, B>(s, f.t.p0 + B, f.t.p1, [&](int q) { return vals[src[q]]; },
+                                    [&](int q) { return y[col[q]]; });
+            } else {
+                const int *ci = a.colidx;
+                s = fma_chain<T, B>(s, f.t.p0 + B, f.t.p1, [&](int p) { return vals[p]; },
+                                    [&](int p) { return y[ci[p]]; });
+            }
+        }
+    }
+    if constexpr (KIND == 2) s = s / f.dv;
+    y[f.t.i] = s;
 }
 
 // --------------------------------------------------------------- kernels
 
 // Fat level: one wave per row.
-template <typename T>
-__global__ __launch_bounds__(64 * kIluWaves) void ilu0_level(
-    const int *__restrict__ rowptr, const int *__restrict__ colidx, const int *__restrict__ dpos,
-    const int *__restrict__ hasdiag, T *vals, int *zero_pivot, const int *__restrict__ rows,
-    int nrows) {
+template <typename T, int B>
+__global__ __launch_bounds__(64 * kIluWaves) void ilu0_level(IluArgs a, int off, int nrows) {
     const int w = blockIdx.x * kIluWaves + (threadIdx.x >> 6);
     if (w >= nrows) return;
-    factor_row<T>(rows[w], threadIdx.x & 63, rowptr, colidx, dpos, hasdiag, vals, zero_pivot);
+    factor_row<T, B>(a, a.plan.rows[off + w], threadIdx.x & 63);
 }
 
 // Thin run of levels [lb, le): one workgroup, 16 waves, one row per wave per pass.
-template <typename T>
-__global__ __launch_bounds__(kThinThreads) void ilu0_thin(
-    const int *__restrict__ rowptr, const int *__restrict__ colidx, const int *__restrict__ dpos,
-    const int *__restrict__ hasdiag, T *vals, int *zero_pivot, const int *__restrict__ rows,
-    const int *__restrict__ ptr, int lb, int le) {
+template <typename T, int B>
+__global__ __launch_bounds__(kThinThreads) void ilu0_thin(IluArgs a, int lb, int le) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int l = lb; l < le; ++l) {
-        const int off = ptr[l], cnt = ptr[l + 1] - off;
-        for (int r = wave; r < cnt; r += kThinThreads / 64)
-            factor_row<T>(rows[off + r], lane, rowptr, colidx, dpos, hasdiag, vals, zero_pivot);
+        const int off = a.plan.ptr_dev[l], cnt = a.plan.ptr_dev[l + 1] - off;
+        for (int r = wave; r < cnt; r += kThinThreads / 64) factor_row<T, B>(a, a.plan.rows[off + r], lane);
         __syncthreads();
     }
 }
 
-// kind: 0 = L (op N), 1 = L^T (op T), 2 = U
-template <typename T, int KIND>
-__device__ __forceinline__ void solve_row(const TrsvArgs &a, int i, T alpha) {
-    if constexpr (KIND == 0)
-        lower_n_row<T>(i, a.rowptr, a.colidx, a.dpos, (const T *)a.vals, (const T *)a.x, (T *)a.y,
-                       alpha);
-    else if constexpr (KIND == 1)
-        lower_t_row<T>(i, a.lt_ptr, a.lt_src, a.lt_col, (const T *)a.vals, (const T *)a.x,
-                       (T *)a.y, alpha);
-    else
-        upper_row<T>(i, a.rowptr, a.colidx, a.dpos, a.hasdiag, (const T *)a.vals, (const T *)a.x,
-                     (T *)a.y, alpha);
-}
-
-template <typename T, int KIND>
+// Fat level: one thread per row.
+template <typename T, int KIND, int B>
 __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, T alpha, int off, int nrows) {
     const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= nrows) return;
-    solve_row<T, KIND>(a, a.plan.rows[off + t], alpha);
+    SolvePre<T, B> f;
+    solve_fetch<T, KIND, B>(a, load_task(a, off + t, t < nrows), f);
+    solve_compute<T, KIND, B>(a, f, alpha);
 }
 
-template <typename T, int KIND>
+// Thin run of levels [lb, le), each <= kThinThreads rows: thread t owns row
+// t of every level. Software pipeline over levels: while level l computes,
+// level l+1's operands and level l+2's task are already in flight.
+template <typename T, int KIND, int B>
 __global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, int lb, int le) {
+    const int t = threadIdx.x;
+    const int *ptr = a.plan.ptr_dev;
+    auto task_of = [&](int l) {
+        if (l >= le) return load_task(a, 0, false);
+        const int off = ptr[l];
+        return load_task(a, off + t, off + t < ptr[l + 1]);
+    };
+    SolvePre<T, B> cur, nxt;
+    solve_fetch<T, KIND, B>(a, task_of(lb), cur);
+    rsp::RowTask t1 = task_of(lb + 1);
     for (int l = lb; l < le; ++l) {
-        const int off = a.plan.ptr_dev[l], cnt = a.plan.ptr_dev[l + 1] - off;
-        for (int t = threadIdx.x; t < cnt; t += kThinThreads) solve_row<T, KIND>(a, a.plan.rows[off + t], alpha);
+        const rsp::RowTask t2 = task_of(l + 2);
+        solve_fetch<T, KIND, B>(a, t1, nxt);
+        solve_compute<T, KIND, B>(a, cur, alpha);
         __syncthreads();
+        cur = nxt;
+        t1 = t2;
     }
 }
 
 // --------------------------------------------------------------- launchers
 
-template <typename T>
+template <typename T, int B>
 static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
     const LevelPlan &P = a.plan;
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
-            hipLaunchKernelGGL((ilu0_thin<T>), dim3(1), dim3(kThinThreads), 0, s, a.rowptr,
-                               a.colidx, a.dpos, a.hasdiag, (T *)a.vals, a.zero_pivot, P.rows,
-                               P.ptr_dev, sg.lb, sg.le);
+            hipLaunchKernelGGL((ilu0_thin<T, B>), dim3(1), dim3(kThinThreads), 0, s, a, sg.lb, sg.le);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {
             const int off = P.ptr_host[l], cnt = P.ptr_host[l + 1] - off;
             if (cnt <= 0) continue;
-            hipLaunchKernelGGL((ilu0_level<T>), dim3((cnt + kIluWaves - 1) / kIluWaves),
-                               dim3(64 * kIluWaves), 0, s, a.rowptr, a.colidx, a.dpos, a.hasdiag,
-                               (T *)a.vals, a.zero_pivot, P.rows + off, cnt);
+            hipLaunchKernelGGL((ilu0_level<T, B>), dim3((cnt + kIluWaves - 1) / kIluWaves),
+                               dim3(64 * kIluWaves), 0, s, a, off, cnt);
         }
     }
     return hipGetLastError();
 }
 
-template <typename T, int KIND>
+template <typename T, int KIND, int B>
 static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
     const LevelPlan &P = a.plan;
     const T alpha = (T)a.alpha;
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
-            hipLaunchKernelGGL((trsv_thin<T, KIND>), dim3(1), dim3(kThinThreads), 0, s, a, alpha,
-                               sg.lb, sg.le);
+            hipLaunchKernelGGL((trsv_thin<T, KIND, B>), dim3(1), dim3(kThinThreads), 0, s, a,
+                               alpha, sg.lb, sg.le);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {
             const int off = P.ptr_host[l], cnt = P.ptr_host[l + 1] - off;
             if (cnt <= 0) continue;
-            hipLaunchKernelGGL((trsv_level<T, KIND>), dim3((cnt + 255) / 256), dim3(256), 0, s, a,
-                               alpha, off, cnt);
+            hipLaunchKernelGGL((trsv_level<T, KIND, B>), dim3((cnt + 255) / 256), dim3(256), 0, s,
+                               a, alpha, off, cnt);
         }
     }
     return hipGetLastError();
 }
 
-hipError_t ilu0_factor_f32(const IluArgs &a, hipStream_t s) { return launch_factor<float>(a, s); }
-hipError_t trsv_lower_n_f32(const TrsvArgs &a, hipStream_t s) { return launch_solve<float, 0>(a, s); }
-hipError_t trsv_lower_t_f32(const TrsvArgs &a, hipStream_t s) { return launch_solve<float, 1>(a, s); }
-hipError_t trsv_upper_f32(const TrsvArgs &a, hipStream_t s) { return launch_solve<float, 2>(a, s); }
+// batch width from the plan (2, 4 or 8)
+template <typename T>
+static hipError_t factor_dispatch(const IluArgs &a, hipStream_t s) {
+    switch (a.plan.batch) {
+        case 2: return launch_factor<T, 2>(a, s);
+        case 4: return launch_factor<T, 4>(a, s);
+        default: return launch_factor<T, 8>(a, s);
+    }
+}
+
+template <typename T, int KIND>
+static hipError_t solve_dispatch(const TrsvArgs &a, hipStream_t s) {
+    switch (a.plan.batch) {
+        case 2: return launch_solve<T, KIND, 2>(a, s);
+        case 4: return launch_solve<T, KIND, 4>(a, s);
+        default: return launch_solve<T, KIND, 8>(a, s);
+    }
+}
+
+hipError_t ilu0_factor_f32(const IluArgs &a, hipStream_t s) { return factor_dispatch<float>(a, s); }
+hipError_t trsv_lower_n_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 0>(a, s); }
+hipError_t trsv_lower_t_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 1>(a, s); }
+hipError_t trsv_upper_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 2>(a, s); }
 #ifndef RSP_FTZ_BUILD
-hipError_t ilu0_factor_f64(const IluArgs &a, hipStream_t s) { return launch_factor<double>(a, s); }
-hipError_t trsv_lower_n_f64(const TrsvArgs &a, hipStream_t s) { return launch_solve<double, 0>(a, s); }
-hipError_t trsv_lower_t_f64(const TrsvArgs &a, hipStream_t s) { return launch_solve<double, 1>(a, s); }
-hipError_t trsv_upper_f64(const TrsvArgs &a, hipStream_t s) { return launch_solve<double, 2>(a, s); }
+hipError_t ilu0_factor_f64(const IluArgs &a, hipStream_t s) { return factor_dispatch<double>(a, s); }
+hipError_t trsv_lower_n_f64(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<double, 0>(a, s); }
+hipError_t trsv_lower_t_f64(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<double, 1>(a, s); }
+hipError_t trsv_upper_f64(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<double, 2>(a, s); }
 #endif
 
 }  // namespace RSP_KNS

@@ -51,14 +51,19 @@ struct rsp_ilu0_info {
     int factored;
     int *d_dpos, *d_hasdiag;
     int *d_lt_ptr, *d_lt_src, *d_lt_col;
+    int *d_upd_ptr, *d_upd_l, *d_upd_u, *d_lord, *d_lend;
     int *d_zero;
+    long long n_updates;
     // one level set per DAG: L (factor + L solve), L^T, U
     struct Dag {
         std::vector<int> ptr;                  // host level pointers
         int *d_rows = nullptr, *d_ptr = nullptr;
+        rsp::RowTask *d_tasks = nullptr;
         std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
+        int batch = 8;                         // solve fma-chain batch
     } L, LT, U;
     std::vector<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
+    int fac_batch;
 };
 
 #define RSP_CHECK_HIP(call)                                                     \
@@ -424,10 +429,16 @@ rsp_status_t rsp_scatter(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, c
 static void ilu_free_device(rsp_ilu0_info *f) {
     int **ptrs[] = {&f->d_dpos,     &f->d_hasdiag, &f->L.d_rows,  &f->L.d_ptr,
                     &f->LT.d_rows,  &f->LT.d_ptr,  &f->U.d_rows,  &f->U.d_ptr,
-                    &f->d_lt_ptr,   &f->d_lt_src,  &f->d_lt_col,  &f->d_zero};
+                    &f->d_lt_ptr,   &f->d_lt_src,  &f->d_lt_col,  &f->d_zero,
+                    &f->d_upd_ptr,  &f->d_upd_l,   &f->d_upd_u,   &f->d_lord,
+                    &f->d_lend};
     for (int **p : ptrs) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
+    }
+    for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) {
+        if (d->d_tasks) (void)hipFree(d->d_tasks);
+        d->d_tasks = nullptr;
     }
 }
 
@@ -440,6 +451,8 @@ rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
     f->factored = 0;
     f->d_dpos = f->d_hasdiag = nullptr;
     f->d_lt_ptr = f->d_lt_src = f->d_lt_col = f->d_zero = nullptr;
+    f->d_upd_ptr = f->d_upd_l = f->d_upd_u = f->d_lord = f->d_lend = nullptr;
+    f->n_updates = 0;
     *info = f;
     return RSP_STATUS_SUCCESS;
 }
@@ -486,12 +499,94 @@ static std::vector<rsp::LevelSeg> make_segs(const std::vector<int> &ptr, int thi
     return segs;
 }
 
+static int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+// fma-chain batch for a mean chain length of total / count
+static int chain_batch(long long total, long long count) {
+    const double mean = count > 0 ? (double)total / (double)count : 0.0;
+    return mean <= 2.5 ? 2 : (mean <= 5.0 ? 4 : 8);
+}
+
 static hipError_t upload(int **dst, const std::vector<int> &v) {
     size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(int);
     hipError_t e = hipMalloc((void **)dst, bytes);
     if (e != hipSuccess) return e;
     if (!v.empty()) e = hipMemcpy(*dst, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice);
     return e;
+}
+
+// Symbolic ILU(0): the update list of every position (see IluArgs) and the
+// intra-row stages of the lower positions. Row i is scattered into a dense
+// column -> position map, then each lower k (ascending) walks row k's upper
+// part; a hit at column j appends (pos l_ik, pos u_kj) to position (i, j).
+struct IluSymbolic {
+    std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
+};
+
+static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<int> &ci,
+                         const std::vector<int> &dpos, const std::vector<int> &hasdiag,
+                         IluSymbolic &s) {
+    const int nnz = rp[(size_t)n];
+    std::vector<int> map((size_t)n, -1), cnt((size_t)nnz, 0);
+    // pass 1: counts
+    long long total = 0;
+    for (int i = 0; i < n; i++) {
+        for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
+        for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) {
+            const int k = ci[(size_t)p];
+            for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
+                const int t = map[(size_t)ci[(size_t)q]];
+                if (t > p) {
+                    cnt[(size_t)t]++;
+                    total++;
+                }
+            }
+        }
+        for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
+    }
+    if (total > INT_MAX) return false;
+    s.upd_ptr.assign((size_t)nnz + 1, 0);
+    for (int p = 0; p < nnz; p++) s.upd_ptr[(size_t)p + 1] = s.upd_ptr[(size_t)p] + cnt[(size_t)p];
+    s.upd_l.resize((size_t)total);
+    s.upd_u.resize((size_t)total);
+    std::vector<int> fill(s.upd_ptr.begin(), s.upd_ptr.end() - 1);
+    // pass 2: fill (k ascending per target, since p ascends) + stages
+    std::vector<int> stage((size_t)nnz, 0);
+    s.lord.assign((size_t)nnz, 0);
+    s.lend.assign((size_t)nnz, 0);
+    std::vector<int> order;
+    for (int i = 0; i < n; i++) {
+        const int rs = rp[(size_t)i], di = dpos[(size_t)i];
+        for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
+        for (int p = rs; p < di; p++) {
+            const int k = ci[(size_t)p];
+            for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
+                const int t = map[(size_t)ci[(size_t)q]];
+                if (t > p) {
+                    const int u = fill[(size_t)t]++;
+                    s.upd_l[(size_t)u] = p;
+                    s.upd_u[(size_t)u] = q;
+                    if (t < di) stage[(size_t)t] = std::max(stage[(size_t)t], stage[(size_t)p] + 1);
+                }
+            }
+        }
+        for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
+        // lower positions by (stage, column)
+        order.assign((size_t)(di - rs), 0);
+        for (int p = rs; p < di; p++) order[(size_t)(p - rs)] = p;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int a, int b) { return stage[(size_t)a] < stage[(size_t)b]; });
+        for (int x = 0; x < di - rs; x++) s.lord[(size_t)(rs + x)] = order[(size_t)x];
+        for (int x = di - rs - 1; x >= 0; x--) {
+            const bool last = x == di - rs - 1 ||
+                              stage[(size_t)order[(size_t)x]] != stage[(size_t)order[(size_t)x + 1]];
+            s.lend[(size_t)(rs + x)] = last ? rs + x + 1 : s.lend[(size_t)(rs + x + 1)];
+        }
+    }
+    return true;
 }
 
 rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_offsets,
@@ -578,11 +673,32 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     group_levels(lv, nl, f->L.ptr, rows_l);
     group_levels(lvt, nlt, f->LT.ptr, rows_lt);
     group_levels(lvu, nlu, f->U.ptr, rows_u);
-    f->L.segs = make_segs(f->L.ptr, rsp::kThinSolveRows);
-    f->LT.segs = make_segs(f->LT.ptr, rsp::kThinSolveRows);
-    f->U.segs = make_segs(f->U.ptr, rsp::kThinSolveRows);
-    f->fac_segs = make_segs(f->L.ptr, rsp::kThinFactorRows);
+    // RSP_ILU_THIN_SOLVE / RSP_ILU_THIN_FACTOR: tuning knobs (0 = no thin runs)
+    const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
+    const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
+    f->L.segs = make_segs(f->L.ptr, thin_solve);
+    f->LT.segs = make_segs(f->LT.ptr, thin_solve);
+    f->U.segs = make_segs(f->U.ptr, thin_solve);
+    f->fac_segs = make_segs(f->L.ptr, thin_factor);
+    IluSymbolic sym;
+    if (!ilu_symbolic(n, rp, ci, dpos, hasdiag, sym)) return RSP_STATUS_ALLOC_FAILED;
+    f->n_updates = (long long)sym.upd_l.size();
+    {
+        long long nl = 0, nu = 0;
+        for (int i = 0; i < n; i++) {
+            nl += dpos[(size_t)i] - rp[(size_t)i];
+            nu += rp[(size_t)i + 1] - dpos[(size_t)i] - hasdiag[(size_t)i];
+        }
+        f->L.batch = f->LT.batch = chain_batch(nl, n);
+        f->U.batch = chain_batch(nu, n);
+        f->fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
+    }
     hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = upload(&f->d_upd_ptr, sym.upd_ptr);
+    if (e == hipSuccess) e = upload(&f->d_upd_l, sym.upd_l);
+    if (e == hipSuccess) e = upload(&f->d_upd_u, sym.upd_u);
+    if (e == hipSuccess) e = upload(&f->d_lord, sym.lord);
+    if (e == hipSuccess) e = upload(&f->d_lend, sym.lend);
     if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
     if (e == hipSuccess) e = upload(&f->d_hasdiag, hasdiag);
     if (e == hipSuccess) e = upload(&f->L.d_rows, rows_l);
@@ -592,6 +708,25 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     if (e == hipSuccess) e = upload(&f->U.d_rows, rows_u);
     if (e == hipSuccess) e = upload(&f->U.d_ptr, f->U.ptr);
     if (e == hipSuccess) e = upload(&f->d_lt_ptr, ltp);
+    // solve tasks in level order
+    for (int kind = 0; kind < 3 && e == hipSuccess; kind++) {
+        rsp_ilu0_info::Dag &d = kind == 0 ? f->L : (kind == 1 ? f->LT : f->U);
+        const std::vector<int> &rows = kind == 0 ? rows_l : (kind == 1 ? rows_lt : rows_u);
+        std::vector<rsp::RowTask> t(std::max<size_t>(rows.size(), 1));
+        for (size_t x = 0; x < rows.size(); x++) {
+            const int i = rows[x];
+            if (kind == 0)
+                t[x] = {i, rp[(size_t)i], dpos[(size_t)i], -1};
+            else if (kind == 1)
+                t[x] = {i, ltp[(size_t)i], ltp[(size_t)i + 1], -1};
+            else
+                t[x] = {i, dpos[(size_t)i] + hasdiag[(size_t)i], rp[(size_t)i + 1],
+                        hasdiag[(size_t)i] ? dpos[(size_t)i] : -1};
+        }
+        e = hipMalloc((void **)&d.d_tasks, t.size() * sizeof(rsp::RowTask));
+        if (e == hipSuccess)
+            e = hipMemcpy(d.d_tasks, t.data(), t.size() * sizeof(rsp::RowTask), hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess) e = upload(&f->d_lt_src, lts);
     if (e == hipSuccess) e = upload(&f->d_lt_col, ltc);
     if (e == hipSuccess) e = hipMalloc((void **)&f->d_zero, sizeof(int));
@@ -634,7 +769,8 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
     return RSP_STATUS_SUCCESS;
 }
 
-static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<rsp::LevelSeg> &segs) {
+static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<rsp::LevelSeg> &segs,
+                                 int batch) {
     rsp::LevelPlan p;
     p.rows = d.d_rows;
     p.ptr_dev = d.d_ptr;
@@ -642,6 +778,8 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<
     p.nlev = (int)d.ptr.size() - 1;
     p.segs = segs.data();
     p.nseg = (int)segs.size();
+    p.batch = batch;
+    p.tasks = d.d_tasks;
     return p;
 }
 
@@ -659,7 +797,12 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.hasdiag = f->d_hasdiag;
     a.vals = d_values;
     a.zero_pivot = f->d_zero;
-    a.plan = level_plan(f->L, f->fac_segs);
+    a.upd_ptr = f->d_upd_ptr;
+    a.upd_l = f->d_upd_l;
+    a.upd_u = f->d_upd_u;
+    a.lord = f->d_lord;
+    a.lend = f->d_lend;
+    a.plan = level_plan(f->L, f->fac_segs, f->fac_batch);
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::ilu0_factor_f64(a, h->stream);
@@ -684,7 +827,7 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.lt_ptr = f->d_lt_ptr;
     a.lt_src = f->d_lt_src;
     a.lt_col = f->d_lt_col;
-    a.plan = level_plan(f->L, f->L.segs);
+    a.plan = level_plan(f->L, f->L.segs, f->L.batch);
     return a;
 }
 
@@ -702,7 +845,7 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
         e = f64 ? rsp_k::trsv_lower_n_f64(a, h->stream)
                 : (ftz ? rsp_k_ftz::trsv_lower_n_f32(a, h->stream) : rsp_k::trsv_lower_n_f32(a, h->stream));
     } else if (op == RSP_OPERATION_TRANSPOSE) {
-        a.plan = level_plan(f->LT, f->LT.segs);
+        a.plan = level_plan(f->LT, f->LT.segs, f->LT.batch);
         e = f64 ? rsp_k::trsv_lower_t_f64(a, h->stream)
                 : (ftz ? rsp_k_ftz::trsv_lower_t_f32(a, h->stream) : rsp_k::trsv_lower_t_f32(a, h->stream));
     } else {
@@ -719,7 +862,7 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
-    a.plan = level_plan(f->U, f->U.segs);
+    a.plan = level_plan(f->U, f->U.segs, f->U.batch);
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::trsv_upper_f64(a, h->stream);

@@ -69,6 +69,13 @@ struct SpmvArgs {
 struct LevelSeg {
     int lb, le, thin;
 };
+// Solve task of one row, stored in level order: the fma chain runs over
+// positions [p0, p1) (for L^T: slots of the transposed map), d = diagonal
+// position for the U solve (-1 = missing), unused otherwise.
+struct alignas(16) RowTask {
+    int i, p0, p1, d;
+};
+
 struct LevelPlan {
     const int *rows;      // device
     const int *ptr_dev;   // device, nlev + 1
@@ -76,11 +83,13 @@ struct LevelPlan {
     int nlev;
     const LevelSeg *segs; // host
     int nseg;
+    int batch;            // fma-chain load batch (2, 4, 8) from the mean chain length
+    const RowTask *tasks; // device, solve DAGs only: task of rows[x] at slot x
 };
 constexpr int kThinThreads = 1024;  // workgroup of a thin segment
 constexpr int kIluWaves = 4;        // rows per 256-thread workgroup (fat factor levels)
-constexpr int kThinSolveRows = 2048;  // solve levels this small run inside a thin segment
-constexpr int kThinFactorRows = 64;   // factor levels (a wave per row: 16 rows per pass)
+constexpr int kThinSolveRows = 256;   // solve levels this small run inside a thin segment (<= kThinThreads)
+constexpr int kThinFactorRows = 32;   // factor levels (a wave per row: 16 rows per pass)
 
 struct IluArgs {
     int n;
@@ -90,6 +99,18 @@ struct IluArgs {
     const int *hasdiag;   // 1 if colidx[dpos[i]] == i
     void *vals;
     int *zero_pivot;      // device int, atomicMin target (INT_MAX = none)
+    // Update lists (symbolic ILU(0)): position p = (i, j) receives
+    // a_ij -= l_ik u_kj for k = the lower columns of row i with u_kj in the
+    // pattern, k ascending: pairs (upd_l[u], upd_u[u]) for u in
+    // [upd_ptr[p], upd_ptr[p+1]) are the positions of l_ik and u_kj.
+    const int *upd_ptr;
+    const int *upd_l;
+    const int *upd_u;
+    // Lower positions of row i, slots [rowptr[i], dpos[i]), grouped by
+    // intra-row stage (l_ij waits for the l_ik of its own update list):
+    // lord = position, lend = one past the last slot of the slot's stage.
+    const int *lord;
+    const int *lend;
     LevelPlan plan;       // L DAG, factor thresholds
 };
 
