@@ -131,8 +131,8 @@ HOST_PROTOS = {
 }
 
 
-def _load(name: str, protos: dict) -> C.CDLL:
-    path = os.path.join(LIB_DIR, name)
+def _load(name: str, protos: dict, path: str | None = None) -> C.CDLL:
+    path = path or os.path.join(LIB_DIR, name)
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build the HIP/C libraries first "
@@ -146,7 +146,9 @@ def _load(name: str, protos: dict) -> C.CDLL:
 
 
 host = _load("librsp_host.so", HOST_PROTOS)
-rsp = _load("librsp.so", RSP_PROTOS)
+# RSP_PROBE_LIB: a diagnostic build of librsp.so (scripts/spmv_probe.py only)
+_RSP_PATH = os.environ.get("RSP_PROBE_LIB") or os.path.join(LIB_DIR, "librsp.so")
+rsp = _load("librsp.so", RSP_PROTOS, _RSP_PATH)
 
 
 def check(status: int, where: str) -> None:
@@ -156,4 +158,4 @@ def check(status: int, where: str) -> None:
 
 def loaded_paths() -> list[str]:
     """Absolute paths of the native libraries this package loaded."""
-    return [os.path.join(LIB_DIR, "librsp_host.so"), os.path.join(LIB_DIR, "librsp.so")]
+    return [os.path.join(LIB_DIR, "librsp_host.so"), _RSP_PATH]

@@ -207,6 +207,7 @@ static SpmvBounds spmv_bounds(int64_t rows, int64_t nnz, int cap) {
     b.nlong = q;
     b.nslots = 2 * q + 1;
     b.nblocks = 6 * q + 2 * l + (size_t)(rows / rsp::kSpmvMaxRows) + 8;
+    b.nblocks += std::min<size_t>(b.nblocks, 8192);  // headroom for spread-out small plans
     return b;
 }
 
@@ -221,6 +222,9 @@ static size_t spmv_bytes(const SpmvBounds &b, size_t elem, size_t *off_long, siz
 static int tile_cap(rsp_datatype_t t) {
     return t == RSP_R_64F ? SpmvTile<double>::kMaxNnz : SpmvTile<float>::kMaxNnz;
 }
+static int chunk_cap(rsp_datatype_t t) {
+    return t == RSP_R_64F ? SpmvTile<double>::kChunk : SpmvTile<float>::kChunk;
+}
 static size_t elem_size(rsp_datatype_t t) { return t == RSP_R_64F ? 8 : 4; }
 
 rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void *alpha,
@@ -232,16 +236,17 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void
     if (!mat || !buffer_size) return RSP_STATUS_INVALID_VALUE;
     if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
     if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
-    SpmvBounds b = spmv_bounds(mat->rows, mat->nnz, tile_cap(compute_type));
+    SpmvBounds b = spmv_bounds(mat->rows, mat->nnz, chunk_cap(compute_type));
     *buffer_size = spmv_bytes(b, elem_size(compute_type), nullptr, nullptr);
     return RSP_STATUS_SUCCESS;
 }
 
 // Greedy row-block schedule over host row offsets (see spmv.hip header).
-// Rows longer than kSpmvLongRow get tiles of their own (one per tile-sized
-// chunk); the others are packed into tiles of <= cap entries / kSpmvMaxRows.
-static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock> &blocks,
-                           std::vector<SpmvLongRow> &longrows, int *nslots) {
+// Rows longer than kSpmvLongRow get tiles of their own (one per `chunk`
+// entries); the others are packed into tiles of <= cap entries / kSpmvMaxRows.
+static int build_spmv_plan(const int *rp, int m, int cap, int chunk, std::vector<SpmvBlock> &blocks,
+                           std::vector<SpmvLongRow> &longrows, int *nslots,
+                           int maxrows = rsp::kSpmvMaxRows) {
     blocks.clear();
     longrows.clear();
     int slots = 0;
@@ -249,7 +254,7 @@ static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock>
     while (r < m) {
         int len = rp[r + 1] - rp[r];
         if (len > rsp::kSpmvLongRow) {
-            if (len <= cap) {  // one chunk: reduced and written in place
+            if (len <= chunk) {  // one chunk: reduced and written in place
                 SpmvBlock b;
                 b.r0 = r;
                 b.r1 = rsp::kSpmvWholeRow;
@@ -264,12 +269,12 @@ static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock>
             lr.first = slots;
             lr.nchunks = 0;
             lr.pad = 0;
-            for (int k = rp[r]; k < rp[r + 1]; k += cap) {
+            for (int k = rp[r]; k < rp[r + 1]; k += chunk) {
                 SpmvBlock b;
                 b.r0 = r;
                 b.r1 = -(slots + 1);
                 b.k0 = k;
-                b.k1 = std::min(k + cap, rp[r + 1]);
+                b.k1 = std::min(k + chunk, rp[r + 1]);
                 blocks.push_back(b);
                 slots++;
                 lr.nchunks++;
@@ -279,9 +284,10 @@ static int build_spmv_plan(const int *rp, int m, int cap, std::vector<SpmvBlock>
             continue;
         }
         int start = r, nnz = 0;
-        while (r < m && r - start < rsp::kSpmvMaxRows) {
+        while (r < m && r - start < maxrows) {
             int l = rp[r + 1] - rp[r];
-            if (l > rsp::kSpmvLongRow || nnz + l > cap) break;
+            // a tile always takes its first row (<= kSpmvLongRow <= kMaxNnz)
+            if (l > rsp::kSpmvLongRow || (r > start && nnz + l > cap)) break;
             nnz += l;
             r++;
         }
@@ -330,13 +336,42 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
         for (int c : ci)
             if ((unsigned)c >= (unsigned)ncols) return RSP_STATUS_INVALID_VALUE;
     }
-    const int cap = tile_cap(compute_type);
+    const int chunk = chunk_cap(compute_type);
+    int cap = tile_cap(compute_type);
     std::vector<SpmvBlock> blocks;
     std::vector<SpmvLongRow> longrows;
     int nslots = 0;
-    build_spmv_plan(rp.data(), m, cap, blocks, longrows, &nslots);
+    build_spmv_plan(rp.data(), m, cap, chunk, blocks, longrows, &nslots);
+    if (!(h->spmv_variant & 16)) {
+        // A matrix with fewer tiles than the chip holds resident workgroups
+        // (R) leaves slots idle and runs each tile latency-bound: spread it
+        // over up to R smaller tiles (measured +2.7 % on the moderate set;
+        // plans of >= 2 waves are left alone, they lost 1 % this way).
+        // Tiling never changes the result (canonical summation order).
+        const int64_t R = (int64_t)rsp_k::spmv_tiles_per_cu((int)elem_size(compute_type)) * h->num_cus;
+        const int64_t nb = (int64_t)blocks.size();
+        if (nb > 0 && nb < R) {
+            const SpmvBounds bb = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), chunk);
+            const int64_t nnz_s = rp[(size_t)m];
+            int c = (int)std::max<int64_t>(64, std::min<int64_t>(cap, (nnz_s + R - 1) / R));
+            for (int tries = 0; tries < 32 && c < cap; tries++) {
+                std::vector<SpmvBlock> b2;
+                std::vector<SpmvLongRow> l2;
+                int s2 = 0;
+                build_spmv_plan(rp.data(), m, c, chunk, b2, l2, &s2);
+                if ((int64_t)b2.size() <= R && b2.size() <= bb.nblocks) {
+                    blocks.swap(b2);
+                    longrows.swap(l2);
+                    nslots = s2;
+                    break;
+                }
+                c += std::max(8, c / 16);
+            }
+        }
+    }
     // the caller sized the buffer from mat->nnz; make sure the plan fits
-    SpmvBounds b = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), cap);
+    // (bounds in units of the chunk, which is <= the packing cap)
+    SpmvBounds b = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), chunk);
     if (blocks.size() > b.nblocks || longrows.size() > b.nlong || (size_t)nslots > b.nslots)
         return RSP_STATUS_INVALID_VALUE;
     if (!blocks.empty() && !d_buffer) return RSP_STATUS_INVALID_VALUE;
@@ -397,7 +432,6 @@ rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp
     a.vector_ok = ((((uintptr_t)mat->colidx) | ((uintptr_t)mat->vals)) & 15) == 0;
     a.nnz = mat->nnz_s;
     a.variant = h->spmv_variant;
-    a.num_cus = h->num_cus;
     hipError_t e;
     if (compute_type == RSP_R_64F)
         e = rsp_k::spmv_f64(a, h->stream);

@@ -30,7 +30,10 @@ struct alignas(16) SpmvLongRow {
 
 // Tile geometry shared by the planner and the kernels.
 constexpr int kSpmvThreads = 256;
-constexpr int kSpmvIter = 4;        // vectors per thread per tile
+#ifndef RSP_SPMV_ITER
+#define RSP_SPMV_ITER 4  // overridable for tile-geometry experiments (scripts/spmv_probe.py)
+#endif
+constexpr int kSpmvIter = RSP_SPMV_ITER;  // vectors per thread per tile
 constexpr int kSpmvMaxRows = 512;   // rows per tile (row offsets staged in LDS)
 constexpr int kSpmvLongRow = 256;   // rows longer than this get the 256-thread tree
 constexpr int kSpmvWholeRow = -2147483647 - 1;  // SpmvBlock::r1 marker (INT_MIN)
@@ -39,6 +42,10 @@ struct SpmvTile {
     static constexpr int kVec = 16 / sizeof(T);                           // 16-B loads
     static constexpr int kSlots = kSpmvThreads * kSpmvIter * kVec;        // LDS products
     static constexpr int kMaxNnz = kSlots - (kVec - 1);                   // any alignment fits
+    // long-row chunk (and longest row reduced whole): fixed by the canonical
+    // summation order (oracle_spmv_canon_*), independent of the tile size
+    static constexpr int kChunk = kSpmvThreads * 4 * kVec - (kVec - 1);   // 2047 / 4093
+    static_assert(kChunk <= kMaxNnz, "a chunk must fit one tile");
 };
 
 struct SpmvArgs {
@@ -57,8 +64,7 @@ struct SpmvArgs {
     int nnz;        // rowptr[m]: tiles touching the last partial vector go scalar
     int vector_ok;  // colidx/vals 16-B aligned -> vector loads
     int variant;    // bit 0: default-policy (not non-temporal) vals/colidx loads;
-                    // bit 1: persistent pipelined kernel
-    int num_cus;    // compute units of the device (persistent grid sizing)
+                    // bit 4 (plan time): no spreading of sub-wave plans
 };
 
 // Level schedule of one dependency DAG. Rows are grouped by level
@@ -152,6 +158,7 @@ hipError_t gather(int elem_bytes, int64_t n, const int64_t *idx, const void *src
 hipError_t scatter(int elem_bytes, int64_t n, const int64_t *idx, const void *src, void *dst,
                    hipStream_t s);
 hipError_t spmv_f64(const rsp::SpmvArgs &a, hipStream_t s);
+int spmv_tiles_per_cu(int elem_bytes);  // resident spmv_tiles workgroups per CU
 hipError_t ilu0_factor_f64(const rsp::IluArgs &a, hipStream_t s);
 hipError_t trsv_lower_n_f64(const rsp::TrsvArgs &a, hipStream_t s);
 hipError_t trsv_lower_t_f64(const rsp::TrsvArgs &a, hipStream_t s);

@@ -35,6 +35,23 @@
 #define RSP_KNS rsp_k
 #endif
 
+// Diagnostic builds only (scripts/spmv_probe.py, never the shipped library):
+// 1 = every gather hits the first 32 KiB of x (gather cost removed),
+// 2 = no row reduce (one LDS read per thread stands in for it),
+// 3 = 1 + 2, 4 = the tile's loads only (no gather, LDS or reduce).
+#ifndef RSP_PROBE
+#define RSP_PROBE 0
+#endif
+#ifndef RSP_PROBE_Y
+#define RSP_PROBE_Y 0  // with RSP_PROBE 4: also store y (one element per row)
+#endif
+#ifndef RSP_NT_Y
+#define RSP_NT_Y 0  // non-temporal y stores (A/B)
+#endif
+#ifndef RSP_PROBE_LDS
+#define RSP_PROBE_LDS 0  // with RSP_PROBE 4: also an LDS write + barrier
+#endif
+
 namespace RSP_KNS {
 
 using rsp::kSpmvThreads;
@@ -82,13 +99,13 @@ __device__ __forceinline__ P ld(const P *p) {
 // touch in-bounds neighbours whose LDS slots are never read. Requires a
 // non-empty tile whose last vector does not straddle the end of the arrays
 // (the caller takes stream_products_scalar otherwise).
-template <typename T, bool NT>
+template <typename T, bool NT, int NTH = kSpmvThreads,
+          int IT = SpmvTile<T>::kSlots / (kSpmvThreads * (16 / sizeof(T)))>
 __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
                                                 const T *__restrict__ vals,
                                                 const T *__restrict__ x, int kb, int k1,
                                                 T *__restrict__ lds) {
     constexpr int VW = 16 / sizeof(T);
-    constexpr int IT = SpmvTile<T>::kSlots / (kSpmvThreads * VW);
     typedef typename VecT<T, VW>::V V;
     typedef typename VecT<T, VW>::I I;
     const int tid = threadIdx.x;
@@ -97,12 +114,12 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
     V vv[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-        const int e = min(kb + (it * kSpmvThreads + tid) * VW, last);
+        const int e = min(kb + (it * NTH + tid) * VW, last);
         ci[it] = ld<NT>(reinterpret_cast<const I *>(colidx + e));
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-        const int e = min(kb + (it * kSpmvThreads + tid) * VW, last);
+        const int e = min(kb + (it * NTH + tid) * VW, last);
         vv[it] = ld<NT>(reinterpret_cast<const V *>(vals + e));
     }
     // keep the scheduler from splitting the load and gather bursts: two
@@ -112,7 +129,7 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
-        for (int j = 0; j < VW; ++j) xv[it][j] = x[ci[it][j]];
+        for (int j = 0; j < VW; ++j) xv[it][j] = x[(RSP_PROBE == 1 || RSP_PROBE == 3) ? (ci[it][j] & 4095) : ci[it][j]];
     __builtin_amdgcn_sched_barrier(0);
     // every slot (it*256 + tid)*VW lies inside the tile's LDS image, so the
     // stores are unpredicated too; slots at or past k1 - kb are never read
@@ -121,28 +138,28 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
         V p;
 #pragma unroll
         for (int j = 0; j < VW; ++j) p[j] = vv[it][j] * xv[it][j];
-        *reinterpret_cast<V *>(lds + (it * kSpmvThreads + tid) * VW) = p;
+        *reinterpret_cast<V *>(lds + (it * NTH + tid) * VW) = p;
     }
 }
 
 // Element-wise variant for a tile that touches the end of the arrays (at
 // most one per call) or unaligned arrays.
-template <typename T>
+template <typename T, int NTH = kSpmvThreads>
 __device__ __forceinline__ void stream_products_scalar(const int *__restrict__ colidx,
                                                        const T *__restrict__ vals,
                                                        const T *__restrict__ x, int k0, int kb,
                                                        int k1, T *lds) {
-    for (int e = kb + (int)threadIdx.x; e < k1; e += kSpmvThreads)
+    for (int e = kb + (int)threadIdx.x; e < k1; e += NTH)
         if (e >= k0) lds[e - kb] = vals[e] * x[colidx[e]];
 }
 
-// Rows [r0, r0 + nrows) of a tile, L lanes per row, canonical 8-way order.
-template <typename T, int L>
-__device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int r0, int nrows,
-                                            int kb, T *__restrict__ y, T alpha, T beta,
-                                            int beta_nonzero) {
+// Rows [0, nrows) of a tile, L lanes per row, canonical 8-way order; the
+// row sum goes to sink(row, sum) (lane 0 of the row's group).
+template <typename T, int L, int NTH, typename Sink>
+__device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int nrows, int kb,
+                                            Sink sink) {
     constexpr int NA = 8 / L;                  // partials held per lane
-    constexpr int NG = kSpmvThreads / L;       // row groups per pass
+    constexpr int NG = NTH / L;                // row groups per pass
     const int tid = threadIdx.x;
     const int g = tid / L, lane = tid & (L - 1);
     for (int rr = g; rr - g < nrows; rr += NG) {  // same trip count for all groups
@@ -169,11 +186,22 @@ __device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int
         // remaining stages across the L lanes of the group
 #pragma unroll
         for (int off = L / 2; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
-        if (active && lane == 0) {
-            T out = alpha * s;
-            if (beta_nonzero) out += beta * y[r0 + rr];
-            y[r0 + rr] = out;
-        }
+        if (active && lane == 0) sink(rr, s);
+    }
+}
+
+// lanes per row: power of two <= 8 such that each lane still sums >= 4
+// products of an average row and the groups fit the workgroup
+template <typename T, int NTH = kSpmvThreads, typename Sink>
+__device__ __forceinline__ void reduce_tile_rows(const T *lds, const int *rp_lds, int nrows,
+                                                 int nnzt, int kb, Sink sink) {
+    int L = 1;
+    while (L < 8 && 2 * L * nrows <= NTH && 8 * L * nrows <= nnzt) L <<= 1;
+    switch (L) {
+        case 1: reduce_rows<T, 1, NTH>(lds, rp_lds, nrows, kb, sink); break;
+        case 2: reduce_rows<T, 2, NTH>(lds, rp_lds, nrows, kb, sink); break;
+        case 4: reduce_rows<T, 4, NTH>(lds, rp_lds, nrows, kb, sink); break;
+        default: reduce_rows<T, 8, NTH>(lds, rp_lds, nrows, kb, sink); break;
     }
 }
 
@@ -181,13 +209,9 @@ __device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int
 // sums slots a+t, a+t+256, ... in order, each wave combines its 64 sums with
 // a xor-butterfly (32, 16, ..., 1), and the four wave sums are added as
 // (w0+w1)+(w2+w3) — the canonical order for rows longer than kSpmvLongRow
-// (oracle_spmv_canon_*). A whole row is written to y; a chunk goes to its
-// partial slot for the in-order fixup.
+// (oracle_spmv_canon_*). The total is valid in thread 0.
 template <typename T>
-__device__ __forceinline__ void reduce_long(const T *lds, int a, int e, T *wsum,
-                                            const SpmvBlock &blk, T *__restrict__ y,
-                                            T *__restrict__ partials, T alpha, T beta,
-                                            int beta_nonzero) {
+__device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
     const int tid = threadIdx.x;
     T s = T(0);
     for (int k = a + tid; k < e; k += kSpmvThreads) s += lds[k];
@@ -195,16 +219,7 @@ __device__ __forceinline__ void reduce_long(const T *lds, int a, int e, T *wsum,
     for (int off = 32; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
     if ((tid & 63) == 0) wsum[tid >> 6] = s;
     __syncthreads();
-    if (tid == 0) {
-        const T t = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
-        if (blk.r1 == rsp::kSpmvWholeRow) {
-            T out = alpha * t;
-            if (beta_nonzero) out += beta * y[blk.r0];
-            y[blk.r0] = out;
-        } else {
-            partials[-(blk.r1 + 1)] = t;
-        }
-    }
+    return (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
 }
 
 template <typename T, bool NT>
@@ -232,6 +247,37 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     // vectors may be used unless the tile reaches the last, partial vector
     const bool vec = vector_ok && k1 > k0 && k1 <= (nnz & ~(VW - 1));
     const int kb = vec ? (k0 & ~(VW - 1)) : k0;
+#if RSP_PROBE == 4
+    if (vec) {  // diagnostic: the tile's colidx/vals stream alone
+        typedef typename VecT<T, VW>::V V;
+        typedef typename VecT<T, VW>::I I;
+        constexpr int IT = SpmvTile<T>::kSlots / (kSpmvThreads * VW);
+        const int last = (k1 - 1) & ~(VW - 1);
+        T acc = T(0);
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int e = min(kb + (it * kSpmvThreads + tid) * VW, last);
+            const I c = ld<NT>(reinterpret_cast<const I *>(colidx + e));
+            const V v = ld<NT>(reinterpret_cast<const V *>(vals + e));
+#pragma unroll
+            for (int j = 0; j < VW; ++j) acc += v[j] + T(c[j]);
+        }
+#if RSP_PROBE_Y
+#if RSP_NT_Y
+        if (blk.r1 > 0 && tid < nrows) __builtin_nontemporal_store(acc, y + blk.r0 + tid);
+#else
+        if (blk.r1 > 0 && tid < nrows) y[blk.r0 + tid] = acc;  // + the y stream
+#endif
+#endif
+#if RSP_PROBE_LDS
+        lds[tid] = acc;  // + an LDS write and a workgroup barrier
+        __syncthreads();
+        acc = lds[(tid + 1) & (kSpmvThreads - 1)];
+#endif
+        if (acc == T(-12345.0)) y[blk.r0] = acc + T(rpv[0]);  // keeps every load live
+        return;
+    }
+#endif
     if (vec)
         stream_products<T, NT>(colidx, vals, x, kb, k1, lds);
     else
@@ -243,160 +289,34 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     }
     __syncthreads();
 
-    if (blk.r1 < 0) {
-        reduce_long(lds, k0 - kb, k1 - kb, wsum, blk, y, partials, alpha, beta, beta_nonzero);
+    if (blk.r1 < 0) {  // a long row: written whole, or a chunk partial for the fixup
+        const T t = reduce_long(lds, k0 - kb, k1 - kb, wsum);
+        if (tid == 0) {
+            if (blk.r1 == rsp::kSpmvWholeRow) {
+                T out = alpha * t;
+                if (beta_nonzero) out += beta * y[blk.r0];
+                y[blk.r0] = out;
+            } else {
+                partials[-(blk.r1 + 1)] = t;
+            }
+        }
         return;
     }
 
-    const int r0 = blk.r0, nnzt = k1 - k0;
-    // lanes per row: power of two <= 8 such that each lane still sums >= 4
-    // products of an average row and the groups fit the workgroup
-    int L = 1;
-    while (L < 8 && 2 * L * nrows <= kSpmvThreads && 8 * L * nrows <= nnzt) L <<= 1;
-    switch (L) {
-        case 1: reduce_rows<T, 1>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-        case 2: reduce_rows<T, 2>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-        case 4: reduce_rows<T, 4>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-        default: reduce_rows<T, 8>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent, software-pipelined form of spmv_tiles: gridDim.x workgroups,
-// each walking a contiguous run of `tpw` tiles (XCD-swizzled so each XCD owns
-// a contiguous eighth of the matrix). The colidx/vals/row-offset loads of
-// tile t+1 are issued before tile t is reduced, so the HBM stream of a
-// workgroup stays busy through its reduce phase and there is no per-tile
-// dispatch. Same arithmetic and summation order as spmv_tiles.
-
-template <typename T>
-struct TileRegs {
-    static constexpr int VW = 16 / sizeof(T);
-    static constexpr int IT = SpmvTile<T>::kSlots / (kSpmvThreads * VW);
-    static constexpr int RPQ = (rsp::kSpmvMaxRows + kSpmvThreads) / kSpmvThreads;
-    typename VecT<T, VW>::I ci[IT];
-    typename VecT<T, VW>::V vv[IT];
-    int rpv[RPQ];
-};
-
-// Issue the loads of one tile (vector path only; the scalar path loads in
-// finish). Returns the tile's vector flag.
-template <typename T, bool NT>
-__device__ __forceinline__ bool issue_tile(const SpmvBlock &blk, const int *__restrict__ rowptr,
-                                           const int *__restrict__ colidx,
-                                           const T *__restrict__ vals, int nnz, int vector_ok,
-                                           TileRegs<T> &r) {
-    typedef TileRegs<T> R;
-    typedef typename VecT<T, R::VW>::I I;
-    typedef typename VecT<T, R::VW>::V V;
-    const int tid = threadIdx.x;
-    const int nrows = blk.r1 - blk.r0;
-    const int nrows_ld = nrows > 0 ? nrows : 0;
-#pragma unroll
-    for (int q = 0; q < R::RPQ; ++q) r.rpv[q] = rowptr[blk.r0 + min(tid + q * kSpmvThreads, nrows_ld)];
-    const bool vec = vector_ok && blk.k1 > blk.k0 && blk.k1 <= (nnz & ~(R::VW - 1));
-    if (vec) {
-        const int kb = blk.k0 & ~(R::VW - 1);
-        const int last = (blk.k1 - 1) & ~(R::VW - 1);
-#pragma unroll
-        for (int it = 0; it < R::IT; ++it)
-            r.ci[it] = ld<NT>(reinterpret_cast<const I *>(colidx + min(kb + (it * kSpmvThreads + tid) * R::VW, last)));
-#pragma unroll
-        for (int it = 0; it < R::IT; ++it)
-            r.vv[it] = ld<NT>(reinterpret_cast<const V *>(vals + min(kb + (it * kSpmvThreads + tid) * R::VW, last)));
-    }
-    return vec;
-}
-
-// Gathers + products into LDS (+ row offsets); returns kb.
-template <typename T>
-__device__ __forceinline__ int finish_tile(const SpmvBlock &blk, bool vec,
-                                           const int *__restrict__ colidx,
-                                           const T *__restrict__ vals, const T *__restrict__ x,
-                                           const TileRegs<T> &r, T *__restrict__ lds, int *rp_lds) {
-    typedef TileRegs<T> R;
-    typedef typename VecT<T, R::VW>::V V;
-    const int tid = threadIdx.x;
-    int kb;
-    if (vec) {
-        kb = blk.k0 & ~(R::VW - 1);
-        T xv[R::IT][R::VW];
-#pragma unroll
-        for (int it = 0; it < R::IT; ++it)
-#pragma unroll
-            for (int j = 0; j < R::VW; ++j) xv[it][j] = x[r.ci[it][j]];
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int it = 0; it < R::IT; ++it) {
-            V p;
-#pragma unroll
-            for (int j = 0; j < R::VW; ++j) p[j] = r.vv[it][j] * xv[it][j];
-            *reinterpret_cast<V *>(lds + (it * kSpmvThreads + tid) * R::VW) = p;
-        }
-    } else {
-        kb = blk.k0;
-        stream_products_scalar<T>(colidx, vals, x, blk.k0, kb, blk.k1, lds);
-    }
-    const int nrows = blk.r1 - blk.r0;
-#pragma unroll
-    for (int q = 0; q < R::RPQ; ++q) {
-        const int i = tid + q * kSpmvThreads;
-        if (i <= nrows) rp_lds[i] = r.rpv[q];
-    }
-    return kb;
-}
-
-template <typename T>
-__device__ __forceinline__ void reduce_tile(const SpmvBlock &blk, int kb, const T *lds,
-                                            const int *rp_lds, T *wsum, T *__restrict__ y,
-                                            T *__restrict__ partials, T alpha, T beta,
-                                            int beta_nonzero) {
-    if (blk.r1 < 0) {
-        reduce_long(lds, blk.k0 - kb, blk.k1 - kb, wsum, blk, y, partials, alpha, beta,
-                    beta_nonzero);
+    const int r0 = blk.r0;
+    if (RSP_PROBE == 2 || RSP_PROBE == 3) {
+        if (tid < nrows) y[r0 + tid] = lds[tid];
         return;
     }
-    const int r0 = blk.r0, nrows = blk.r1 - blk.r0, nnzt = blk.k1 - blk.k0;
-    int L = 1;
-    while (L < 8 && 2 * L * nrows <= kSpmvThreads && 8 * L * nrows <= nnzt) L <<= 1;
-    switch (L) {
-        case 1: reduce_rows<T, 1>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-        case 2: reduce_rows<T, 2>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-        case 4: reduce_rows<T, 4>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-        default: reduce_rows<T, 8>(lds, rp_lds, r0, nrows, kb, y, alpha, beta, beta_nonzero); break;
-    }
-}
-
-template <typename T, bool NT>
-__global__ __launch_bounds__(kSpmvThreads) void spmv_persistent(
-    const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
-    const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
-    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, int tpw) {
-    __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
-    __shared__ T wsum[kSpmvThreads / 64];
-    __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
-    const int w = xcd_swizzle(blockIdx.x, gridDim.x);
-    int t = w * tpw;
-    const int tend = min(nblocks, t + tpw);
-    if (t >= tend) return;
-    TileRegs<T> r;
-    SpmvBlock blk = blocks[t];
-    bool vec = issue_tile<T, NT>(blk, rowptr, colidx, vals, nnz, vector_ok, r);
-    for (; t < tend; ++t) {
-        const int kb = finish_tile<T>(blk, vec, colidx, vals, x, r, lds, rp_lds);
-        __syncthreads();
-        SpmvBlock nblk = blk;
-        bool nvec = false;
-        if (t + 1 < tend) {  // prefetch the next tile under this tile's reduce
-            nblk = blocks[t + 1];
-            nvec = issue_tile<T, NT>(nblk, rowptr, colidx, vals, nnz, vector_ok, r);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        reduce_tile<T>(blk, kb, lds, rp_lds, wsum, y, partials, alpha, beta, beta_nonzero);
-        __syncthreads();
-        blk = nblk;
-        vec = nvec;
-    }
+    reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, kb, [&](int rr, T sum) {
+        T out = alpha * sum;
+        if (beta_nonzero) out += beta * y[r0 + rr];
+#if RSP_NT_Y
+        __builtin_nontemporal_store(out, y + r0 + rr);
+#else
+        y[r0 + rr] = out;
+#endif
+    });
 }
 
 // y[row] = alpha * sum(partials of the row, chunk order) (+ beta*y[row]).
@@ -420,36 +340,13 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
     const T alpha = (T)a.alpha, beta = (T)a.beta;
     const int bnz = a.beta != 0.0;
-    if (a.variant & 2) {
-        // persistent: one workgroup per resident slot (occupancy query x CUs;
-        // performance only — a non-resident workgroup would just run late),
-        // tiles shared out in contiguous runs
-        auto kern = (a.variant & 1) ? spmv_persistent<T, false> : spmv_persistent<T, true>;
-        static int occ[2] = {0, 0};
-        int &o = occ[a.variant & 1];
-        if (o == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, kSpmvThreads, 0) !=
-                           hipSuccess || o < 1))
-            o = 1;
-        const int grid = min(a.nblocks, o * a.num_cus);
-        const int tpw = (a.nblocks + grid - 1) / grid;
-        const int g = (a.nblocks + tpw - 1) / tpw;
-        hipLaunchKernelGGL(kern, dim3(g), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
-                           (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks,
-                           (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok, tpw);
-    } else
     // vals/colidx are read once per call: non-temporal loads keep them from
     // evicting x (measured +2% fp64 / +7.5% fp32 on the cache-cold big set);
     // variant bit 0 restores default-policy loads for A/B runs
-    if (!(a.variant & 1))
-        hipLaunchKernelGGL((spmv_tiles<T, true>), dim3(a.nblocks), dim3(kSpmvThreads), 0, s,
-                           a.rowptr, a.colidx, (const T *)a.vals, (const T *)a.x, (T *)a.y,
-                           a.blocks, a.nblocks, (T *)a.partials, alpha, beta, bnz, a.nnz,
-                           a.vector_ok);
-    else
-        hipLaunchKernelGGL((spmv_tiles<T, false>), dim3(a.nblocks), dim3(kSpmvThreads), 0, s,
-                           a.rowptr, a.colidx, (const T *)a.vals, (const T *)a.x, (T *)a.y,
-                           a.blocks, a.nblocks, (T *)a.partials, alpha, beta, bnz, a.nnz,
-                           a.vector_ok);
+    auto kern = (a.variant & 1) ? spmv_tiles<T, false> : spmv_tiles<T, true>;
+    hipLaunchKernelGGL(kern, dim3(a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
+                       (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks,
+                       (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.nlong > 0) {
@@ -462,6 +359,15 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
 
 hipError_t spmv_f32(const SpmvArgs &a, hipStream_t s) { return launch_spmv<float>(a, s); }
 #ifndef RSP_FTZ_BUILD
+int spmv_tiles_per_cu(int elem_bytes) {
+    int o = 0;
+    const hipError_t e =
+        elem_bytes == 8
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, spmv_tiles<double, true>, kSpmvThreads, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, spmv_tiles<float, true>, kSpmvThreads, 0);
+    return (e == hipSuccess && o > 0) ? o : 1;
+}
+
 // dst[i] = src[idx[i]]: halo pack/unpack of the multi-GPU SpMV. Grid-stride,
 // 4 elements in flight per thread; ~12-20 B per element, HBM/L2 bound.
 template <typename E>

@@ -150,3 +150,16 @@ def test_full_size_moderate(handle):
     """A full moderate-set surrogate (config 3 size) fp64, bitwise vs oracle."""
     A = csr.surrogate("FEM_3D_thermal2")
     compare(A, torch.float64, handle)
+
+
+@pytest.mark.parametrize("thin_solve,thin_factor", [(0, 0), (1024, 1 << 30), (1, 1)])
+@pytest.mark.parametrize("name,scale", [("G2_circuit", 0.2), ("stomach", 0.05), ("ss1", 0.05)])
+def test_schedule_variants(handle, monkeypatch, thin_solve, thin_factor, name, scale):
+    """Every launch schedule gives the same bits: all levels launched one by
+    one (0), all levels in single-workgroup thin runs (max), and mixed."""
+    monkeypatch.setenv("RSP_ILU_THIN_SOLVE", str(thin_solve))
+    monkeypatch.setenv("RSP_ILU_THIN_FACTOR", str(thin_factor))
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float64, handle, x=x)
+    compare(A, torch.float32, handle, x=x, true_lu=True)

@@ -205,3 +205,22 @@ def test_invalid_inputs_are_status_codes(handle):
     with pytest.raises(RspError) as e:
         SpMat(handle, rp, ci, va, 2)
     assert e.value.status == 3
+
+
+@pytest.mark.parametrize("variant", [1, 16, 17])
+def test_kernel_variants_same_bits(monkeypatch, variant):
+    """Every kernel / plan variant (RSP_SPMV_VARIANT: default-policy instead of
+    non-temporal loads; small plans not spread over the chip) gives the same
+    bits as the canonical-order oracle, on matrices with short rows, rows
+    just above the 256 threshold and chunked hub rows."""
+    monkeypatch.setenv("RSP_SPMV_VARIANT", str(variant))
+    h = Handle()
+    try:
+        for name, scale in (("ecology2", 0.05), ("ASIC_320ks", 0.3), ("G2_circuit", 0.3),
+                            ("Serena", 0.02), ("cage13", 0.05)):
+            A = csr.surrogate(name, scale)
+            x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+            for dt in (torch.float64, torch.float32):
+                check(A, x, dt, h)
+    finally:
+        h.close()
