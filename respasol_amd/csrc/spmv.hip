@@ -205,6 +205,15 @@ __device__ __forceinline__ void reduce_tile_rows(const T *lds, const int *rp_lds
     }
 }
 
+// LDS-only workgroup barrier: orders LDS traffic and leaves global stores in
+// flight (__syncthreads() waits vmcnt(0), i.e. for the previous tile's y
+// stores to be acknowledged).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // A long row (or one tile-sized chunk of it) in LDS slots [a, e): thread t
 // sums slots a+t, a+t+256, ... in order, each wave combines its 64 sums with
 // a xor-butterfly (32, 16, ..., 1), and the four wave sums are added as
@@ -218,22 +227,21 @@ __device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) s = s + __shfl_xor(s, off, 64);
     if ((tid & 63) == 0) wsum[tid >> 6] = s;
-    __syncthreads();
+    lds_barrier();
     return (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
 }
 
-template <typename T, bool NT>
-__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
-    const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
-    const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
-    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok) {
+// One tile: stream -> gathers -> products in LDS -> canonical reduce -> y.
+// BETA: beta != 0 (y is read); the beta == 0 form issues no y loads, so its
+// y stores never wait on anything.
+template <typename T, bool NT, bool BETA>
+__device__ __forceinline__ void spmv_tile(
+    const SpmvBlock blk, const int *__restrict__ rowptr, const int *__restrict__ colidx,
+    const T *__restrict__ vals, const T *__restrict__ x, T *__restrict__ y,
+    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, T *lds,
+    T *wsum, int *rp_lds) {
     constexpr int VW = 16 / sizeof(T);
-    __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
-    __shared__ T wsum[kSpmvThreads / 64];
-    __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
     constexpr int RPQ = (rsp::kSpmvMaxRows + kSpmvThreads) / kSpmvThreads;
-    const int b = xcd_swizzle(blockIdx.x, nblocks);
-    const SpmvBlock blk = blocks[b];
     const int tid = threadIdx.x;
     const int k0 = blk.k0, k1 = blk.k1;
     // the tile's row offsets, loaded ahead of the stream and parked in LDS
@@ -287,14 +295,14 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
         const int i = tid + q * kSpmvThreads;
         if (i <= nrows) rp_lds[i] = rpv[q];
     }
-    __syncthreads();
+    lds_barrier();
 
     if (blk.r1 < 0) {  // a long row: written whole, or a chunk partial for the fixup
         const T t = reduce_long(lds, k0 - kb, k1 - kb, wsum);
         if (tid == 0) {
             if (blk.r1 == rsp::kSpmvWholeRow) {
                 T out = alpha * t;
-                if (beta_nonzero) out += beta * y[blk.r0];
+                if (BETA) out += beta * y[blk.r0];
                 y[blk.r0] = out;
             } else {
                 partials[-(blk.r1 + 1)] = t;
@@ -310,13 +318,29 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     }
     reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, kb, [&](int rr, T sum) {
         T out = alpha * sum;
-        if (beta_nonzero) out += beta * y[r0 + rr];
+        if (BETA) out += beta * y[r0 + rr];
 #if RSP_NT_Y
         __builtin_nontemporal_store(out, y + r0 + rr);
 #else
         y[r0 + rr] = out;
 #endif
     });
+}
+
+// One workgroup per tile (XCD-swizzled). Measured alternatives, all slower
+// on the big set: 2/4/8 tiles walked per workgroup (-5/-10/
+// -18 %), all of a workgroup's tiles loaded up front (-4 %), a software-
+// pipelined persistent kernel (-29 %), one-wave tiles (-1 %).
+template <typename T, bool NT, bool BETA>
+__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
+    const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
+    const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
+    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok) {
+    __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
+    __shared__ T wsum[kSpmvThreads / 64];
+    __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
+    spmv_tile<T, NT, BETA>(blocks[xcd_swizzle(blockIdx.x, nblocks)], rowptr, colidx, vals, x, y,
+                           partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds);
 }
 
 // y[row] = alpha * sum(partials of the row, chunk order) (+ beta*y[row]).
@@ -343,7 +367,8 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     // vals/colidx are read once per call: non-temporal loads keep them from
     // evicting x (measured +2% fp64 / +7.5% fp32 on the cache-cold big set);
     // variant bit 0 restores default-policy loads for A/B runs
-    auto kern = (a.variant & 1) ? spmv_tiles<T, false> : spmv_tiles<T, true>;
+    auto kern = (a.variant & 1) ? (bnz ? spmv_tiles<T, false, true> : spmv_tiles<T, false, false>)
+                                : (bnz ? spmv_tiles<T, true, true> : spmv_tiles<T, true, false>);
     hipLaunchKernelGGL(kern, dim3(a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
                        (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks,
                        (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok);
@@ -363,8 +388,8 @@ int spmv_tiles_per_cu(int elem_bytes) {
     int o = 0;
     const hipError_t e =
         elem_bytes == 8
-            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, spmv_tiles<double, true>, kSpmvThreads, 0)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, spmv_tiles<float, true>, kSpmvThreads, 0);
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, spmv_tiles<double, true, false>, kSpmvThreads, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, spmv_tiles<float, true, false>, kSpmvThreads, 0);
     return (e == hipSuccess && o > 0) ? o : 1;
 }
 
