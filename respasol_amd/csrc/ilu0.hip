@@ -109,75 +109,11 @@ __device__ __forceinline__ void factor_row(const IluArgs &a, int i, int lane) {
     }
 }
 
-// Triangular solve of one row task. kind: 0 = L (op N), 1 = L^T (op T), 2 = U.
-// The structural operands of the first B terms (and x_i, u_ii) are fetched
-// by solve_fetch — for a thin run one level AHEAD, while the previous level
-// computes — so a level's critical path is only its y loads.
-template <typename T, int B>
-struct SolvePre {
-    rsp::RowTask t;
-    T xv, dv;
-    T v[B];
-    int c[B];
-};
-
-__device__ __forceinline__ rsp::RowTask load_task(const TrsvArgs &a, int slot, bool ok) {
-    rsp::RowTask t;
-    t.i = -1;
-    if (ok) t = a.plan.tasks[slot];
-    return t;
-}
-
-template <typename T, int KIND, int B>
-__device__ __forceinline__ void solve_fetch(const TrsvArgs &a, const rsp::RowTask &t, SolvePre<T, B> &f) {
-    f.t = t;
-    if (t.i < 0) return;
-    const T *vals = (const T *)a.vals;
-    f.xv = ((const T *)a.x)[t.i];
-    f.dv = (KIND == 2 && t.d >= 0) ? vals[t.d] : T(0);
-    const int n = t.p1 - t.p0;
-    if (n <= 0) return;
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        const int q = t.p0 + min(b, n - 1);
-        if constexpr (KIND == 1) {
-            f.c[b] = a.lt_col[q];
-            f.v[b] = vals[a.lt_src[q]];
-        } else {
-            f.c[b] = a.colidx[q];
-            f.v[b] = vals[q];
-        }
-    }
-}
-
-template <typename T, int KIND, int B>
-__device__ __forceinline__ void solve_compute(const TrsvArgs &a, const SolvePre<T, B> &f, T alpha) {
-    if (f.t.i < 0) return;
-    const T *vals = (const T *)a.vals;
-    T *y = (T *)a.y;
-    T s = alpha * f.xv;
-    const int n = f.t.p1 - f.t.p0;
-    if (n > 0) {
-        T yy[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) yy[b] = y[f.c[b]];
-#pragma unroll
-        for (int b = 0; b < B; ++b)
-            if (b < n) s = __builtin_fma(-f.v[b], yy[b], s);
-        if (n > B) {
-            if constexpr (KIND == 1) {
-                const int *src = a.lt_src, *col = a.lt_col;
-                s = fma_chain<T, B>(s, f.t.p0 + B, f.t.p1, [&](int q) { return vals[src[q]]; },
-                                    [&](int q) { return y[col[q]]; });
-            } else {
-                const int *ci = a.colidx;
-                s = fma_chain<T, B>(s, f.t.p0 + B, f.t.p1, [&](int p) { return vals[p]; },
-                                    [&](int p) { return y[ci[p]]; });
-            }
-        }
-    }
-    if constexpr (KIND == 2) s = s / f.dv;
-    y[f.t.i] = s;
+// LDS-only workgroup barrier (no vmcnt drain).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // --------------------------------------------------------------- kernels
@@ -201,37 +137,81 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_thin(IluArgs a, int lb, int
     }
 }
 
-// Fat level: one thread per row.
+// Triangular solves (kind 0 = L op N, 1 = L^T op T, 2 = U) over the DAG's
+// flat terms: y_i = (alpha x_i - sum_k vals[tpos[k]] * y[src[k]]) (/ u_ii),
+// one fma per term in the term order (for L^T: j descending).
+
+// Fat level: one thread per row, terms straight from global memory.
 template <typename T, int KIND, int B>
 __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, T alpha, int off, int nrows) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    SolvePre<T, B> f;
-    solve_fetch<T, KIND, B>(a, load_task(a, off + t, t < nrows), f);
-    solve_compute<T, KIND, B>(a, f, alpha);
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= nrows) return;
+    const rsp::RowTask t = a.plan.tasks[off + r];
+    const T *vals = (const T *)a.vals;
+    T *y = (T *)a.y;
+    const int *tpos = a.plan.tpos, *src = a.plan.src;
+    T s = fma_chain<T, B>(alpha * ((const T *)a.x)[t.i], t.t0, t.t1,
+                          [&](int k) { return vals[tpos[k]]; }, [&](int k) { return y[src[k]]; });
+    if constexpr (KIND == 2) s = s / (t.d >= 0 ? vals[t.d] : T(0));
+    y[t.i] = s;
 }
 
-// Thin run of levels [lb, le), each <= kThinThreads rows: thread t owns row
-// t of every level. Software pipeline over levels: while level l computes,
-// level l+1's operands and level l+2's task are already in flight.
+// Thin run (levels [lb, le) cut into chunks [c0, c1)), one 1024-thread
+// workgroup. Per chunk: a full barrier (every earlier y store visible), then
+// the chunk's tasks, x_i, u_ii, term values and — for terms whose y was
+// produced before the chunk and has left the LDS window — those y values are
+// staged in LDS by all threads at once (one memory round trip per chunk);
+// then the chunk's levels run on LDS alone: thread r computes row r of the
+// level, reading each y from the LDS window (src < 0: produced earlier in the
+// run, slot = run index mod kYWin) or from the staged copy, writes y to
+// global memory and to its window slot, and an LDS-only barrier separates
+// the levels. Same operation order as trsv_level.
 template <typename T, int KIND, int B>
-__global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, int lb, int le) {
-    const int t = threadIdx.x;
+__global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, int c0, int c1,
+                                                          int base) {
+    __shared__ T ywin[rsp::kYWin];
+    __shared__ T lval[rsp::kChunkTerms], lyv[rsp::kChunkTerms];
+    __shared__ int lsrc[rsp::kChunkTerms];
+    __shared__ rsp::RowTask ltask[rsp::kChunkRows];
+    __shared__ T lx[rsp::kChunkRows], ldg[rsp::kChunkRows];
+    const int tid = threadIdx.x;
+    const T *vals = (const T *)a.vals, *x = (const T *)a.x;
+    T *y = (T *)a.y;
     const int *ptr = a.plan.ptr_dev;
-    auto task_of = [&](int l) {
-        if (l >= le) return load_task(a, 0, false);
-        const int off = ptr[l];
-        return load_task(a, off + t, off + t < ptr[l + 1]);
-    };
-    SolvePre<T, B> cur, nxt;
-    solve_fetch<T, KIND, B>(a, task_of(lb), cur);
-    rsp::RowTask t1 = task_of(lb + 1);
-    for (int l = lb; l < le; ++l) {
-        const rsp::RowTask t2 = task_of(l + 2);
-        solve_fetch<T, KIND, B>(a, t1, nxt);
-        solve_compute<T, KIND, B>(a, cur, alpha);
+    for (int c = c0; c < c1; ++c) {
+        const rsp::LevelChunk ch = a.plan.chunks[c];
+        const int x0 = ptr[ch.l0], x1 = ptr[ch.l1];
+        const int k0 = a.plan.tasks[x0].t0, k1 = a.plan.tasks[x1 - 1].t1;
+        __syncthreads();  // the previous chunk's y stores are visible, LDS is free
+        for (int r = tid; r < x1 - x0; r += kThinThreads) {
+            const rsp::RowTask t = a.plan.tasks[x0 + r];
+            ltask[r] = t;
+            lx[r] = alpha * x[t.i];
+            ldg[r] = (KIND == 2 && t.d >= 0) ? vals[t.d] : T(0);
+        }
+        for (int k = tid; k < k1 - k0; k += kThinThreads) {
+            const int sc = a.plan.src[k0 + k];
+            lsrc[k] = sc;
+            lval[k] = vals[a.plan.tpos[k0 + k]];
+            lyv[k] = sc >= 0 ? y[sc] : T(0);
+        }
         __syncthreads();
-        cur = nxt;
-        t1 = t2;
+        for (int l = ch.l0; l < ch.l1; ++l) {
+            const int off = ptr[l] - x0, cnt = ptr[l + 1] - ptr[l];
+            if (tid < cnt) {
+                const rsp::RowTask t = ltask[off + tid];
+                T s = fma_chain<T, B>(lx[off + tid], t.t0 - k0, t.t1 - k0,
+                                      [&](int k) { return lval[k]; },
+                                      [&](int k) {
+                                          const int sc = lsrc[k];
+                                          return sc < 0 ? ywin[-sc - 1] : lyv[k];
+                                      });
+                if constexpr (KIND == 2) s = s / ldg[off + tid];
+                y[t.i] = s;
+                ywin[(ptr[l] + tid - base) & (rsp::kYWin - 1)] = s;
+            }
+            lds_barrier();
+        }
     }
 }
 
@@ -264,7 +244,7 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
             hipLaunchKernelGGL((trsv_thin<T, KIND, B>), dim3(1), dim3(kThinThreads), 0, s, a,
-                               alpha, sg.lb, sg.le);
+                               alpha, sg.c0, sg.c1, P.ptr_host[sg.lb]);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

@@ -50,7 +50,6 @@ struct rsp_ilu0_info {
     int structural_zero;         // -1 = none
     int factored;
     int *d_dpos, *d_hasdiag;
-    int *d_lt_ptr, *d_lt_src, *d_lt_col;
     int *d_upd_ptr, *d_upd_l, *d_upd_u, *d_lord, *d_lend;
     int *d_zero;
     long long n_updates;
@@ -58,7 +57,9 @@ struct rsp_ilu0_info {
     struct Dag {
         std::vector<int> ptr;                  // host level pointers
         int *d_rows = nullptr, *d_ptr = nullptr;
-        rsp::RowTask *d_tasks = nullptr;
+        rsp::RowTask *d_tasks = nullptr;       // solve: task per level-order slot
+        int *d_tpos = nullptr, *d_src = nullptr;  // solve: flat terms
+        rsp::LevelChunk *d_chunks = nullptr;   // solve: LDS-staged chunks of thin runs
         std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
         int batch = 8;                         // solve fma-chain batch
     } L, LT, U;
@@ -463,7 +464,7 @@ rsp_status_t rsp_scatter(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, c
 static void ilu_free_device(rsp_ilu0_info *f) {
     int **ptrs[] = {&f->d_dpos,     &f->d_hasdiag, &f->L.d_rows,  &f->L.d_ptr,
                     &f->LT.d_rows,  &f->LT.d_ptr,  &f->U.d_rows,  &f->U.d_ptr,
-                    &f->d_lt_ptr,   &f->d_lt_src,  &f->d_lt_col,  &f->d_zero,
+                    &f->d_zero,
                     &f->d_upd_ptr,  &f->d_upd_l,   &f->d_upd_u,   &f->d_lord,
                     &f->d_lend};
     for (int **p : ptrs) {
@@ -471,8 +472,11 @@ static void ilu_free_device(rsp_ilu0_info *f) {
         *p = nullptr;
     }
     for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) {
-        if (d->d_tasks) (void)hipFree(d->d_tasks);
-        d->d_tasks = nullptr;
+        for (void **p : {(void **)&d->d_tasks, (void **)&d->d_tpos, (void **)&d->d_src,
+                         (void **)&d->d_chunks}) {
+            if (*p) (void)hipFree(*p);
+            *p = nullptr;
+        }
     }
 }
 
@@ -484,7 +488,7 @@ rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
     f->structural_zero = -1;
     f->factored = 0;
     f->d_dpos = f->d_hasdiag = nullptr;
-    f->d_lt_ptr = f->d_lt_src = f->d_lt_col = f->d_zero = nullptr;
+    f->d_zero = nullptr;
     f->d_upd_ptr = f->d_upd_l = f->d_upd_u = f->d_lord = f->d_lend = nullptr;
     f->n_updates = 0;
     *info = f;
@@ -543,6 +547,114 @@ static int chain_batch(long long total, long long count) {
     const double mean = count > 0 ? (double)total / (double)count : 0.0;
     return mean <= 2.5 ? 2 : (mean <= 5.0 ? 4 : 8);
 }
+
+}  // extern "C" (C++ helpers)
+
+// Solve plan of one DAG (see LevelPlan): tasks in level order over flat
+// terms (term k of row i: matrix value at tpos[k], y of column col_of(k)),
+// segments (a level is thin if it has <= thin_rows rows and its terms fit one
+// chunk), the LDS-staged chunks of every thin run (<= kChunkRows rows and
+// <= kChunkTerms terms each), and the y source of every term of a thin run:
+// the LDS window slot (run index mod kYWin) if the column was produced earlier
+// in the run and no later row of the run can have reused that slot by the end
+// of the consumer's level, else the column (global y, or its value staged at
+// the chunk start — the producer is then in an earlier chunk or before the
+// run, so its store is visible after the chunk's full barrier).
+struct SolvePlan {
+    std::vector<rsp::RowTask> tasks;
+    std::vector<int> tpos, src;
+    std::vector<rsp::LevelSeg> segs;
+    std::vector<rsp::LevelChunk> chunks;
+};
+
+// row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
+template <typename RowTerms>
+static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
+                             int thin_rows, const std::vector<int> &diag, RowTerms row_terms,
+                             SolvePlan &sp) {
+    const int nlev = (int)ptr.size() - 1;
+    std::vector<int> col;
+    sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
+    sp.tpos.clear();
+    for (size_t x = 0; x < rows.size(); x++) {
+        const int i = rows[x];
+        rsp::RowTask &t = sp.tasks[x];
+        t.i = i;
+        t.t0 = (int)sp.tpos.size();
+        row_terms(i, [&](int tp, int c) {
+            sp.tpos.push_back(tp);
+            col.push_back(c);
+        });
+        t.t1 = (int)sp.tpos.size();
+        t.d = diag.empty() ? -1 : diag[(size_t)i];
+    }
+    sp.src = col;
+    // segments: runs of thin levels / fat levels
+    std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
+    for (int l = 0; l < nlev; l++)
+        if (ptr[(size_t)l + 1] > ptr[(size_t)l])
+            lterms[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l + 1] - 1].t1 - sp.tasks[(size_t)ptr[(size_t)l]].t0;
+    sp.segs.clear();
+    for (int l = 0; l < nlev; l++) {
+        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
+        const int thin = (cnt <= thin_rows && cnt <= rsp::kThinThreads && cnt <= rsp::kChunkRows &&
+                          lterms[(size_t)l] <= rsp::kChunkTerms) ? 1 : 0;
+        if (!sp.segs.empty() && sp.segs.back().thin == thin && sp.segs.back().le == l)
+            sp.segs.back().le = l + 1;
+        else
+            sp.segs.push_back({l, l + 1, thin, 0, 0});
+    }
+    // chunks of the thin runs + term sources
+    std::vector<int> slot_of((size_t)n, -1);
+    for (size_t x = 0; x < rows.size(); x++) slot_of[(size_t)rows[x]] = (int)x;
+    sp.chunks.clear();
+    for (rsp::LevelSeg &sg : sp.segs) {
+        if (!sg.thin) continue;
+        sg.c0 = (int)sp.chunks.size();
+        int crow = 0, cterm = 0;
+        for (int l = sg.lb; l < sg.le; l++) {
+            const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
+            if (sp.chunks.size() == (size_t)sg.c0 || crow + cnt > rsp::kChunkRows ||
+                cterm + lterms[(size_t)l] > rsp::kChunkTerms) {
+                sp.chunks.push_back({l, l + 1});
+                crow = 0;
+                cterm = 0;
+            } else {
+                sp.chunks.back().l1 = l + 1;
+            }
+            crow += cnt;
+            cterm += lterms[(size_t)l];
+        }
+        sg.c1 = (int)sp.chunks.size();
+        const int base = ptr[(size_t)sg.lb];
+        for (int l = sg.lb; l < sg.le; l++) {
+            const int r_end = ptr[(size_t)l + 1] - base;
+            for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++)
+                for (int k = sp.tasks[(size_t)x].t0; k < sp.tasks[(size_t)x].t1; k++) {
+                    const int sj = slot_of[(size_t)col[(size_t)k]];
+                    if (sj < base || sj >= ptr[(size_t)l]) continue;  // before the run
+                    const int rj = sj - base;
+                    if (r_end - rj <= rsp::kYWin) sp.src[(size_t)k] = -((rj & (rsp::kYWin - 1)) + 1);
+                }
+        }
+    }
+    if (sp.tpos.empty()) {  // keep the device arrays non-empty
+        sp.tpos.push_back(0);
+        sp.src.push_back(0);
+    }
+    if (sp.chunks.empty()) sp.chunks.push_back({0, 0});
+}
+
+template <typename V>
+static hipError_t upload_vec(V **dst, const std::vector<V> &v) {
+    size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(V);
+    hipError_t e = hipMalloc((void **)dst, bytes);
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpy(*dst, v.data(), v.size() * sizeof(V), hipMemcpyHostToDevice);
+    return e;
+}
+
+extern "C" {
 
 static hipError_t upload(int **dst, const std::vector<int> &v) {
     size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(int);
@@ -710,9 +822,6 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     // RSP_ILU_THIN_SOLVE / RSP_ILU_THIN_FACTOR: tuning knobs (0 = no thin runs)
     const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
     const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
-    f->L.segs = make_segs(f->L.ptr, thin_solve);
-    f->LT.segs = make_segs(f->LT.ptr, thin_solve);
-    f->U.segs = make_segs(f->U.ptr, thin_solve);
     f->fac_segs = make_segs(f->L.ptr, thin_factor);
     IluSymbolic sym;
     if (!ilu_symbolic(n, rp, ci, dpos, hasdiag, sym)) return RSP_STATUS_ALLOC_FAILED;
@@ -741,28 +850,31 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     if (e == hipSuccess) e = upload(&f->LT.d_ptr, f->LT.ptr);
     if (e == hipSuccess) e = upload(&f->U.d_rows, rows_u);
     if (e == hipSuccess) e = upload(&f->U.d_ptr, f->U.ptr);
-    if (e == hipSuccess) e = upload(&f->d_lt_ptr, ltp);
-    // solve tasks in level order
+    // solve plans (flat terms in level order, thin-run chunks, y sources)
+    std::vector<int> udiag((size_t)n);
+    for (int i = 0; i < n; i++) udiag[(size_t)i] = hasdiag[(size_t)i] ? dpos[(size_t)i] : -1;
     for (int kind = 0; kind < 3 && e == hipSuccess; kind++) {
         rsp_ilu0_info::Dag &d = kind == 0 ? f->L : (kind == 1 ? f->LT : f->U);
-        const std::vector<int> &rows = kind == 0 ? rows_l : (kind == 1 ? rows_lt : rows_u);
-        std::vector<rsp::RowTask> t(std::max<size_t>(rows.size(), 1));
-        for (size_t x = 0; x < rows.size(); x++) {
-            const int i = rows[x];
-            if (kind == 0)
-                t[x] = {i, rp[(size_t)i], dpos[(size_t)i], -1};
-            else if (kind == 1)
-                t[x] = {i, ltp[(size_t)i], ltp[(size_t)i + 1], -1};
-            else
-                t[x] = {i, dpos[(size_t)i] + hasdiag[(size_t)i], rp[(size_t)i + 1],
-                        hasdiag[(size_t)i] ? dpos[(size_t)i] : -1};
-        }
-        e = hipMalloc((void **)&d.d_tasks, t.size() * sizeof(rsp::RowTask));
-        if (e == hipSuccess)
-            e = hipMemcpy(d.d_tasks, t.data(), t.size() * sizeof(rsp::RowTask), hipMemcpyHostToDevice);
+        SolvePlan sp;
+        if (kind == 0)
+            build_solve_plan(n, d.ptr, rows_l, thin_solve, std::vector<int>(), [&](int i, auto emit) {
+                for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
+            }, sp);
+        else if (kind == 1)
+            build_solve_plan(n, d.ptr, rows_lt, thin_solve, std::vector<int>(), [&](int i, auto emit) {
+                for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++) emit(lts[(size_t)q], ltc[(size_t)q]);
+            }, sp);
+        else
+            build_solve_plan(n, d.ptr, rows_u, thin_solve, udiag, [&](int i, auto emit) {
+                for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++)
+                    emit(p, ci[(size_t)p]);
+            }, sp);
+        d.segs = sp.segs;
+        e = upload_vec(&d.d_tasks, sp.tasks);
+        if (e == hipSuccess) e = upload_vec(&d.d_tpos, sp.tpos);
+        if (e == hipSuccess) e = upload_vec(&d.d_src, sp.src);
+        if (e == hipSuccess) e = upload_vec(&d.d_chunks, sp.chunks);
     }
-    if (e == hipSuccess) e = upload(&f->d_lt_src, lts);
-    if (e == hipSuccess) e = upload(&f->d_lt_col, ltc);
     if (e == hipSuccess) e = hipMalloc((void **)&f->d_zero, sizeof(int));
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
     if (e != hipSuccess) {
@@ -814,6 +926,9 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<
     p.nseg = (int)segs.size();
     p.batch = batch;
     p.tasks = d.d_tasks;
+    p.tpos = d.d_tpos;
+    p.src = d.d_src;
+    p.chunks = d.d_chunks;
     return p;
 }
 
@@ -858,9 +973,6 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.x = x;
     a.y = y;
     a.alpha = (t == RSP_R_64F) ? *(const double *)alpha : (double)*(const float *)alpha;
-    a.lt_ptr = f->d_lt_ptr;
-    a.lt_src = f->d_lt_src;
-    a.lt_col = f->d_lt_col;
     a.plan = level_plan(f->L, f->L.segs, f->L.batch);
     return a;
 }

@@ -69,17 +69,22 @@ struct SpmvArgs {
 
 // Level schedule of one dependency DAG. Rows are grouped by level
 // (rows[ptr[l] .. ptr[l+1])); `segs` (host) cover the levels in order, each
-// {lev_begin, lev_end, thin}: a thin segment is a run of small levels that
-// one 1024-thread workgroup walks with __syncthreads() between levels (one
-// launch for the whole run); a fat segment is one launch per level.
+// {lev_begin, lev_end, thin, chunk_begin, chunk_end}: a thin segment is a run
+// of small levels that one 1024-thread workgroup walks with workgroup
+// barriers between levels (one launch for the whole run; a solve run is cut
+// into LDS-staged chunks [c0, c1) of `chunks`); a fat segment is one launch
+// per level.
 struct LevelSeg {
-    int lb, le, thin;
+    int lb, le, thin, c0, c1;
 };
-// Solve task of one row, stored in level order: the fma chain runs over
-// positions [p0, p1) (for L^T: slots of the transposed map), d = diagonal
-// position for the U solve (-1 = missing), unused otherwise.
+// Solve task of one row, stored in level order: the fma chain runs over the
+// flat terms [t0, t1) (term k: matrix value vals[tpos[k]] times the y given
+// by src[k]); d = diagonal position for the U solve (-1 = missing).
 struct alignas(16) RowTask {
-    int i, p0, p1, d;
+    int i, t0, t1, d;
+};
+struct alignas(8) LevelChunk {  // levels [l0, l1) of a thin solve run, staged in LDS together
+    int l0, l1;
 };
 
 struct LevelPlan {
@@ -90,12 +95,20 @@ struct LevelPlan {
     const LevelSeg *segs; // host
     int nseg;
     int batch;            // fma-chain load batch (2, 4, 8) from the mean chain length
-    const RowTask *tasks; // device, solve DAGs only: task of rows[x] at slot x
+    // solve DAGs only (device):
+    const RowTask *tasks; // task of rows[x] at slot x
+    const int *tpos;      // flat term -> position in vals
+    const int *src;       // flat term -> y source: >= 0 the column (global y, or its value
+                          // staged at the chunk start), < 0 slot -(s+1) of the LDS y window
+    const LevelChunk *chunks;
 };
-constexpr int kThinThreads = 1024;  // workgroup of a thin segment
-constexpr int kIluWaves = 4;        // rows per 256-thread workgroup (fat factor levels)
-constexpr int kThinSolveRows = 256;   // solve levels this small run inside a thin segment (<= kThinThreads)
-constexpr int kThinFactorRows = 32;   // factor levels (a wave per row: 16 rows per pass)
+constexpr int kYWin = 8192;          // LDS y window of a thin solve run (entries, power of 2)
+constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin)
+constexpr int kChunkTerms = 2048;    // terms staged per thin-run chunk
+constexpr int kThinThreads = 1024;   // workgroup of a thin segment
+constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels)
+constexpr int kThinSolveRows = 256;  // solve levels this small (and <= kChunkTerms terms) run thin
+constexpr int kThinFactorRows = 32;  // factor levels (a wave per row: 16 rows per pass)
 
 struct IluArgs {
     int n;
@@ -130,12 +143,7 @@ struct TrsvArgs {
     const void *x;
     void *y;
     double alpha;
-    // transposed strict-lower map (op == T): row i lists l_ji for j > i,
-    // j descending: lt_ptr[n+1], lt_src (positions in vals), lt_col (j).
-    const int *lt_ptr;
-    const int *lt_src;
-    const int *lt_col;
-    LevelPlan plan;
+    LevelPlan plan;       // the DAG of the solve (L, L^T or U), with its flat terms
 };
 
 }  // namespace rsp
