@@ -107,7 +107,7 @@ constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin
 constexpr int kChunkTerms = 2048;    // terms staged per thin-run chunk
 constexpr int kThinThreads = 1024;   // workgroup of a thin segment
 constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels)
-constexpr int kThinSolveRows = 256;  // solve levels this small (and <= kChunkTerms terms) run thin
+constexpr int kThinSolveRows = 1024; // solve levels this small (and <= kChunkTerms terms) run thin
 constexpr int kThinFactorRows = 32;  // factor levels (a wave per row: 16 rows per pass)
 
 struct IluArgs {
