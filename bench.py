@@ -349,7 +349,7 @@ def main():
             "hbm_gbps": round(hbm_gbs, 1),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "rsp_k::spmv_tiles<double,true>",
+                "kernel": "rsp_k::spmv_tiles<double,true,false>",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -68,7 +68,7 @@ def main():
     algb = sum(p["alg_bytes"] for p in steady) / len(steady)
     out = {
         "workload": args.workload,
-        "kernel": "rsp_k::spmv_tiles<double,true>",
+        "kernel": "rsp_k::spmv_tiles<double,true,false>",
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs; corrected by a "
                   "diagonal-matrix calibration launch of the same kernel with exactly known bytes",
         "calibration": {"read_bytes_per_counted_byte": rf, "write_bytes_per_counted_byte": wf,
