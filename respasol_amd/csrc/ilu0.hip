@@ -126,14 +126,87 @@ __global__ __launch_bounds__(64 * kIluWaves) void ilu0_level(IluArgs a, int off,
     factor_row<T, B>(a, a.plan.rows[off + w], threadIdx.x & 63);
 }
 
-// Thin run of levels [lb, le): one workgroup, 16 waves, one row per wave per pass.
-template <typename T, int B>
-__global__ __launch_bounds__(kThinThreads) void ilu0_thin(IluArgs a, int lb, int le) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int l = lb; l < le; ++l) {
-        const int off = a.plan.ptr_dev[l], cnt = a.plan.ptr_dev[l + 1] - off;
-        for (int r = wave; r < cnt; r += kThinThreads / 64) factor_row<T, B>(a, a.plan.rows[off + r], lane);
+// Thin run of the factor, chunk by chunk (rsp::FacChunk), one 1024-thread
+// workgroup. Per chunk: a full barrier (every earlier factor value is in
+// global memory and visible), then all threads stage in LDS the values of
+// the chunk's rows (cv, one slot per item), the item / update-pair index
+// lists, and the values of every u_kk / u_kj that comes from a row before the
+// chunk; the chunk's levels then run on LDS alone: wave w takes rows w, w+16,
+// ... of a level, each row stage by stage exactly as factor_row (same fma
+// order), writing every finished value to its LDS slot and to vals; an
+// LDS-only barrier separates the levels.
+template <typename T>
+__global__ __launch_bounds__(kThinThreads) void ilu0_chunked(IluArgs a, int c0, int c1) {
+    __shared__ T cv[rsp::kFacItems];
+    __shared__ T dpre[rsp::kFacItems];
+    __shared__ int lpos[rsp::kFacItems], lu0[rsp::kFacItems + 1], lsend[rsp::kFacItems], ld[rsp::kFacItems];
+    __shared__ T upre[rsp::kFacPairs];
+    __shared__ int lpl[rsp::kFacPairs], lpu[rsp::kFacPairs];
+    __shared__ rsp::FacRow lrow[rsp::kFacRows];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    T *vals = (T *)a.vals;
+    const int *ptr = a.plan.ptr_dev;
+    for (int c = c0; c < c1; ++c) {
+        const rsp::FacChunk ch = a.fchunks[c];
+        const int ni = ch.item1 - ch.item0, np = ch.pair1 - ch.pair0;
+        __syncthreads();  // earlier chunks' values visible, LDS free
+        for (int x = tid; x < ni; x += kThinThreads) {
+            const int g = ch.item0 + x;
+            const int pos = a.fpos[g], d = a.fd[g];
+            lpos[x] = pos;
+            cv[x] = vals[pos];
+            lu0[x] = a.fu0[g];
+            lsend[x] = a.fsend[g];
+            ld[x] = d;
+            dpre[x] = (d < 0 && d != INT_MIN) ? vals[-d - 1] : T(0);
+        }
+        if (tid == 0) lu0[ni] = np;
+        const int x0 = ptr[ch.l0], nr = ptr[ch.l1] - x0;
+        for (int r = tid; r < nr; r += kThinThreads) lrow[r] = a.frows[x0 + r];
+        for (int u = tid; u < np; u += kThinThreads) {
+            const int g = ch.pair0 + u;
+            const int pu = a.fpu[g];
+            lpl[u] = a.fpl[g];
+            lpu[u] = pu;
+            upre[u] = pu < 0 ? vals[-pu - 1] : T(0);
+        }
         __syncthreads();
+        for (int l = ch.l0; l < ch.l1; ++l) {
+            for (int x = ptr[l] + wave; x < ptr[l + 1]; x += kThinThreads / 64) {
+                const rsp::FacRow r = lrow[x - x0];
+                const int nitem = r.nitem_hd & ((1 << 30) - 1), hd = r.nitem_hd >> 30;
+                const int lo_end = r.item0 + r.nlow, end = r.item0 + nitem;
+                auto item = [&](int it) {
+                    T v = cv[it];
+                    for (int u = lu0[it]; u < lu0[it + 1]; ++u) {
+                        const int pu = lpu[u];
+                        v = __builtin_fma(-cv[lpl[u]], pu >= 0 ? cv[pu] : upre[u], v);
+                    }
+                    return v;
+                };
+                for (int st = r.item0; st < lo_end;) {
+                    const int e = lsend[st];
+                    for (int it = st + lane; it < e; it += 64) {
+                        const int d = ld[it];
+                        const T v = item(it) / (d >= 0 ? cv[d] : dpre[it]);
+                        cv[it] = v;
+                        vals[lpos[it]] = v;
+                    }
+                    // this stage's l_ik visible to the wave's next stage
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                    st = e;
+                }
+                for (int it = lo_end + lane; it < end; it += 64) {
+                    const T v = item(it);
+                    cv[it] = v;
+                    vals[lpos[it]] = v;
+                    if (it == lo_end && hd && v == T(0)) atomicMin(a.zero_pivot, r.i);
+                }
+            }
+            lds_barrier();
+        }
     }
 }
 
@@ -223,7 +296,7 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
-            hipLaunchKernelGGL((ilu0_thin<T, B>), dim3(1), dim3(kThinThreads), 0, s, a, sg.lb, sg.le);
+            hipLaunchKernelGGL((ilu0_chunked<T>), dim3(1), dim3(kThinThreads), 0, s, a, sg.c0, sg.c1);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

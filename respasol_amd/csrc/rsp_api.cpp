@@ -64,6 +64,10 @@ struct rsp_ilu0_info {
         int batch = 8;                         // solve fma-chain batch
     } L, LT, U;
     std::vector<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
+    rsp::FacChunk *d_fchunks = nullptr;        // LDS-staged factor chunks (thin runs)
+    rsp::FacRow *d_frows = nullptr;
+    int *d_fpos = nullptr, *d_fu0 = nullptr, *d_fsend = nullptr, *d_fd = nullptr;
+    int *d_fpl = nullptr, *d_fpu = nullptr;
     int fac_batch;
 };
 
@@ -471,6 +475,12 @@ static void ilu_free_device(rsp_ilu0_info *f) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
+    for (void **p : {(void **)&f->d_fchunks, (void **)&f->d_frows, (void **)&f->d_fpos,
+                     (void **)&f->d_fu0, (void **)&f->d_fsend, (void **)&f->d_fd, (void **)&f->d_fpl,
+                     (void **)&f->d_fpu}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
     for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) {
         for (void **p : {(void **)&d->d_tasks, (void **)&d->d_tpos, (void **)&d->d_src,
                          (void **)&d->d_chunks}) {
@@ -522,20 +532,6 @@ static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int>
     for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
 }
 
-// Consecutive levels of at most thin_max rows form one thin run (one
-// single-workgroup launch); the other levels are launched one by one.
-static std::vector<rsp::LevelSeg> make_segs(const std::vector<int> &ptr, int thin_max) {
-    std::vector<rsp::LevelSeg> segs;
-    const int nlev = (int)ptr.size() - 1;
-    for (int l = 0; l < nlev; l++) {
-        const int thin = (ptr[(size_t)l + 1] - ptr[(size_t)l]) <= thin_max ? 1 : 0;
-        if (!segs.empty() && segs.back().thin == thin && segs.back().le == l)
-            segs.back().le = l + 1;
-        else
-            segs.push_back({l, l + 1, thin});
-    }
-    return segs;
-}
 
 static int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
@@ -654,6 +650,119 @@ static hipError_t upload_vec(V **dst, const std::vector<V> &v) {
     return e;
 }
 
+// Symbolic ILU(0) data (built by ilu_symbolic below).
+struct IluSymbolic {
+    std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
+};
+
+// Factor plan of the L DAG (see IluArgs): segments (a level is thin if it
+// has <= thin_rows rows and its positions / update pairs fit one chunk), the
+// LDS-staged chunks of every thin run, and per chunk its items (the positions
+// of its rows: lower ones in intra-row stage order, then upper ones) and update
+// pairs with their sources: a chunk-local item when the producing row is in
+// the chunk, else the position (its final value is staged at the chunk start).
+struct FacPlan {
+    std::vector<rsp::LevelSeg> segs;
+    std::vector<rsp::FacChunk> chunks;
+    std::vector<rsp::FacRow> rows;  // per level-order slot
+    std::vector<int> pos, u0, send, d, pl, pu;
+};
+
+static void build_factor_plan(int n, const std::vector<int> &rp, const std::vector<int> &ci,
+                              const std::vector<int> &dpos, const std::vector<int> &hasdiag,
+                              const IluSymbolic &sym, const std::vector<int> &ptr,
+                              const std::vector<int> &rows, int thin_rows, FacPlan &fp) {
+    const int nlev = (int)ptr.size() - 1;
+    auto row_items = [&](int i) { return rp[(size_t)i + 1] - rp[(size_t)i]; };
+    auto row_pairs = [&](int i) {
+        return sym.upd_ptr[(size_t)rp[(size_t)i + 1]] - sym.upd_ptr[(size_t)rp[(size_t)i]];
+    };
+    std::vector<long long> litems((size_t)std::max(nlev, 1), 0), lpairs((size_t)std::max(nlev, 1), 0);
+    for (int l = 0; l < nlev; l++)
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
+            litems[(size_t)l] += row_items(rows[(size_t)x]);
+            lpairs[(size_t)l] += row_pairs(rows[(size_t)x]);
+        }
+    fp.segs.clear();
+    for (int l = 0; l < nlev; l++) {
+        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
+        const int thin = (cnt <= thin_rows && cnt <= rsp::kFacRows && litems[(size_t)l] <= rsp::kFacItems &&
+                          lpairs[(size_t)l] <= rsp::kFacPairs) ? 1 : 0;
+        if (!fp.segs.empty() && fp.segs.back().thin == thin && fp.segs.back().le == l)
+            fp.segs.back().le = l + 1;
+        else
+            fp.segs.push_back({l, l + 1, thin, 0, 0});
+    }
+    fp.rows.assign(std::max<size_t>(rows.size(), 1), rsp::FacRow{0, 0, 0, 0});
+    fp.chunks.clear();
+    fp.pos.clear(); fp.u0.clear(); fp.send.clear(); fp.d.clear(); fp.pl.clear(); fp.pu.clear();
+    std::vector<int> item_of((size_t)rp[(size_t)n], -1);
+    auto close_chunk = [&](rsp::FacChunk &ch) {
+        // items of the chunk's rows, then their update pairs and u_kk sources
+        for (int x = ptr[(size_t)ch.l0]; x < ptr[(size_t)ch.l1]; x++) {
+            const int i = rows[(size_t)x], rs = rp[(size_t)i], di = dpos[(size_t)i], re = rp[(size_t)i + 1];
+            const int b = (int)fp.pos.size() - ch.item0;
+            fp.rows[(size_t)x] = {i, b, di - rs, (re - rs) | (hasdiag[(size_t)i] << 30)};
+            for (int s2 = rs; s2 < di; s2++) {
+                const int p2 = sym.lord[(size_t)s2], k = ci[(size_t)p2];
+                item_of[(size_t)p2] = (int)fp.pos.size() - ch.item0;
+                fp.pos.push_back(p2);
+                fp.send.push_back(b + (sym.lend[(size_t)s2] - rs));
+                int dc = INT_MIN;  // u_kk of the lower item: row k is in an earlier level
+                if (hasdiag[(size_t)k]) {
+                    const int dk = dpos[(size_t)k];
+                    dc = item_of[(size_t)dk] >= 0 ? item_of[(size_t)dk] : -(dk + 1);
+                }
+                fp.d.push_back(dc);
+            }
+            for (int p2 = di; p2 < re; p2++) {
+                item_of[(size_t)p2] = (int)fp.pos.size() - ch.item0;
+                fp.pos.push_back(p2);
+                fp.send.push_back(0);
+                fp.d.push_back(INT_MIN);
+            }
+        }
+        ch.item1 = (int)fp.pos.size();
+        ch.pair0 = (int)fp.pl.size();
+        for (int it = ch.item0; it < ch.item1; it++) {
+            const int p2 = fp.pos[(size_t)it];
+            fp.u0.push_back((int)fp.pl.size() - ch.pair0);
+            for (int u = sym.upd_ptr[(size_t)p2]; u < sym.upd_ptr[(size_t)p2 + 1]; u++) {
+                fp.pl.push_back(item_of[(size_t)sym.upd_l[(size_t)u]]);
+                const int q = sym.upd_u[(size_t)u];
+                fp.pu.push_back(item_of[(size_t)q] >= 0 ? item_of[(size_t)q] : -(q + 1));
+            }
+        }
+        ch.pair1 = (int)fp.pl.size();
+        for (int it = ch.item0; it < ch.item1; it++) item_of[(size_t)fp.pos[(size_t)it]] = -1;
+        fp.chunks.push_back(ch);
+    };
+    for (rsp::LevelSeg &sg : fp.segs) {
+        if (!sg.thin) continue;
+        sg.c0 = (int)fp.chunks.size();
+        rsp::FacChunk ch{sg.lb, sg.lb, (int)fp.pos.size(), 0, 0, 0};
+        long long crow = 0, citem = 0, cpair = 0;
+        for (int l = sg.lb; l < sg.le; l++) {
+            const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
+            if (ch.l1 > ch.l0 && (crow + cnt > rsp::kFacRows || citem + litems[(size_t)l] > rsp::kFacItems ||
+                                  cpair + lpairs[(size_t)l] > rsp::kFacPairs)) {
+                close_chunk(ch);
+                ch = rsp::FacChunk{l, l, (int)fp.pos.size(), 0, 0, 0};
+                crow = citem = cpair = 0;
+            }
+            ch.l1 = l + 1;
+            crow += cnt;
+            citem += litems[(size_t)l];
+            cpair += lpairs[(size_t)l];
+        }
+        close_chunk(ch);
+        sg.c1 = (int)fp.chunks.size();
+    }
+    for (std::vector<int> *v : {&fp.pos, &fp.u0, &fp.send, &fp.d, &fp.pl, &fp.pu})
+        if (v->empty()) v->push_back(0);
+    if (fp.chunks.empty()) fp.chunks.push_back(rsp::FacChunk{0, 0, 0, 0, 0, 0});
+}
+
 extern "C" {
 
 static hipError_t upload(int **dst, const std::vector<int> &v) {
@@ -668,9 +777,6 @@ static hipError_t upload(int **dst, const std::vector<int> &v) {
 // intra-row stages of the lower positions. Row i is scattered into a dense
 // column -> position map, then each lower k (ascending) walks row k's upper
 // part; a hit at column j appends (pos l_ik, pos u_kj) to position (i, j).
-struct IluSymbolic {
-    std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
-};
 
 static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<int> &ci,
                          const std::vector<int> &dpos, const std::vector<int> &hasdiag,
@@ -822,9 +928,11 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     // RSP_ILU_THIN_SOLVE / RSP_ILU_THIN_FACTOR: tuning knobs (0 = no thin runs)
     const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
     const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
-    f->fac_segs = make_segs(f->L.ptr, thin_factor);
     IluSymbolic sym;
     if (!ilu_symbolic(n, rp, ci, dpos, hasdiag, sym)) return RSP_STATUS_ALLOC_FAILED;
+    FacPlan fplan;
+    build_factor_plan(n, rp, ci, dpos, hasdiag, sym, f->L.ptr, rows_l, thin_factor, fplan);
+    f->fac_segs = fplan.segs;
     f->n_updates = (long long)sym.upd_l.size();
     {
         long long nl = 0, nu = 0;
@@ -837,6 +945,14 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         f->fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
     }
     hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = upload_vec(&f->d_fchunks, fplan.chunks);
+    if (e == hipSuccess) e = upload_vec(&f->d_frows, fplan.rows);
+    if (e == hipSuccess) e = upload_vec(&f->d_fpos, fplan.pos);
+    if (e == hipSuccess) e = upload_vec(&f->d_fu0, fplan.u0);
+    if (e == hipSuccess) e = upload_vec(&f->d_fsend, fplan.send);
+    if (e == hipSuccess) e = upload_vec(&f->d_fd, fplan.d);
+    if (e == hipSuccess) e = upload_vec(&f->d_fpl, fplan.pl);
+    if (e == hipSuccess) e = upload_vec(&f->d_fpu, fplan.pu);
     if (e == hipSuccess) e = upload(&f->d_upd_ptr, sym.upd_ptr);
     if (e == hipSuccess) e = upload(&f->d_upd_l, sym.upd_l);
     if (e == hipSuccess) e = upload(&f->d_upd_u, sym.upd_u);
@@ -951,6 +1067,14 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.upd_u = f->d_upd_u;
     a.lord = f->d_lord;
     a.lend = f->d_lend;
+    a.fchunks = f->d_fchunks;
+    a.frows = f->d_frows;
+    a.fpos = f->d_fpos;
+    a.fu0 = f->d_fu0;
+    a.fsend = f->d_fsend;
+    a.fd = f->d_fd;
+    a.fpl = f->d_fpl;
+    a.fpu = f->d_fpu;
     a.plan = level_plan(f->L, f->fac_segs, f->fac_batch);
     hipError_t e;
     if (value_type == RSP_R_64F)

@@ -108,7 +108,23 @@ constexpr int kChunkTerms = 2048;    // terms staged per thin-run chunk
 constexpr int kThinThreads = 1024;   // workgroup of a thin segment
 constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels)
 constexpr int kThinSolveRows = 1024; // solve levels this small (and <= kChunkTerms terms) run thin
-constexpr int kThinFactorRows = 32;  // factor levels (a wave per row: 16 rows per pass)
+constexpr int kThinFactorRows = 64;  // factor levels this small (and fitting a chunk) run thin
+// LDS-staged factor chunks (ilu0_chunked): a chunk is a run of levels whose
+// rows' positions ("items") and update pairs fit these budgets.
+constexpr int kFacRows = 512;
+constexpr int kFacItems = 2048;
+constexpr int kFacPairs = 4096;
+struct alignas(8) FacChunk {
+    int l0, l1;        // levels
+    int item0, item1;  // flat item range
+    int pair0, pair1;  // flat update-pair range
+};
+// Factor row of a thin run, per level-order slot: its items are chunk-local
+// [item0, item0 + nitem), the first nlow in intra-row stage order (lower
+// positions), then the upper positions; hd = row has a diagonal.
+struct alignas(16) FacRow {
+    int i, item0, nlow, nitem_hd;  // nitem | hd << 30
+};
 
 struct IluArgs {
     int n;
@@ -131,6 +147,16 @@ struct IluArgs {
     const int *lord;
     const int *lend;
     LevelPlan plan;       // L DAG, factor thresholds
+    // LDS-staged thin runs (ilu0_chunked). Items: fpos = position in vals,
+    // fu0 = first update pair (chunk-local), fsend = end of the item's
+    // intra-row stage (chunk-local, lower items), fd = u_kk source of a lower
+    // item (>= 0 chunk-local item, INT_MIN none (u_kk = 0), else -(pos + 1):
+    // staged from vals). Pairs: fpl = chunk-local item of l_ik, fpu = u_kj
+    // source (>= 0 chunk-local item, else -(pos + 1): staged).
+    const FacChunk *fchunks;
+    const FacRow *frows;  // per level-order slot of the L DAG
+    const int *fpos, *fu0, *fsend, *fd;
+    const int *fpl, *fpu;
 };
 
 struct TrsvArgs {
