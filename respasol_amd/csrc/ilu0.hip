@@ -72,6 +72,29 @@ __device__ __forceinline__ T fma_chain(T s, int p0, int p1, FV vat, FY yat) {
     return s;
 }
 
+// The same serial fma chain for one long row, by a whole wave: lanes load 64
+// terms at once, then the chain runs over them in order on wave-uniform
+// registers (readlane), so a hub row pays one load round trip per 64 terms.
+__device__ __forceinline__ double wave_read(double v, int j) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, j), hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float wave_read(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+template <typename T, typename FV, typename FY>
+__device__ __forceinline__ T wave_chain(T s, int k0, int k1, int lane, FV vat, FY yat) {
+    for (int base = k0; base < k1; base += 64) {
+        const int k = min(base + lane, k1 - 1);
+        const T v = vat(k), yv = yat(k);
+        const int cnt = min(64, k1 - base);
+        for (int j = 0; j < cnt; ++j) s = __builtin_fma(-wave_read(v, j), wave_read(yv, j), s);
+    }
+    return s;
+}
+
 // One position of the factor, pull form: v = a_p - sum_k l_ik u_kj over the
 // position's update list (k ascending, one fma each — the same sequence of
 // roundings as the IKJ loop).
@@ -143,6 +166,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_chunked(IluArgs a, int c0, 
     __shared__ T upre[rsp::kFacPairs];
     __shared__ int lpl[rsp::kFacPairs], lpu[rsp::kFacPairs];
     __shared__ rsp::FacRow lrow[rsp::kFacRows];
+    __shared__ int lptr[rsp::kFacRows + 1];  // a chunk has <= kFacRows levels
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     T *vals = (T *)a.vals;
     const int *ptr = a.plan.ptr_dev;
@@ -163,6 +187,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_chunked(IluArgs a, int c0, 
         if (tid == 0) lu0[ni] = np;
         const int x0 = ptr[ch.l0], nr = ptr[ch.l1] - x0;
         for (int r = tid; r < nr; r += kThinThreads) lrow[r] = a.frows[x0 + r];
+        for (int q = tid; q <= ch.l1 - ch.l0; q += kThinThreads) lptr[q] = ptr[ch.l0 + q];
         for (int u = tid; u < np; u += kThinThreads) {
             const int g = ch.pair0 + u;
             const int pu = a.fpu[g];
@@ -172,7 +197,8 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_chunked(IluArgs a, int c0, 
         }
         __syncthreads();
         for (int l = ch.l0; l < ch.l1; ++l) {
-            for (int x = ptr[l] + wave; x < ptr[l + 1]; x += kThinThreads / 64) {
+            const int xe = lptr[l - ch.l0 + 1];
+            for (int x = lptr[l - ch.l0] + wave; x < xe; x += kThinThreads / 64) {
                 const rsp::FacRow r = lrow[x - x0];
                 const int nitem = r.nitem_hd & ((1 << 30) - 1), hd = r.nitem_hd >> 30;
                 const int lo_end = r.item0 + r.nlow, end = r.item0 + nitem;
@@ -214,17 +240,31 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_chunked(IluArgs a, int c0, 
 // flat terms: y_i = (alpha x_i - sum_k vals[tpos[k]] * y[src[k]]) (/ u_ii),
 // one fma per term in the term order (for L^T: j descending).
 
-// Fat level: one thread per row, terms straight from global memory.
+// Fat level, terms straight from global memory: blocks [0, nb) one thread
+// per short row (the level's first nshort rows), the blocks after them one
+// wave per long row.
 template <typename T, int KIND, int B>
-__global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, T alpha, int off, int nrows) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= nrows) return;
-    const rsp::RowTask t = a.plan.tasks[off + r];
+__global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, T alpha, int off, int nrows,
+                                                  int nshort, int nb) {
     const T *vals = (const T *)a.vals;
     T *y = (T *)a.y;
     const int *tpos = a.plan.tpos, *src = a.plan.src;
-    T s = fma_chain<T, B>(alpha * ((const T *)a.x)[t.i], t.t0, t.t1,
-                          [&](int k) { return vals[tpos[k]]; }, [&](int k) { return y[src[k]]; });
+    auto vat = [&](int k) { return vals[tpos[k]]; };
+    auto yat = [&](int k) { return y[src[k]]; };
+    T s;
+    rsp::RowTask t;
+    if ((int)blockIdx.x < nb) {
+        const int r = blockIdx.x * 256 + threadIdx.x;
+        if (r >= nshort) return;
+        t = a.plan.tasks[off + r];
+        s = fma_chain<T, B>(alpha * ((const T *)a.x)[t.i], t.t0, t.t1, vat, yat);
+    } else {
+        const int r = nshort + (blockIdx.x - nb) * 4 + (threadIdx.x >> 6);
+        if (r >= nrows) return;
+        t = a.plan.tasks[off + r];
+        s = wave_chain<T>(alpha * ((const T *)a.x)[t.i], t.t0, t.t1, threadIdx.x & 63, vat, yat);
+        if ((threadIdx.x & 63) != 0) return;
+    }
     if constexpr (KIND == 2) s = s / (t.d >= 0 ? vals[t.d] : T(0));
     y[t.i] = s;
 }
@@ -247,6 +287,7 @@ __global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, i
     __shared__ int lsrc[rsp::kChunkTerms];
     __shared__ rsp::RowTask ltask[rsp::kChunkRows];
     __shared__ T lx[rsp::kChunkRows], ldg[rsp::kChunkRows];
+    __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];  // a chunk has <= kChunkRows levels
     const int tid = threadIdx.x;
     const T *vals = (const T *)a.vals, *x = (const T *)a.x;
     T *y = (T *)a.y;
@@ -268,20 +309,34 @@ __global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, i
             lval[k] = vals[a.plan.tpos[k0 + k]];
             lyv[k] = sc >= 0 ? y[sc] : T(0);
         }
+        for (int q = tid; q <= ch.l1 - ch.l0; q += kThinThreads) {
+            lptr[q] = ptr[ch.l0 + q];
+            if (q < ch.l1 - ch.l0) lns[q] = a.plan.nshort[ch.l0 + q];
+        }
         __syncthreads();
         for (int l = ch.l0; l < ch.l1; ++l) {
-            const int off = ptr[l] - x0, cnt = ptr[l + 1] - ptr[l];
-            if (tid < cnt) {
+            const int lp = lptr[l - ch.l0], off = lp - x0, cnt = lptr[l - ch.l0 + 1] - lp,
+                      ns = lns[l - ch.l0];
+            auto vat = [&](int k) { return lval[k]; };
+            auto yat = [&](int k) {
+                const int sc = lsrc[k];
+                return sc < 0 ? ywin[-sc - 1] : lyv[k];
+            };
+            if (tid < ns) {
                 const rsp::RowTask t = ltask[off + tid];
-                T s = fma_chain<T, B>(lx[off + tid], t.t0 - k0, t.t1 - k0,
-                                      [&](int k) { return lval[k]; },
-                                      [&](int k) {
-                                          const int sc = lsrc[k];
-                                          return sc < 0 ? ywin[-sc - 1] : lyv[k];
-                                      });
+                T s = fma_chain<T, B>(lx[off + tid], t.t0 - k0, t.t1 - k0, vat, yat);
                 if constexpr (KIND == 2) s = s / ldg[off + tid];
                 y[t.i] = s;
-                ywin[(ptr[l] + tid - base) & (rsp::kYWin - 1)] = s;
+                ywin[(lp + tid - base) & (rsp::kYWin - 1)] = s;
+            }
+            for (int r = ns + (tid >> 6); r < cnt; r += kThinThreads / 64) {  // long rows: a wave each
+                const rsp::RowTask t = ltask[off + r];
+                T s = wave_chain<T>(lx[off + r], t.t0 - k0, t.t1 - k0, tid & 63, vat, yat);
+                if constexpr (KIND == 2) s = s / ldg[off + r];
+                if ((tid & 63) == 0) {
+                    y[t.i] = s;
+                    ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
+                }
             }
             lds_barrier();
         }
@@ -323,8 +378,9 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
         for (int l = sg.lb; l < sg.le; ++l) {
             const int off = P.ptr_host[l], cnt = P.ptr_host[l + 1] - off;
             if (cnt <= 0) continue;
-            hipLaunchKernelGGL((trsv_level<T, KIND, B>), dim3((cnt + 255) / 256), dim3(256), 0, s,
-                               a, alpha, off, cnt);
+            const int ns = P.nshort_host[l], nb = (ns + 255) / 256;
+            hipLaunchKernelGGL((trsv_level<T, KIND, B>), dim3(nb + (cnt - ns + 3) / 4), dim3(256), 0,
+                               s, a, alpha, off, cnt, ns, nb);
         }
     }
     return hipGetLastError();

@@ -60,6 +60,8 @@ struct rsp_ilu0_info {
         rsp::RowTask *d_tasks = nullptr;       // solve: task per level-order slot
         int *d_tpos = nullptr, *d_src = nullptr;  // solve: flat terms
         rsp::LevelChunk *d_chunks = nullptr;   // solve: LDS-staged chunks of thin runs
+        int *d_nshort = nullptr;               // solve: short rows per level (device)
+        std::vector<int> nshort;               // (host)
         std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
         int batch = 8;                         // solve fma-chain batch
     } L, LT, U;
@@ -483,7 +485,7 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     }
     for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) {
         for (void **p : {(void **)&d->d_tasks, (void **)&d->d_tpos, (void **)&d->d_src,
-                         (void **)&d->d_chunks}) {
+                         (void **)&d->d_chunks, (void **)&d->d_nshort}) {
             if (*p) (void)hipFree(*p);
             *p = nullptr;
         }
@@ -557,6 +559,7 @@ static int chain_batch(long long total, long long count) {
 // the chunk start — the producer is then in an earlier chunk or before the
 // run, so its store is visible after the chunk's full barrier).
 struct SolvePlan {
+    std::vector<int> nshort;  // per level
     std::vector<rsp::RowTask> tasks;
     std::vector<int> tpos, src;
     std::vector<rsp::LevelSeg> segs;
@@ -569,11 +572,24 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
                              int thin_rows, const std::vector<int> &diag, RowTerms row_terms,
                              SolvePlan &sp) {
     const int nlev = (int)ptr.size() - 1;
+    // within each level: rows of <= kLongTerms terms first (a thread each),
+    // longer rows after them (a wave each)
+    std::vector<int> order(rows);
+    sp.nshort.assign((size_t)std::max(nlev, 1), 0);
+    for (int l = 0; l < nlev; l++) {
+        auto b = order.begin() + ptr[(size_t)l], e = order.begin() + ptr[(size_t)l + 1];
+        auto mid = std::stable_partition(b, e, [&](int i) {
+            int cnt = 0;
+            row_terms(i, [&](int, int) { cnt++; });
+            return cnt <= rsp::kLongTerms;
+        });
+        sp.nshort[(size_t)l] = (int)(mid - b);
+    }
     std::vector<int> col;
     sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
     sp.tpos.clear();
-    for (size_t x = 0; x < rows.size(); x++) {
-        const int i = rows[x];
+    for (size_t x = 0; x < order.size(); x++) {
+        const int i = order[x];
         rsp::RowTask &t = sp.tasks[x];
         t.i = i;
         t.t0 = (int)sp.tpos.size();
@@ -602,7 +618,7 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     }
     // chunks of the thin runs + term sources
     std::vector<int> slot_of((size_t)n, -1);
-    for (size_t x = 0; x < rows.size(); x++) slot_of[(size_t)rows[x]] = (int)x;
+    for (size_t x = 0; x < order.size(); x++) slot_of[(size_t)order[x]] = (int)x;
     sp.chunks.clear();
     for (rsp::LevelSeg &sg : sp.segs) {
         if (!sg.thin) continue;
@@ -986,7 +1002,9 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
                     emit(p, ci[(size_t)p]);
             }, sp);
         d.segs = sp.segs;
+        d.nshort = sp.nshort;
         e = upload_vec(&d.d_tasks, sp.tasks);
+        if (e == hipSuccess) e = upload_vec(&d.d_nshort, sp.nshort);
         if (e == hipSuccess) e = upload_vec(&d.d_tpos, sp.tpos);
         if (e == hipSuccess) e = upload_vec(&d.d_src, sp.src);
         if (e == hipSuccess) e = upload_vec(&d.d_chunks, sp.chunks);
@@ -1045,6 +1063,8 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<
     p.tpos = d.d_tpos;
     p.src = d.d_src;
     p.chunks = d.d_chunks;
+    p.nshort = d.d_nshort;
+    p.nshort_host = d.nshort.data();
     return p;
 }
 

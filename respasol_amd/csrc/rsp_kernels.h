@@ -101,7 +101,10 @@ struct LevelPlan {
     const int *src;       // flat term -> y source: >= 0 the column (global y, or its value
                           // staged at the chunk start), < 0 slot -(s+1) of the LDS y window
     const LevelChunk *chunks;
+    const int *nshort;    // per level: rows with <= kLongTerms terms come first (host copy: nshort_host)
+    const int *nshort_host;
 };
+constexpr int kLongTerms = 64;       // solve rows with more terms are done by a whole wave
 constexpr int kYWin = 8192;          // LDS y window of a thin solve run (entries, power of 2)
 constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin)
 constexpr int kChunkTerms = 2048;    // terms staged per thin-run chunk
