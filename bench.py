@@ -54,7 +54,7 @@ class Slice:
     """One matrix's share on this rank: its rows [r0, r1) (nnz-balanced split),
     generated locally, with the column layout of the chosen exchange."""
 
-    def __init__(self, name, rank, world, handle, device, exchange):
+    def __init__(self, name, rank, world, handle, device, exchange, overlap=False):
         self.name = name
         m = csr.surrogate_rows(name)
         lens = csr.surrogate_rowlens(name)
@@ -81,6 +81,9 @@ class Slice:
         self.host = (rp, ci_dev, va)
         self.mat64 = SpMat(handle, *upload_csr(rp, ci_dev, va, torch.float64, device), self.n_x)
         self.mat32 = SpMat(handle, *upload_csr(rp, ci_dev, va, torch.float32, device), self.n_x)
+        if self.mode == "halo" and overlap:  # interior tiles (own columns only) run under the exchange
+            self.mat64.set_local_cols(self.m_local)
+            self.mat32.set_local_cols(self.m_local)
         self.y64 = torch.empty(max(self.m_local, 1), dtype=torch.float64, device=device)
         self.y32 = torch.empty(max(self.m_local, 1), dtype=torch.float32, device=device)
         if self.mode != "halo":  # replicated x (padded layout for the all-gather)
@@ -168,6 +171,9 @@ def main():
                     help="N>1 x exchange: halo-only all_to_all (default) or full all-gather")
     ap.add_argument("--no-bucket", action="store_true",
                     help="halo mode: one exchange per matrix instead of one per step")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="halo mode: finish the exchange before any SpMV instead of running the "
+                         "interior tiles under it")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
@@ -187,7 +193,8 @@ def main():
     names = workload_names(args.workload)
 
     t_setup = time.perf_counter()
-    slices = [Slice(n, rank, world, handle, device, args.exchange) for n in names]
+    overlap = world > 1 and args.exchange == "halo" and not args.no_overlap
+    slices = [Slice(n, rank, world, handle, device, args.exchange, overlap) for n in names]
     exchanges64, exchanges32 = [], []
     if world > 1 and args.exchange == "halo":
         groups = [[i] for i in range(len(slices))] if args.no_bucket else [list(range(len(slices)))]
@@ -209,6 +216,18 @@ def main():
     first_of = {g[0]: ex for g, ex in exchanges64}  # halo: exchange before a group's first SpMV
 
     def step(exchange=True, events=None):
+        if exchange and overlap:
+            # halo overlap: start every exchange, interior tiles of every matrix
+            # (own columns only), join the exchanges, then the boundary tiles
+            for _, ex in exchanges64:
+                ex.start()
+            for s in slices:
+                s.mat64.spmv_part(s.x64(), s.y64, 1)
+            for _, ex in exchanges64:
+                ex.finish()
+            for s in slices:
+                s.mat64.spmv_part(s.x64(), s.y64, 2)
+            return
         for i, s in enumerate(slices):
             if exchange:
                 if s.mode == "allgather":
@@ -241,6 +260,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    big = max(slices, key=lambda s: s.nnz_global)
+    y_step_t = big.y64.clone()  # checked against a whole SpMV below
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -297,10 +318,10 @@ def main():
     # parity spot check of this rank's slice of the largest matrix vs the oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind as ob
-    big = max(slices, key=lambda s: s.nnz_global)
     xf = big.x64().cpu().numpy()
     rp, ci_dev, va = big.host
     ref = ob.spmv(rp, ci_dev, va, xf, threads=True)
+    y_step = y_step_t.cpu().numpy()[: big.m_local]  # as the last timed step left it
     got = big.mat64.spmv(big.x64()).cpu().numpy()[: big.m_local]
     bound = ob.spmv_bound(rp, ci_dev, va, xf, 2.0 ** -53)
     # the exchanged x must hold exactly the global x entries the slice references
@@ -309,7 +330,9 @@ def main():
         xg = csr.dlarnv(1, [0, 0, 0, 1], big.n)[0]
         cols = np.concatenate([c for c in big.halo.recv_cols])
         ok_x = np.array_equal(xf[big.m_local:], xg[cols]) and np.array_equal(xf[: big.m_local], xg[big.r0:big.r1])
-    check_ok = bool(np.all(np.abs(got - ref) <= bound)) and ok_x
+    # the step's y (overlapped split at N > 1) equals one whole SpMV bit for bit
+    ok_step = np.array_equal(y_step, got) if big.m_local else True
+    check_ok = bool(np.all(np.abs(got - ref) <= bound)) and ok_x and ok_step
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -339,6 +362,7 @@ def main():
                 "parallelism": f"row-partition x{world}" if world > 1 else "1 GPU",
                 "collective": (("halo all_to_all_single" + ("" if args.no_bucket else
                                  " (one per step, bucketed over the matrices)")
+                                 + (", interior tiles overlapped" if overlap else "")
                                  if args.exchange == "halo" else "all_gather_into_tensor")
                                + f" over {args.dist_backend}"
                                + (" (RCCL, xGMI)" if args.dist_backend == "nccl" else " (rehearsal)"))

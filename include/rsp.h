@@ -179,6 +179,19 @@ rsp_status_t rsp_gather(rsp_handle_t handle, rsp_datatype_t value_type, int64_t 
 rsp_status_t rsp_scatter(rsp_handle_t handle, rsp_datatype_t value_type, int64_t n,
                          const int64_t *d_idx, const void *d_src, void *d_dst);
 
+/* Overlap of the halo exchange with the SpMV. Columns [0, ncols_local) of
+ * `mat` are the rank's own x entries, the others arrive with the exchange.
+ * Set before rsp_spmv_preprocess (a later call re-plans): the schedule then
+ * puts the tiles that read own columns only first. rsp_spmv_part runs
+ * part 1 = those interior tiles (launch it while the exchange is in flight),
+ * part 2 = the remaining tiles and the long-row fixup; part 0 = everything
+ * (== rsp_spmv). Part 1 followed by part 2 gives y bit for bit equal to
+ * rsp_spmv. beta must be 0 for parts 1 and 2. */
+rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local);
+rsp_status_t rsp_spmv_part(rsp_handle_t handle, const void *alpha, rsp_spmat_t mat,
+                           const void *d_x, const void *beta, void *d_y,
+                           rsp_datatype_t compute_type, void *d_buffer, int part);
+
 /* Number of dependency levels found by the analysis (L DAG, L^T DAG). */
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *levels_upper);
 

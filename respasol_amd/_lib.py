@@ -104,6 +104,8 @@ RSP_PROTOS = {
     "rsp_ilu0_levels": (i32, [vp, ip, ip]),
     "rsp_gather": (i32, [vp, i32, i64, vp, vp, vp]),
     "rsp_scatter": (i32, [vp, i32, i64, vp, vp, vp]),
+    "rsp_spmat_set_local_cols": (i32, [vp, i64]),
+    "rsp_spmv_part": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, i32]),
 }
 
 HOST_PROTOS = {

@@ -41,6 +41,8 @@ struct rsp_spmat {
     int nblocks, nlong, nslots;
     int nnz_s;                  // rowptr[rows] seen by the preprocess
     size_t off_long, off_part;  // byte offsets inside the buffer
+    int64_t local_cols;         // rsp_spmat_set_local_cols (-1: not split)
+    int nint;                   // interior tiles at the front of the schedule
 };
 
 struct rsp_ilu0_info {
@@ -176,7 +178,15 @@ rsp_status_t rsp_create_csr(rsp_spmat_t *mat, int64_t rows, int64_t cols, int64_
     a->vals = d_values;
     a->type = value_type;
     a->plan_buffer = nullptr;
+    a->local_cols = -1;
     *mat = a;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local) {
+    if (!mat || ncols_local < 0 || ncols_local > mat->cols) return RSP_STATUS_INVALID_VALUE;
+    mat->local_cols = ncols_local;
+    mat->plan_buffer = nullptr;  // re-plan on the next call
     return RSP_STATUS_SUCCESS;
 }
 
@@ -333,9 +343,10 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     // Column indices are gathered unchecked by the kernel: validate them once
     // here (preprocess is outside the timed loop) so a malformed matrix is an
     // INVALID_VALUE status, never an out-of-bounds read of x on the GPU.
+    std::vector<int> ci;
     if (m > 0 && rp[(size_t)m] > 0) {
         if (!mat->colidx) return RSP_STATUS_INVALID_VALUE;
-        std::vector<int> ci((size_t)rp[(size_t)m]);
+        ci.resize((size_t)rp[(size_t)m]);
         RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), mat->colidx, ci.size() * sizeof(int),
                                      hipMemcpyDeviceToHost, h->stream));
         RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
@@ -376,6 +387,19 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
             }
         }
     }
+    // split schedule (rsp_spmat_set_local_cols): tiles reading own columns
+    // only first; long-row tiles always in the second part (with the fixup)
+    int nint = 0;
+    if (mat->local_cols >= 0) {
+        auto interior = [&](const SpmvBlock &b) {
+            if (b.r1 < 0) return false;
+            for (int k = b.k0; k < b.k1; k++)
+                if (ci[(size_t)k] >= mat->local_cols) return false;
+            return true;
+        };
+        auto mid = std::stable_partition(blocks.begin(), blocks.end(), interior);
+        nint = (int)(mid - blocks.begin());
+    }
     // the caller sized the buffer from mat->nnz; make sure the plan fits
     // (bounds in units of the chunk, which is <= the packing cap)
     SpmvBounds b = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), chunk);
@@ -396,6 +420,7 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     mat->plan_buffer = d_buffer;
     mat->plan_type = compute_type;
     mat->nblocks = (int)blocks.size();
+    mat->nint = nint;
     mat->nlong = (int)longrows.size();
     mat->nslots = nslots;
     mat->nnz_s = m > 0 ? rp[(size_t)m] : 0;
@@ -404,9 +429,9 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     return RSP_STATUS_SUCCESS;
 }
 
-rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
-                      const void *d_x, const void *beta, void *d_y, rsp_datatype_t compute_type,
-                      void *d_buffer) {
+static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
+                             const void *d_x, const void *beta, void *d_y,
+                             rsp_datatype_t compute_type, void *d_buffer, int part) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     if (!mat || !alpha || !beta) return RSP_STATUS_INVALID_VALUE;
     if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
@@ -436,6 +461,16 @@ rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp
         a.alpha = *(const float *)alpha;
         a.beta = *(const float *)beta;
     }
+    if (part != 0) {  // split schedule: part 1 = interior tiles, part 2 = the rest + fixup
+        if (a.beta != 0.0) return RSP_STATUS_INVALID_VALUE;
+        if (part == 1) {
+            a.nblocks = mat->nint;
+            a.nlong = 0;
+        } else {
+            a.blocks += mat->nint;
+            a.nblocks = mat->nblocks - mat->nint;
+        }
+    }
     a.vector_ok = ((((uintptr_t)mat->colidx) | ((uintptr_t)mat->vals)) & 15) == 0;
     a.nnz = mat->nnz_s;
     a.variant = h->spmv_variant;
@@ -445,6 +480,20 @@ rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp
     else
         e = h->ftz ? rsp_k_ftz::spmv_f32(a, h->stream) : rsp_k::spmv_f32(a, h->stream);
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
+                      const void *d_x, const void *beta, void *d_y, rsp_datatype_t compute_type,
+                      void *d_buffer) {
+    return spmv_run(h, op, alpha, mat, d_x, beta, d_y, compute_type, d_buffer, 0);
+}
+
+rsp_status_t rsp_spmv_part(rsp_handle_t h, const void *alpha, rsp_spmat_t mat, const void *d_x,
+                           const void *beta, void *d_y, rsp_datatype_t compute_type,
+                           void *d_buffer, int part) {
+    if (part < 0 || part > 2) return RSP_STATUS_INVALID_VALUE;
+    return spmv_run(h, RSP_OPERATION_NON_TRANSPOSE, alpha, mat, d_x, beta, d_y, compute_type,
+                    d_buffer, part);
 }
 
 rsp_status_t rsp_gather(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, const int64_t *d_idx,

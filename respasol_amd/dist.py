@@ -222,6 +222,7 @@ class HaloExchange:
         self.unpack_idx = torch.from_numpy(cat(unpack)).to(self.device)
         self.sendbuf = torch.empty(max(self.pack_idx.numel(), 1), dtype=dtype, device=self.device)
         self.recvbuf = torch.empty(max(self.unpack_idx.numel(), 1), dtype=dtype, device=self.device)
+        self._work = None
 
     def x_ext(self, i: int) -> torch.Tensor:
         return self.arena[int(self.offsets[i]):int(self.offsets[i + 1])]
@@ -234,19 +235,43 @@ class HaloExchange:
         return int(self.pack_idx.numel() + self.unpack_idx.numel()) * self.arena.element_size()
 
     def exchange(self) -> None:
+        self.start()
+        self.finish()
+
+    def start(self) -> None:
+        """Pack and launch the all-to-all (asynchronous on RCCL: the local,
+        interior part of the SpMV can run meanwhile; finish() joins it)."""
+        self._work = None
         if self.P <= 1:
             return
         n_send, n_recv = self.pack_idx.numel(), self.unpack_idx.numel()
         if self.device.type == "cuda":
-            from .sparse import gather, scatter
+            from .sparse import gather
             if n_send:
                 gather(self.handle, self.pack_idx, self.arena, self.sendbuf)
-            _a2a(self.recvbuf[:n_recv], self.sendbuf[:n_send], self.recv_split, self.send_split,
-                 self.group)
-            if n_recv:
-                scatter(self.handle, self.unpack_idx, self.recvbuf, self.arena)
+            if dist.get_backend(self.group) == "gloo":  # rehearsal: synchronous, staged
+                _a2a(self.recvbuf[:n_recv], self.sendbuf[:n_send], self.recv_split, self.send_split,
+                     self.group)
+            else:
+                self._work = dist.all_to_all_single(self.recvbuf[:n_recv], self.sendbuf[:n_send],
+                                                    list(self.recv_split), list(self.send_split),
+                                                    group=self.group, async_op=True)
         else:  # CPU tensors: gloo tests of the host logic
             self.sendbuf[:n_send] = self.arena[self.pack_idx]
             dist.all_to_all_single(self.recvbuf[:n_recv], self.sendbuf[:n_send],
                                    list(self.recv_split), list(self.send_split), group=self.group)
+
+    def finish(self) -> None:
+        """Wait for the all-to-all (on the current stream) and unpack the halos."""
+        if self.P <= 1:
+            return
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        n_recv = self.unpack_idx.numel()
+        if self.device.type == "cuda":
+            from .sparse import scatter
+            if n_recv:
+                scatter(self.handle, self.unpack_idx, self.recvbuf, self.arena)
+        else:
             self.arena[self.unpack_idx] = self.recvbuf[:n_recv]

@@ -58,6 +58,24 @@ class Handle:
         self.ftz = bool(on)
         check(rsp.rsp_set_ftz(self._h, 1 if on else 0), "rsp_set_ftz")
 
+    def set_local_cols(self, ncols_local: int) -> None:
+        """Split the schedule for halo overlap (rsp_spmat_set_local_cols): tiles
+        reading columns < ncols_local only (the rank's own x) run as part 1."""
+        check(rsp.rsp_spmat_set_local_cols(self._mat, int(ncols_local)), "rsp_spmat_set_local_cols")
+        one, zero = _scalar(1.0, self.dtype), _scalar(0.0, self.dtype)
+        check(rsp.rsp_spmv_preprocess(self.handle.ptr, _lib.OP_N, C.byref(one), self._mat, None,
+                                      C.byref(zero), None, _DT[self.dtype], _ptr(self.buffer)),
+              "rsp_spmv_preprocess")
+
+    def spmv_part(self, x: torch.Tensor, y: torch.Tensor, part: int, alpha: float = 1.0) -> torch.Tensor:
+        """Part 1 (interior tiles) or 2 (the rest + fixup) of y = alpha*A*x (rsp_spmv_part)."""
+        if x.dtype != self.dtype or x.numel() < self.n:
+            raise ValueError("x has the wrong dtype or length")
+        a, b = _scalar(alpha, self.dtype), _scalar(0.0, self.dtype)
+        check(rsp.rsp_spmv_part(self.handle.ptr, C.byref(a), self._mat, _ptr(x), C.byref(b), _ptr(y),
+                                _DT[self.dtype], _ptr(self.buffer), int(part)), "rsp_spmv_part")
+        return y
+
     def close(self) -> None:
         if self._h:
             rsp.rsp_destroy(self._h)
@@ -125,6 +143,24 @@ class SpMat:
                            _ptr(y), _DT[self.dtype], _ptr(self.buffer)), "rsp_spmv")
         return y
 
+    def set_local_cols(self, ncols_local: int) -> None:
+        """Split the schedule for halo overlap (rsp_spmat_set_local_cols): tiles
+        reading columns < ncols_local only (the rank's own x) run as part 1."""
+        check(rsp.rsp_spmat_set_local_cols(self._mat, int(ncols_local)), "rsp_spmat_set_local_cols")
+        one, zero = _scalar(1.0, self.dtype), _scalar(0.0, self.dtype)
+        check(rsp.rsp_spmv_preprocess(self.handle.ptr, _lib.OP_N, C.byref(one), self._mat, None,
+                                      C.byref(zero), None, _DT[self.dtype], _ptr(self.buffer)),
+              "rsp_spmv_preprocess")
+
+    def spmv_part(self, x: torch.Tensor, y: torch.Tensor, part: int, alpha: float = 1.0) -> torch.Tensor:
+        """Part 1 (interior tiles) or 2 (the rest + fixup) of y = alpha*A*x (rsp_spmv_part)."""
+        if x.dtype != self.dtype or x.numel() < self.n:
+            raise ValueError("x has the wrong dtype or length")
+        a, b = _scalar(alpha, self.dtype), _scalar(0.0, self.dtype)
+        check(rsp.rsp_spmv_part(self.handle.ptr, C.byref(a), self._mat, _ptr(x), C.byref(b), _ptr(y),
+                                _DT[self.dtype], _ptr(self.buffer), int(part)), "rsp_spmv_part")
+        return y
+
     def close(self) -> None:
         if self._mat:
             rsp.rsp_destroy_spmat(self._mat)
@@ -188,6 +224,24 @@ class Ilu0:
         a = _scalar(alpha, values.dtype)
         check(rsp.rsp_trsv_upper(self.handle.ptr, C.byref(a), self._info, _DT[values.dtype],
                                  _ptr(values), _ptr(x), _ptr(y)), "rsp_trsv_upper")
+        return y
+
+    def set_local_cols(self, ncols_local: int) -> None:
+        """Split the schedule for halo overlap (rsp_spmat_set_local_cols): tiles
+        reading columns < ncols_local only (the rank's own x) run as part 1."""
+        check(rsp.rsp_spmat_set_local_cols(self._mat, int(ncols_local)), "rsp_spmat_set_local_cols")
+        one, zero = _scalar(1.0, self.dtype), _scalar(0.0, self.dtype)
+        check(rsp.rsp_spmv_preprocess(self.handle.ptr, _lib.OP_N, C.byref(one), self._mat, None,
+                                      C.byref(zero), None, _DT[self.dtype], _ptr(self.buffer)),
+              "rsp_spmv_preprocess")
+
+    def spmv_part(self, x: torch.Tensor, y: torch.Tensor, part: int, alpha: float = 1.0) -> torch.Tensor:
+        """Part 1 (interior tiles) or 2 (the rest + fixup) of y = alpha*A*x (rsp_spmv_part)."""
+        if x.dtype != self.dtype or x.numel() < self.n:
+            raise ValueError("x has the wrong dtype or length")
+        a, b = _scalar(alpha, self.dtype), _scalar(0.0, self.dtype)
+        check(rsp.rsp_spmv_part(self.handle.ptr, C.byref(a), self._mat, _ptr(x), C.byref(b), _ptr(y),
+                                _DT[self.dtype], _ptr(self.buffer), int(part)), "rsp_spmv_part")
         return y
 
     def close(self) -> None:

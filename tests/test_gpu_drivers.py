@@ -133,6 +133,17 @@ def test_halo_partitioned_spmv_single_gpu(P):
         scatter(h, idx, x_ext, back)                   # unpack: x_ext -> global slots
         assert np.array_equal(back.cpu().numpy()[cols], x[cols])
         assert np.array_equal(x_ext.cpu().numpy(), x[cols])
-        ys.append(SpMat(h, *upload_csr(rp, hs.colidx_ext, va), hs.n_ext).spmv(x_ext).cpu().numpy())
+        M = SpMat(h, *upload_csr(rp, hs.colidx_ext, va), hs.n_ext)
+        ys.append(M.spmv(x_ext).cpu().numpy())
+        # overlap split: interior tiles (own columns) with a poisoned halo, then
+        # the boundary tiles after the halo is restored — same bits
+        M.set_local_cols(hs.m_local)
+        y2 = torch.full((max(r1 - r0, 1),), float("nan"), dtype=torch.float64, device="cuda")
+        saved = x_ext[hs.m_local:].clone()
+        x_ext[hs.m_local:] = float("nan")
+        M.spmv_part(x_ext, y2, 1)
+        x_ext[hs.m_local:] = saved
+        M.spmv_part(x_ext, y2, 2)
+        assert np.array_equal(y2.cpu().numpy()[: r1 - r0], ys[-1])
     assert np.array_equal(np.concatenate(ys), y_full)
     h.close()
