@@ -64,6 +64,7 @@ typedef enum {
 /* Load options beyond the reference's (outputBase, transpose). */
 #define RSP_MM_FULL_SYMMETRIC 0x1 /* keep the mirrored entries in the CSR */
 #define RSP_MM_QUIET 0x2          /* do not print the reference's stderr messages */
+#define RSP_MM_SERIAL 0x4         /* parse entries on one thread (default: OpenMP for large files) */
 
 /* Reference-compatible loader: loadMatrixMarket.cpp:47-253. Returns 1 on
  * success and 0 on failure; prints the reference's messages on stderr and

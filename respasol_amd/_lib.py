@@ -52,6 +52,7 @@ OP_T = 1
 
 MM_FULL_SYMMETRIC = 0x1
 MM_QUIET = 0x2
+MM_SERIAL = 0x4
 SURR_FTZ_STRESS = 0x1
 
 

@@ -75,10 +75,14 @@ def _from_struct(s: CSRStruct, base: int) -> CsrMatrix:
 
 
 def load_matrix_market(path: str, output_base: int = 0, transpose: int = 0,
-                       full_symmetric: bool = False, quiet: bool = True) -> CsrMatrix:
-    """loadMatrixMarket (loadMatrixMarket.cpp:47-253); raises LoadError."""
+                       full_symmetric: bool = False, quiet: bool = True,
+                       serial: bool = False) -> CsrMatrix:
+    """loadMatrixMarket (loadMatrixMarket.cpp:47-253); raises LoadError.
+    Large files parse their entries on all OpenMP threads (same result);
+    serial=True forces the one-thread parse."""
     s = CSRStruct()
-    flags = (_lib.MM_FULL_SYMMETRIC if full_symmetric else 0) | (_lib.MM_QUIET if quiet else 0)
+    flags = ((_lib.MM_FULL_SYMMETRIC if full_symmetric else 0) | (_lib.MM_QUIET if quiet else 0)
+             | (_lib.MM_SERIAL if serial else 0))
     st = host.rsp_mm_load(path.encode(), C.byref(s), output_base, transpose, flags)
     if st != 0:
         raise LoadError(st, path)
@@ -86,10 +90,11 @@ def load_matrix_market(path: str, output_base: int = 0, transpose: int = 0,
 
 
 def load_matrix_market_text(text: str | bytes, output_base: int = 0, transpose: int = 0,
-                            full_symmetric: bool = False) -> CsrMatrix:
+                            full_symmetric: bool = False, serial: bool = False) -> CsrMatrix:
     buf = text.encode() if isinstance(text, str) else bytes(text)
     s = CSRStruct()
-    flags = (_lib.MM_FULL_SYMMETRIC if full_symmetric else 0) | _lib.MM_QUIET
+    flags = ((_lib.MM_FULL_SYMMETRIC if full_symmetric else 0) | _lib.MM_QUIET
+             | (_lib.MM_SERIAL if serial else 0))
     st = host.rsp_mm_load_buffer(buf, len(buf), C.byref(s), output_base, transpose, flags)
     if st != 0:
         raise LoadError(st, "<buffer>")

@@ -38,6 +38,10 @@
 
 #include "rsp_host.h"
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
 #define MM_LINE_MAX 1025 /* MM_MAX_LINE_LENGTH, mm_io.h:12 */
 #define MM_TOKEN_MAX 64  /* MM_MAX_TOKEN_LENGTH, mm_io.h:14 */
 
@@ -300,13 +304,107 @@ static void coo_tmp_free(coo_tmp *t) {
     t->val = NULL;
 }
 
+/* Parallel entry parse (the reference's fscanf loop is the
+ * sweep's bottleneck). The entry text is cut at newlines into one piece per
+ * thread; each piece is parsed with the same token rules (parse_entry). It is
+ * accepted only if every piece parses to its end — then no entry straddles a
+ * cut (a cut at a newline never splits a token, and a piece ending inside an
+ * entry would fail), so the concatenated entries are exactly the sequential
+ * parse's. Any failure (malformed text, a cut inside an entry) returns -1 and
+ * the caller parses sequentially, which reproduces the reference's error
+ * behaviour. Returns the entry count; the arrays are malloc'ed into px, py, pv. */
+#define MM_PAR_MIN_BYTES (8u << 20)
+
+static long parse_entries_parallel(const char *p, const char *end, const mm_code *k, int **px,
+                                   int **py, double **pv) {
+    int nt = 1;
+#ifdef _OPENMP
+    nt = omp_get_max_threads();
+#endif
+    if (nt < 2 || (size_t)(end - p) < MM_PAR_MIN_BYTES) return -1;
+    if (nt > 256) nt = 256;
+    const char *cut[257];
+    cut[0] = p;
+    for (int t = 1; t < nt; t++) {
+        const char *q = p + (size_t)(end - p) * (size_t)t / (size_t)nt;
+        if (q < cut[t - 1]) q = cut[t - 1];
+        while (q < end && *q != '\n') q++;
+        cut[t] = q < end ? q + 1 : end;
+    }
+    cut[nt] = end;
+    long cnt[256];
+    int *bx[256];
+    int *by[256];
+    double *bv[256];
+    int ok = 1;
+#pragma omp parallel for num_threads(nt) schedule(static, 1) reduction(&& : ok)
+    for (int t = 0; t < nt; t++) {
+        cursor c = {cut[t], cut[t + 1]};
+        size_t cap = (size_t)(cut[t + 1] - cut[t]) / 4 + 16; /* an entry takes >= 4 bytes */
+        bx[t] = (int *)malloc(cap * sizeof(int));
+        by[t] = (int *)malloc(cap * sizeof(int));
+        bv[t] = (double *)malloc(cap * sizeof(double));
+        cnt[t] = 0;
+        if (!bx[t] || !by[t] || !bv[t]) {
+            ok = 0;
+            continue;
+        }
+        int x, y;
+        double v;
+        while ((size_t)cnt[t] < cap && parse_entry(&c, k, &x, &y, &v)) {
+            bx[t][cnt[t]] = x;
+            by[t][cnt[t]] = y;
+            bv[t][cnt[t]] = v;
+            cnt[t]++;
+        }
+        cur_skip_ws(&c);
+        if (c.p < c.end) ok = 0; /* stopped early: malformed or a straddling entry */
+    }
+    long total = 0;
+    for (int t = 0; t < nt; t++) total += cnt[t];
+    int *X = NULL, *Y = NULL;
+    double *V = NULL;
+    if (ok) {
+        X = (int *)malloc((total ? total : 1) * sizeof(int));
+        Y = (int *)malloc((total ? total : 1) * sizeof(int));
+        V = (double *)malloc((total ? total : 1) * sizeof(double));
+        ok = X && Y && V;
+    }
+    if (ok) {
+        long off[257];
+        off[0] = 0;
+        for (int t = 0; t < nt; t++) off[t + 1] = off[t] + cnt[t];
+#pragma omp parallel for num_threads(nt) schedule(static, 1)
+        for (int t = 0; t < nt; t++) {
+            memcpy(X + off[t], bx[t], (size_t)cnt[t] * sizeof(int));
+            memcpy(Y + off[t], by[t], (size_t)cnt[t] * sizeof(int));
+            memcpy(V + off[t], bv[t], (size_t)cnt[t] * sizeof(double));
+        }
+    }
+    for (int t = 0; t < nt; t++) {
+        free(bx[t]);
+        free(by[t]);
+        free(bv[t]);
+    }
+    if (!ok) {
+        free(X);
+        free(Y);
+        free(V);
+        return -1;
+    }
+    *px = X;
+    *py = Y;
+    *pv = V;
+    return total;
+}
+
 static const char *status_msg_open = "Failed to open file %s\n";
 
 /* Banner + size + entries + base fix-up + nnz check, shared by the CSR and
  * COO entry points. Entries are stored in file order with room for the
  * symmetric mirror (2*nnz), exactly like loadMatrixMarket.cpp:79-141. */
 static int read_coo(const char *buf, size_t len, int transpose, int quiet, const char *fname,
-                    coo_tmp *t) {
+                    coo_tmp *t, int serial) {
     cursor c = {buf, buf + len};
     mm_code code;
     memset(t, 0, sizeof(*t));
@@ -351,7 +449,22 @@ static int read_coo(const char *buf, size_t len, int transpose, int quiet, const
     long lines = 0;
     int x, y;
     double v;
-    while (parse_entry(&c, &code, &x, &y, &v)) {
+    /* entries: parsed in parallel when the text is large (same result), else
+     * one by one; the per-entry checks below run in file order either way */
+    int *px = NULL, *py = NULL;
+    double *pv = NULL;
+    const long npar = serial ? -1 : parse_entries_parallel(c.p, c.end, &code, &px, &py, &pv);
+    long ip = 0;
+    for (;;) {
+        if (npar >= 0) {
+            if (ip >= npar) break;
+            x = px[ip];
+            y = py[ip];
+            v = pv[ip];
+            ip++;
+        } else if (!parse_entry(&c, &code, &x, &y, &v)) {
+            break;
+        }
         if (transpose) {
             int s = x;
             x = y;
@@ -360,6 +473,9 @@ static int read_coo(const char *buf, size_t len, int transpose, int quiet, const
         if (x > m || y > n || x < 0 || y < 0) {
             if (!quiet) fprintf(stderr, "Error: (%d %d) coordinate is out of range.\n", x, y);
             coo_tmp_free(t);
+            free(px);
+            free(py);
+            free(pv);
             return RSP_MM_OUT_OF_RANGE;
         }
         if ((size_t)lines >= cap) { /* more entries than the header: the
@@ -373,6 +489,9 @@ static int read_coo(const char *buf, size_t len, int transpose, int quiet, const
         if (x == 0 || y == 0) base = 0;
         lines++;
     }
+    free(px);
+    free(py);
+    free(pv);
     if (lines != nz) {
         if (!quiet)
             fprintf(stderr,
@@ -501,7 +620,7 @@ int rsp_mm_load_buffer(const char *buf, size_t len, CSR *A, int outputBase, int 
                        int flags) {
     coo_tmp t;
     memset(A, 0, sizeof(*A));
-    int st = read_coo(buf, len, transpose, flags & RSP_MM_QUIET, NULL, &t);
+    int st = read_coo(buf, len, transpose, flags & RSP_MM_QUIET, NULL, &t, flags & RSP_MM_SERIAL);
     if (st != RSP_MM_OK) return st;
     st = build_csr(&t, A, outputBase, flags);
     coo_tmp_free(&t);
@@ -542,7 +661,7 @@ int rsp_mm_load(const char *file, CSR *A, int outputBase, int transpose, int fla
         return RSP_MM_OPEN_FAILED;
     }
     coo_tmp t;
-    int st = read_coo(buf, len, transpose, flags & RSP_MM_QUIET, file, &t);
+    int st = read_coo(buf, len, transpose, flags & RSP_MM_QUIET, file, &t, flags & RSP_MM_SERIAL);
     free(buf);
     if (st != RSP_MM_OK) return st;
     st = build_csr(&t, A, outputBase, flags);
@@ -565,7 +684,7 @@ int loadCooMatrix(const char *file, COO *matrix, int outputbase, int transpose) 
         exit(-1);
     }
     coo_tmp t;
-    int st = read_coo(buf, len, transpose, 0, file, &t);
+    int st = read_coo(buf, len, transpose, 0, file, &t, 0);
     free(buf);
     if (st != RSP_MM_OK) return 0;
     int count = t.lines;

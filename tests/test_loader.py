@@ -133,3 +133,66 @@ def test_binary_cache_roundtrip(tmp_path):
     assert [t.rowptr[i] for i in range(t.m + 1)] == [s.rowptr[i] for i in range(s.m + 1)]
     host.rsp_csr_free(C.byref(s))
     host.rsp_csr_free(C.byref(t))
+
+
+# --------------------------------------------------- parallel entry parse
+
+def _big_text(n_rows=60000, per_row=30, sym=False, seed=7, pattern=False, split_lines=False):
+    """A > 8 MB coordinate file (the parallel-parse threshold)."""
+    rng = np.random.default_rng(seed)
+    rows = np.repeat(np.arange(1, n_rows + 1), per_row)
+    cols = rng.integers(1, n_rows + 1, rows.size)
+    if sym:
+        lo = np.minimum(rows, cols)
+        hi = np.maximum(rows, cols)
+        rows, cols = hi, lo
+    vals = rng.standard_normal(rows.size) * 10.0 ** rng.integers(-30, 30, rows.size)
+    field = "pattern" if pattern else "real"
+    head = f"%%MatrixMarket matrix coordinate {field} {'symmetric' if sym else 'general'}\n% c\n"
+    head += f"{n_rows} {n_rows} {rows.size}\n"
+    sep = "\n" if split_lines else " "
+    if pattern:
+        body = "".join(f"{r} {c}\n" for r, c in zip(rows.tolist(), cols.tolist()))
+    else:
+        body = "".join(f"{r} {c}{sep}{v!r}\n" for r, c, v in zip(rows.tolist(), cols.tolist(), vals.tolist()))
+    return head + body
+
+
+def _same_csr(a, b):
+    return (a.m == b.m and a.n == b.n and a.nnz == b.nnz and np.array_equal(a.rowptr, b.rowptr)
+            and np.array_equal(a.colidx, b.colidx) and np.array_equal(a.values.view(np.uint64), b.values.view(np.uint64)))
+
+
+@pytest.mark.parametrize("sym,pattern,split", [(False, False, False), (True, False, False),
+                                               (False, True, False), (False, False, True)])
+def test_parallel_parse_identical(sym, pattern, split):
+    """Large files: the OpenMP entry parse gives the same CSR as the serial
+    parse (incl. entries split over lines, where it falls back)."""
+    text = _big_text(sym=sym, pattern=pattern, split_lines=split)
+    assert len(text) > (8 << 20)
+    a = csr.load_matrix_market_text(text)
+    b = csr.load_matrix_market_text(text, serial=True)
+    assert _same_csr(a, b)
+
+
+@pytest.mark.parametrize("bad", ["garbage", "range", "extra"])
+def test_parallel_parse_errors_identical(bad):
+    """Malformed / out-of-range / surplus entries: same status as the serial parse."""
+    text = _big_text()
+    lines = text.split("\n")
+    k = len(lines) // 2
+    if bad == "garbage":
+        lines[k] = "12 x7 1.0"
+    elif bad == "range":
+        lines[k] = "999999999 1 1.0"
+    else:
+        lines.insert(k, "1 1 1.0")
+    text = "\n".join(lines)
+    errs = []
+    for serial in (False, True):
+        try:
+            csr.load_matrix_market_text(text, serial=serial)
+            errs.append(None)
+        except csr.LoadError as e:
+            errs.append(e.status)
+    assert errs[0] == errs[1] and errs[0] is not None
