@@ -279,9 +279,8 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, T alpha, int off, 
 // run, slot = run index mod kYWin) or from the staged copy, writes y to
 // global memory and to its window slot, and an LDS-only barrier separates
 // the levels. Same operation order as trsv_level.
-template <typename T, int KIND, int B>
-__global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, int c0, int c1,
-                                                          int base) {
+template <typename T, int KIND, int B, int NTH>
+__global__ __launch_bounds__(NTH) void trsv_thin(TrsvArgs a, T alpha, int c0, int c1, int base) {
     __shared__ T ywin[rsp::kYWin];
     __shared__ T lval[rsp::kChunkTerms], lyv[rsp::kChunkTerms];
     __shared__ int lsrc[rsp::kChunkTerms];
@@ -297,19 +296,19 @@ __global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, i
         const int x0 = ptr[ch.l0], x1 = ptr[ch.l1];
         const int k0 = a.plan.tasks[x0].t0, k1 = a.plan.tasks[x1 - 1].t1;
         __syncthreads();  // the previous chunk's y stores are visible, LDS is free
-        for (int r = tid; r < x1 - x0; r += kThinThreads) {
+        for (int r = tid; r < x1 - x0; r += NTH) {
             const rsp::RowTask t = a.plan.tasks[x0 + r];
             ltask[r] = t;
             lx[r] = alpha * x[t.i];
             ldg[r] = (KIND == 2 && t.d >= 0) ? vals[t.d] : T(0);
         }
-        for (int k = tid; k < k1 - k0; k += kThinThreads) {
+        for (int k = tid; k < k1 - k0; k += NTH) {
             const int sc = a.plan.src[k0 + k];
             lsrc[k] = sc;
             lval[k] = vals[a.plan.tpos[k0 + k]];
             lyv[k] = sc >= 0 ? y[sc] : T(0);
         }
-        for (int q = tid; q <= ch.l1 - ch.l0; q += kThinThreads) {
+        for (int q = tid; q <= ch.l1 - ch.l0; q += NTH) {
             lptr[q] = ptr[ch.l0 + q];
             if (q < ch.l1 - ch.l0) lns[q] = a.plan.nshort[ch.l0 + q];
         }
@@ -322,14 +321,14 @@ __global__ __launch_bounds__(kThinThreads) void trsv_thin(TrsvArgs a, T alpha, i
                 const int sc = lsrc[k];
                 return sc < 0 ? ywin[-sc - 1] : lyv[k];
             };
-            if (tid < ns) {
-                const rsp::RowTask t = ltask[off + tid];
-                T s = fma_chain<T, B>(lx[off + tid], t.t0 - k0, t.t1 - k0, vat, yat);
-                if constexpr (KIND == 2) s = s / ldg[off + tid];
+            for (int r = tid; r < ns; r += NTH) {
+                const rsp::RowTask t = ltask[off + r];
+                T s = fma_chain<T, B>(lx[off + r], t.t0 - k0, t.t1 - k0, vat, yat);
+                if constexpr (KIND == 2) s = s / ldg[off + r];
                 y[t.i] = s;
-                ywin[(lp + tid - base) & (rsp::kYWin - 1)] = s;
+                ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
             }
-            for (int r = ns + (tid >> 6); r < cnt; r += kThinThreads / 64) {  // long rows: a wave each
+            for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
                 const rsp::RowTask t = ltask[off + r];
                 T s = wave_chain<T>(lx[off + r], t.t0 - k0, t.t1 - k0, tid & 63, vat, yat);
                 if constexpr (KIND == 2) s = s / ldg[off + r];
@@ -371,8 +370,16 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
-            hipLaunchKernelGGL((trsv_thin<T, KIND, B>), dim3(1), dim3(kThinThreads), 0, s, a,
-                               alpha, sg.c0, sg.c1, P.ptr_host[sg.lb]);
+            const int base = P.ptr_host[sg.lb];
+            if (sg.nth <= 64)
+                hipLaunchKernelGGL((trsv_thin<T, KIND, B, 64>), dim3(1), dim3(64), 0, s, a, alpha,
+                                   sg.c0, sg.c1, base);
+            else if (sg.nth <= 256)
+                hipLaunchKernelGGL((trsv_thin<T, KIND, B, 256>), dim3(1), dim3(256), 0, s, a, alpha,
+                                   sg.c0, sg.c1, base);
+            else
+                hipLaunchKernelGGL((trsv_thin<T, KIND, B, kThinThreads>), dim3(1), dim3(kThinThreads),
+                                   0, s, a, alpha, sg.c0, sg.c1, base);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

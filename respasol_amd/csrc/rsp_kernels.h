@@ -76,6 +76,7 @@ struct SpmvArgs {
 // per level.
 struct LevelSeg {
     int lb, le, thin, c0, c1;
+    int nth;  // thin solve runs: workgroup size (64 / 256 / 1024, >= the run's widest level)
 };
 // Solve task of one row, stored in level order: the fma chain runs over the
 // flat terms [t0, t1) (term k: matrix value vals[tpos[k]] times the y given
