@@ -163,3 +163,30 @@ def test_schedule_variants(handle, monkeypatch, thin_solve, thin_factor, name, s
     x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
     compare(A, torch.float64, handle, x=x)
     compare(A, torch.float32, handle, x=x, true_lu=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_tiny_and_diagonal(handle, dtype):
+    """1x1, a pure diagonal (one level, no terms) and a 2x2 lower-only chain."""
+    for rp, ci, va in (([0, 1], [0], [4.0]),
+                       (list(range(6)), list(range(5)), [1.0, 2.0, 3.0, 4.0, 5.0]),
+                       ([0, 1, 3], [0, 0, 1], [2.0, -1.0, 3.0])):
+        n = len(rp) - 1
+        A = csr.CsrMatrix(0, n, n, len(ci), np.array(rp, np.int32), np.array(ci, np.int32),
+                          np.array(va, np.float64))
+        compare(A, dtype, handle, x=np.arange(1, n + 1, dtype=np.float64))
+        compare(A, dtype, handle, x=np.arange(1, n + 1, dtype=np.float64), true_lu=True)
+
+
+def test_empty_matrix(handle):
+    """n = 0: analysis, factor and solves are no-ops that succeed."""
+    A = csr.CsrMatrix(0, 0, 0, 0, np.zeros(1, np.int32), np.zeros(0, np.int32), np.zeros(0))
+    rp = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ci = torch.zeros(1, dtype=torch.int32, device="cuda")
+    va = torch.zeros(1, dtype=torch.float64, device="cuda")
+    il = Ilu0(handle, rp, ci, nnz=0)
+    il.analysis()
+    assert il.zero_pivot() == -1
+    il.factor(va)
+    assert il.zero_pivot() == -1
+    assert A.n == 0
