@@ -34,7 +34,10 @@ constexpr int kSpmvThreads = 256;
 #define RSP_SPMV_ITER 4  // overridable for tile-geometry experiments (scripts/spmv_probe.py)
 #endif
 constexpr int kSpmvIter = RSP_SPMV_ITER;  // vectors per thread per tile
-constexpr int kSpmvMaxRows = 512;   // rows per tile (row offsets staged in LDS)
+#ifndef RSP_SPMV_MAXROWS
+#define RSP_SPMV_MAXROWS 512  // overridable for tile-geometry experiments (scripts/spmv_probe.py)
+#endif
+constexpr int kSpmvMaxRows = RSP_SPMV_MAXROWS;  // rows per tile (row offsets staged in LDS)
 constexpr int kSpmvLongRow = 256;   // rows longer than this get the 256-thread tree
 constexpr int kSpmvWholeRow = -2147483647 - 1;  // SpmvBlock::r1 marker (INT_MIN)
 template <typename T>

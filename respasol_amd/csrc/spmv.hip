@@ -45,6 +45,12 @@
 #ifndef RSP_PROBE_Y
 #define RSP_PROBE_Y 0  // with RSP_PROBE 4: also store y (one element per row)
 #endif
+#ifndef RSP_PROBE_NOSWIZZLE
+#define RSP_PROBE_NOSWIZZLE 0  // plain blockIdx -> tile order (A/B)
+#endif
+#ifndef RSP_PROBE_PRIO
+#define RSP_PROBE_PRIO 0  // s_setprio at kernel entry (A/B)
+#endif
 #ifndef RSP_NT_Y
 #define RSP_NT_Y 0  // non-temporal y stores (A/B)
 #endif
@@ -125,6 +131,9 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
     // keep the scheduler from splitting the load and gather bursts: two
     // memory round trips per tile, not one per vector
     __builtin_amdgcn_sched_barrier(0);
+#if RSP_PROBE_PRIO
+    __builtin_amdgcn_s_setprio(0);  // loads issued: back to normal priority
+#endif
     T xv[IT][VW];
 #pragma unroll
     for (int it = 0; it < IT; ++it)
@@ -339,7 +348,15 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
-    spmv_tile<T, NT, BETA>(blocks[xcd_swizzle(blockIdx.x, nblocks)], rowptr, colidx, vals, x, y,
+#if RSP_PROBE_NOSWIZZLE
+    const int b = blockIdx.x;
+#else
+    const int b = xcd_swizzle(blockIdx.x, nblocks);
+#endif
+#if RSP_PROBE_PRIO
+    __builtin_amdgcn_s_setprio(RSP_PROBE_PRIO);
+#endif
+    spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, vals, x, y,
                            partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds);
 }
 

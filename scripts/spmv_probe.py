@@ -32,6 +32,10 @@ PROBES = {
     "loads_y_lds": "-DRSP_PROBE=4 -DRSP_PROBE_Y=1 -DRSP_PROBE_LDS=1",
     "loads_nty": "-DRSP_PROBE=4 -DRSP_PROBE_Y=1 -DRSP_NT_Y=1",
     "nty": "-DRSP_NT_Y=1",
+    "noswz": "-DRSP_PROBE_NOSWIZZLE=1",
+    "rows256": "-DRSP_SPMV_MAXROWS=256",
+    "rows1024": "-DRSP_SPMV_MAXROWS=1024",
+    "prio2": "-DRSP_PROBE_PRIO=2",
 }
 
 
@@ -111,6 +115,7 @@ def main():
     ap.add_argument("--workload", default="big")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--stream-ref", action="store_true")
+    ap.add_argument("--rounds", type=int, default=2)
     args = ap.parse_args()
     names = args.probes.split(",")
     if args.build:
@@ -122,7 +127,7 @@ def main():
     if args.child:
         child(args.steps, args.workload)
         return
-    for rnd in range(2):  # two rounds, interleaved, to see the box noise
+    for rnd in range(args.rounds):  # interleaved rounds, to see the box noise
         for n in names:
             env = dict(os.environ, RSP_PROBE_LIB=lib_path(n))
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--steps",
