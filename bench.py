@@ -8,14 +8,19 @@
 Workload (default "big"): one step = one fp64 y = A x over EACH of the 15
 "big" SuiteSparse matrices (BASELINE config 4; seeded surrogates of the same
 m / stored nnz / structure, since no .mtx data exists offline). With N > 1
-every matrix is row-partitioned (nnz-balanced) across the ranks and each
-SpMV is preceded by the RCCL all-gather of the x slices over xGMI (config 5
-applied to the whole set); total work is fixed => "scaling": "strong".
-Cycling through 3.4 GB of matrices per step also keeps the 256 MB Infinity
-Cache from serving any matrix twice, so the rate is an HBM rate.
+every matrix is row-partitioned (nnz-balanced) across the ranks; one bucketed
+RCCL all_to_all_single per step moves each rank's halo of x over xGMI while
+the interior tiles (own columns only) run, then the boundary tiles finish
+(config 5 applied to the whole set; --no-overlap / --exchange allgather are
+the simpler variants); total work is fixed => "scaling": "strong". A
+step's SpMVs go out as one batched launch (rsp_spmv_batch; --no-batch: one
+launch per matrix, also timed and reported as "per_matrix_calls"). Cycling
+through 3.4 GB of matrices per step also keeps the 256 MB Infinity Cache
+from serving any matrix twice, so the rate is an HBM rate.
 
 value = total GFLOP of all ranks / max-over-ranks wall time of the K steps.
-roofline = the dominant kernel (spmv_tiles, every launch of the step) timed
+roofline = the dominant kernel (spmv_tiles_batch: the step's one launch over
+all 15 matrices; spmv_tiles per matrix with --no-batch) timed
 with one HIP event pair on the stream it runs on around the K steps (N = 1:
 the timed region itself; N > 1: a kernel-only repeat of the K steps):
 algorithmic bytes / average launch duration against 8 TB/s. cpu_baseline = the oracle's OpenMP CSR SpMV (the reference's
@@ -39,7 +44,7 @@ sys.path.insert(0, ROOT)
 
 from respasol_amd import csr  # noqa: E402
 from respasol_amd.dist import HaloExchange, HaloSlice, RowPartitionedSpmv, remap_columns  # noqa: E402
-from respasol_amd.sparse import Handle, SpMat, upload_csr  # noqa: E402
+from respasol_amd.sparse import Handle, SpMat, SpmvBatch, upload_csr  # noqa: E402
 
 METRIC = "CSR SpMV GFLOP/s + achieved HBM GB/s (fp64 vs fp32), SuiteSparse set, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -144,8 +149,9 @@ def cpu_baseline(slices, seconds):
                       f"({el:.1f} s), OpenMP row-parallel CSR, x=dlarnv(1,{{0,0,0,1}})"}
 
 
-def pmc_traffic(workload):
-    """HBM bytes per dominant-kernel launch from a committed rocprofv3 --pmc
+def pmc_traffic(workload, batched):
+    """HBM bytes per dominant-kernel launch (the batched launch, or one
+    per-matrix launch with --no-batch) from a committed rocprofv3 --pmc
     summary (profiles/*pmc*.json written by scripts/pmc_summary.py), or None."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -153,8 +159,11 @@ def pmc_traffic(workload):
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload and "hbm_bytes_per_launch" in d:
-            best = d["hbm_bytes_per_launch"]
+        if d.get("workload") != workload:
+            continue
+        part = d.get("batch") if batched else d.get("per_matrix", d)
+        if part and "hbm_bytes_per_launch" in part:
+            best = part["hbm_bytes_per_launch"]
     return best
 
 
@@ -174,6 +183,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="halo mode: finish the exchange before any SpMV instead of running the "
                          "interior tiles under it")
+    ap.add_argument("--no-batch", action="store_true",
+                    help="one rsp_spmv launch per matrix instead of one batched launch per step")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
@@ -213,32 +224,53 @@ def main():
 
     stream = torch.cuda.current_stream()
 
-    first_of = {g[0]: ex for g, ex in exchanges64}  # halo: exchange before a group's first SpMV
+    def spmv_all(part):
+        for s in slices:
+            if part:
+                s.mat64.spmv_part(s.x64(), s.y64, part)
+            else:
+                s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
+
+    # part -> one batched launch over every matrix (rsp_spmv_batch): a step's
+    # 15 SpMVs cost one kernel ramp and drain instead of 15 (--no-batch: one
+    # rsp_spmv per matrix)
+    batches = {}
+    if not args.no_batch:
+        for part in ((0, 1, 2) if overlap else (0,)):
+            batches[part] = SpmvBatch(handle, [s.mat64 for s in slices], [s.x64() for s in slices],
+                                      [s.y64 for s in slices], part)
+
+    def run(part):
+        b = batches.get(part)
+        if b is not None:
+            b.run()
+        else:
+            spmv_all(part)
 
     def step(exchange=True, events=None):
+        if events is not None:  # instrumented pass: kernels only, one event pair per matrix
+            for i, s in enumerate(slices):
+                events[i][0].record(stream)
+                s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
+                events[i][1].record(stream)
+            return
         if exchange and overlap:
             # halo overlap: start every exchange, interior tiles of every matrix
             # (own columns only), join the exchanges, then the boundary tiles
             for _, ex in exchanges64:
                 ex.start()
-            for s in slices:
-                s.mat64.spmv_part(s.x64(), s.y64, 1)
+            run(1)
             for _, ex in exchanges64:
                 ex.finish()
-            for s in slices:
-                s.mat64.spmv_part(s.x64(), s.y64, 2)
+            run(2)
             return
-        for i, s in enumerate(slices):
-            if exchange:
+        if exchange and world > 1:  # every matrix's x is independent: exchange all, then compute
+            for s in slices:
                 if s.mode == "allgather":
                     s.part64.exchange()
-                elif i in first_of:
-                    first_of[i].exchange()
-            if events is not None:
-                events[i][0].record(stream)
-            s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
-            if events is not None:
-                events[i][1].record(stream)
+            for _, ex in exchanges64:
+                ex.exchange()
+        run(0)
 
     for _ in range(args.warmup):
         step()
@@ -270,7 +302,8 @@ def main():
     # dominant kernel, this rank: algorithmic bytes / average launch duration.
     # N = 1: the timed region is nothing but back-to-back launches of it; N > 1:
     # the same K steps again without the exchange (kernel-only), same stream.
-    launches = args.steps * len(slices)
+    per_step = -(-len(slices) // 16) if batches else len(slices)  # 16 matrices per batch launch
+    launches = args.steps * per_step
     if world == 1:
         kern_ms = e_start.elapsed_time(e_end)
     else:
@@ -283,6 +316,19 @@ def main():
         kern_ms = k0_.elapsed_time(k1_)
     bytes64 = sum(s.bytes_local(8) for s in slices)
     achieved = bytes64 * args.steps / (kern_ms * 1e-3) / 1e9
+    # the same K steps as one rsp_spmv launch per matrix (kernel-only), for
+    # comparison with the batched launch: what a caller doing one SpMV at a
+    # time sees
+    p0_, p1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    p0_.record(stream)
+    for _ in range(args.steps):
+        spmv_all(0)
+    p1_.record(stream)
+    torch.cuda.synchronize()
+    pm_ms = p0_.elapsed_time(p1_) / args.steps
+    per_matrix_calls = {"ms_per_step_rank0": round(pm_ms, 4),
+                        "gbps_rank0": round(bytes64 / (pm_ms * 1e6), 1),
+                        "frac_rank0": round(bytes64 / (pm_ms * 1e6) / HBM_PEAK_GBS, 4)}
     # informative per-matrix split (one instrumented pass, outside the timing)
     ev = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in slices]
     step(exchange=False, events=ev)
@@ -298,15 +344,23 @@ def main():
     value = flops_step * args.steps / elapsed / 1e9
     hbm_gbs = bytes_step * args.steps / elapsed / 1e9
 
-    # fp32 companion measurement (outside the timed region)
+    # fp32 companion measurement (outside the timed region), launched as the fp64 step
+    b32 = (SpmvBatch(handle, [s.mat32 for s in slices], [s.x32() for s in slices],
+                     [s.y32 for s in slices]) if batches else None)
+
+    def pass32():
+        if b32 is not None:
+            b32.run()
+            return
+        for s in slices:
+            s.mat32.spmv(s.x32(), s.y32[: s.m_local] if s.m_local else s.y32)
+
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for s in slices:
-        s.mat32.spmv(s.x32(), s.y32[: s.m_local] if s.m_local else s.y32)
+    pass32()
     torch.cuda.synchronize()
     e0.record(stream)
     for _ in range(args.fp32_reps):
-        for s in slices:
-            s.mat32.spmv(s.x32(), s.y32[: s.m_local] if s.m_local else s.y32)
+        pass32()
     e1.record(stream)
     torch.cuda.synchronize()
     ms32 = e0.elapsed_time(e1) / args.fp32_reps
@@ -339,7 +393,7 @@ def main():
         cpu = cpu_baseline(slices, args.cpu_seconds)
 
     if rank == 0:
-        traffic = pmc_traffic(args.workload) if world == 1 else None  # PMC run was N = 1
+        traffic = pmc_traffic(args.workload, bool(batches)) if world == 1 else None  # PMC run was N = 1
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -360,6 +414,9 @@ def main():
                 "matrices": len(slices),
                 "nnz_stored_total": int(sum(s.nnz_global for s in slices)),
                 "parallelism": f"row-partition x{world}" if world > 1 else "1 GPU",
+                "launch": "one rsp_spmv per matrix" if args.no_batch else
+                          ("rsp_spmv_batch: interior + boundary launches" if overlap
+                           else "rsp_spmv_batch: one launch per step"),
                 "collective": (("halo all_to_all_single" + ("" if args.no_bucket else
                                  " (one per step, bucketed over the matrices)")
                                  + (", interior tiles overlapped" if overlap else "")
@@ -373,17 +430,19 @@ def main():
             "hbm_gbps": round(hbm_gbs, 1),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "rsp_k::spmv_tiles<double,true,false>",
+                "kernel": ("rsp_k::spmv_tiles_batch<double,true,false,true>" if batches
+                           else "rsp_k::spmv_tiles<double,true,false>"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "avg_launch_us": round(kern_ms / launches * 1e3, 3),
-                "bytes_per_launch_avg": int(bytes64 / len(slices)),
+                "bytes_per_launch_avg": int(bytes64 / per_step),
             },
             "cpu_baseline": cpu,
             "fp32": fp32,
+            "per_matrix_calls": per_matrix_calls,
             "per_matrix_us_rank0": per_matrix,
             "parity_check": "ok" if check_ok else "FAILED",
         }

@@ -62,6 +62,7 @@ typedef enum { RSP_OPERATION_NON_TRANSPOSE = 0, RSP_OPERATION_TRANSPOSE = 1 } rs
 typedef struct rsp_context *rsp_handle_t;       /* cusparseHandle_t       */
 typedef struct rsp_spmat *rsp_spmat_t;          /* cusparseSpMatDescr_t   */
 typedef struct rsp_ilu0_info *rsp_ilu0_info_t;  /* csrilu02Info_t + both csrsv2Info_t */
+typedef struct rsp_spmv_batch *rsp_spmv_batch_t; /* no cuSPARSE counterpart (below) */
 
 /* ---------------------------------------------------------------- handle */
 
@@ -191,6 +192,27 @@ rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local);
 rsp_status_t rsp_spmv_part(rsp_handle_t handle, const void *alpha, rsp_spmat_t mat,
                            const void *d_x, const void *beta, void *d_y,
                            rsp_datatype_t compute_type, void *d_buffer, int part);
+
+/* Batched SpMV: y_j = alpha*A_j*x_j + beta*y_j for `count` independent
+ * matrices of one compute type, as ONE kernel launch (plus one long-row
+ * fixup launch when any A_j has rows longer than a tile) per 16 matrices.
+ * No cuSPARSE counterpart: the reference calls cusparseSpMV once per matrix
+ * (GPU/spmv.cu:179-186); this is the same product per matrix, bit for bit
+ * equal to rsp_spmv / rsp_spmv_part on each, without the per-launch ramp and
+ * drain. `part` selects the schedule part of every matrix as rsp_spmv_part
+ * (0 = whole product). Create records the pointers (x_j, y_j, d_buffers[j]
+ * stay valid until destroy) and copies the matrices' schedules (a matrix not
+ * yet preprocessed into d_buffers[j] is preprocessed); run fails with
+ * INVALID_VALUE if a matrix has been re-planned or given other values
+ * (rsp_csr_set_values) since. Create and destroy
+ * are host-blocking. */
+rsp_status_t rsp_spmv_batch_create(rsp_handle_t handle, int count, const rsp_spmat_t *mats,
+                                   const void *const *d_x, void *const *d_y,
+                                   void *const *d_buffers, rsp_datatype_t compute_type,
+                                   int part, rsp_spmv_batch_t *batch);
+rsp_status_t rsp_spmv_batch_run(rsp_handle_t handle, rsp_spmv_batch_t batch, const void *alpha,
+                                const void *beta);
+rsp_status_t rsp_spmv_batch_destroy(rsp_spmv_batch_t batch);
 
 /* Number of dependency levels found by the analysis (L DAG, L^T DAG). */
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *levels_upper);

@@ -107,6 +107,9 @@ RSP_PROTOS = {
     "rsp_scatter": (i32, [vp, i32, i64, vp, vp, vp]),
     "rsp_spmat_set_local_cols": (i32, [vp, i64]),
     "rsp_spmv_part": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, i32]),
+    "rsp_spmv_batch_create": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, vp]),
+    "rsp_spmv_batch_run": (i32, [vp, vp, vp, vp]),
+    "rsp_spmv_batch_destroy": (i32, [vp]),
 }
 
 HOST_PROTOS = {

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <new>
 #include <vector>
 
@@ -43,6 +44,7 @@ struct rsp_spmat {
     size_t off_long, off_part;  // byte offsets inside the buffer
     int64_t local_cols;         // rsp_spmat_set_local_cols (-1: not split)
     int nint;                   // interior tiles at the front of the schedule
+    unsigned plan_gen;          // bumped by every preprocess (batch staleness check)
 };
 
 struct rsp_ilu0_info {
@@ -193,6 +195,7 @@ rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local) {
 rsp_status_t rsp_csr_set_values(rsp_spmat_t mat, void *d_values, rsp_datatype_t value_type) {
     if (!mat) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    if (d_values != mat->vals) mat->plan_gen++;  // batches hold the old pointer
     mat->vals = d_values;
     if (value_type != mat->type) mat->plan_buffer = nullptr;  // tile size depends on type
     mat->type = value_type;
@@ -421,6 +424,7 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     mat->plan_type = compute_type;
     mat->nblocks = (int)blocks.size();
     mat->nint = nint;
+    mat->plan_gen++;
     mat->nlong = (int)longrows.size();
     mat->nslots = nslots;
     mat->nnz_s = m > 0 ? rp[(size_t)m] : 0;
@@ -494,6 +498,157 @@ rsp_status_t rsp_spmv_part(rsp_handle_t h, const void *alpha, rsp_spmat_t mat, c
     if (part < 0 || part > 2) return RSP_STATUS_INVALID_VALUE;
     return spmv_run(h, RSP_OPERATION_NON_TRANSPOSE, alpha, mat, d_x, beta, d_y, compute_type,
                     d_buffer, part);
+}
+
+/* ------------------------------------------------------- batched SpMV */
+
+struct rsp_spmv_batch {
+    rsp_datatype_t type;
+    int part;
+    std::vector<rsp_spmat_t> mats;
+    std::vector<const void *> buffers;
+    std::vector<unsigned> plan_gen;  // schedules as copied (stale check)
+    std::vector<rsp::SpmvBatchArgs> launches;  // one per kSpmvBatchMax matrices
+    void *d_mem = nullptr;                      // entries, tiles, long rows of every launch
+    ~rsp_spmv_batch() {
+        if (d_mem) (void)hipFree(d_mem);
+    }
+};
+
+rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t *mats,
+                                   const void *const *d_x, void *const *d_y,
+                                   void *const *d_buffers, rsp_datatype_t compute_type,
+                                   int part, rsp_spmv_batch_t *batch) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!batch || count < 0 || (count > 0 && (!mats || !d_x || !d_y || !d_buffers)))
+        return RSP_STATUS_INVALID_VALUE;
+    if (part < 0 || part > 2) return RSP_STATUS_INVALID_VALUE;
+    if (compute_type != RSP_R_64F && compute_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    *batch = nullptr;
+    const double one = 1.0, zero = 0.0;
+    const float onef = 1.0f, zerof = 0.0f;
+    const void *pa = compute_type == RSP_R_64F ? (const void *)&one : (const void *)&onef;
+    const void *pb = compute_type == RSP_R_64F ? (const void *)&zero : (const void *)&zerof;
+    for (int j = 0; j < count; j++) {
+        rsp_spmat_t A = mats[j];
+        if (!A || !d_buffers[j]) return RSP_STATUS_INVALID_VALUE;
+        if (A->type != compute_type) return RSP_STATUS_NOT_SUPPORTED;
+        if (A->rows > 0 && (!d_y[j] || (A->cols > 0 && !d_x[j]))) return RSP_STATUS_INVALID_VALUE;
+        if (A->plan_buffer != d_buffers[j] || A->plan_type != compute_type) {
+            rsp_status_t st = rsp_spmv_preprocess(h, RSP_OPERATION_NON_TRANSPOSE, pa, A, d_x[j],
+                                                  pb, d_y[j], compute_type, d_buffers[j]);
+            if (st != RSP_STATUS_SUCCESS) return st;
+        }
+    }
+    std::unique_ptr<rsp_spmv_batch> b(new rsp_spmv_batch());
+    b->type = compute_type;
+    b->part = part;
+    // layout: per launch [entries | tiles | long rows], each 16-B aligned
+    struct Span { int first, count, t0, t1, l0, l1; size_t off_e, off_t, off_l; };
+    std::vector<Span> spans;
+    size_t bytes = 0;
+    for (int first = 0; first < count; first += rsp::kSpmvBatchMax) {
+        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, 0, 0, 0};
+        int nt = 0, nl = 0;
+        for (int j = first; j < first + sp.count; j++) {
+            rsp_spmat_t A = mats[j];
+            const int t0 = part == 2 ? A->nint : 0, t1 = part == 1 ? A->nint : A->nblocks;
+            nt += t1 - t0;
+            nl += part == 1 ? 0 : A->nlong;
+        }
+        sp.off_e = bytes;
+        bytes += (size_t)sp.count * sizeof(rsp::SpmvBatchEntry);
+        sp.off_t = bytes;
+        bytes += (size_t)nt * sizeof(SpmvBlock);
+        sp.off_l = bytes;
+        bytes += ((size_t)nl * sizeof(SpmvLongRow) + 15) & ~(size_t)15;
+        spans.push_back(sp);
+    }
+    if (bytes > 0) RSP_CHECK_HIP(hipMalloc(&b->d_mem, bytes));
+    RSP_CHECK_HIP(hipStreamSynchronize(h->stream));  // schedules written on the handle's stream
+    std::vector<unsigned char> host(bytes);
+    for (const Span &sp : spans) {
+        rsp::SpmvBatchArgs a{};
+        a.entries = (const rsp::SpmvBatchEntry *)((char *)b->d_mem + sp.off_e);
+        a.tiles = (const SpmvBlock *)((char *)b->d_mem + sp.off_t);
+        a.longrows = (const SpmvLongRow *)((char *)b->d_mem + sp.off_l);
+        a.count = sp.count;
+        for (int q = 0; q <= rsp::kSpmvBatchMax; q++)
+            a.tiles_at.begin[q] = a.longs_at.begin[q] = INT_MAX;
+        int nt = 0, nl = 0;
+        for (int q = 0; q < sp.count; q++) {
+            rsp_spmat_t A = mats[sp.first + q];
+            const char *buf = (const char *)d_buffers[sp.first + q];
+            const int t0 = part == 2 ? A->nint : 0, t1 = part == 1 ? A->nint : A->nblocks;
+            const int nlq = part == 1 ? 0 : A->nlong;
+            rsp::SpmvBatchEntry e{};
+            e.rowptr = A->rowptr;
+            e.colidx = A->colidx;
+            e.vals = A->vals;
+            e.x = d_x[sp.first + q];
+            e.y = d_y[sp.first + q];
+            e.partials = (void *)(buf + A->off_part);
+            e.nnz = A->nnz_s;
+            e.vector_ok = ((((uintptr_t)A->colidx) | ((uintptr_t)A->vals)) & 15) == 0;
+            memcpy(host.data() + sp.off_e + (size_t)q * sizeof(e), &e, sizeof(e));
+            a.tiles_at.begin[q] = nt;
+            a.longs_at.begin[q] = nl;
+            if (t1 > t0)
+                RSP_CHECK_HIP(hipMemcpy(host.data() + sp.off_t + (size_t)nt * sizeof(SpmvBlock),
+                                        buf + (size_t)t0 * sizeof(SpmvBlock),
+                                        (size_t)(t1 - t0) * sizeof(SpmvBlock),
+                                        hipMemcpyDeviceToHost));
+            if (nlq > 0)
+                RSP_CHECK_HIP(hipMemcpy(host.data() + sp.off_l + (size_t)nl * sizeof(SpmvLongRow),
+                                        buf + A->off_long, (size_t)nlq * sizeof(SpmvLongRow),
+                                        hipMemcpyDeviceToHost));
+            nt += t1 - t0;
+            nl += nlq;
+        }
+        a.tiles_at.begin[sp.count] = nt;
+        a.longs_at.begin[sp.count] = nl;
+        b->launches.push_back(a);
+    }
+    if (bytes > 0) RSP_CHECK_HIP(hipMemcpy(b->d_mem, host.data(), bytes, hipMemcpyHostToDevice));
+    for (int j = 0; j < count; j++) {
+        b->mats.push_back(mats[j]);
+        b->buffers.push_back(d_buffers[j]);
+        b->plan_gen.push_back(mats[j]->plan_gen);
+    }
+    *batch = b.release();
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_spmv_batch_run(rsp_handle_t h, rsp_spmv_batch_t b, const void *alpha,
+                                const void *beta) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!b || !alpha || !beta) return RSP_STATUS_INVALID_VALUE;
+    for (size_t j = 0; j < b->mats.size(); j++) {  // re-planned since create: stale copy
+        const rsp_spmat_t A = b->mats[j];
+        if (A->plan_buffer != b->buffers[j] || A->plan_gen != b->plan_gen[j])
+            return RSP_STATUS_INVALID_VALUE;
+    }
+    const double av = b->type == RSP_R_64F ? *(const double *)alpha : *(const float *)alpha;
+    const double bv = b->type == RSP_R_64F ? *(const double *)beta : *(const float *)beta;
+    if (b->part != 0 && bv != 0.0) return RSP_STATUS_INVALID_VALUE;
+    for (rsp::SpmvBatchArgs a : b->launches) {
+        a.alpha = av;
+        a.beta = bv;
+        a.variant = h->spmv_variant;
+        hipError_t e;
+        if (b->type == RSP_R_64F)
+            e = rsp_k::spmv_batch_f64(a, h->stream);
+        else
+            e = h->ftz ? rsp_k_ftz::spmv_batch_f32(a, h->stream) : rsp_k::spmv_batch_f32(a, h->stream);
+        if (e != hipSuccess) return RSP_STATUS_EXECUTION_FAILED;
+    }
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_spmv_batch_destroy(rsp_spmv_batch_t b) {
+    if (!b) return RSP_STATUS_INVALID_VALUE;
+    delete b;
+    return RSP_STATUS_SUCCESS;
 }
 
 rsp_status_t rsp_gather(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, const int64_t *d_idx,

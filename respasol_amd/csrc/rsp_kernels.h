@@ -70,6 +70,36 @@ struct SpmvArgs {
                     // bit 4 (plan time): no spreading of sub-wave plans
 };
 
+// Several independent SpMVs in one launch (rsp_spmv_batch_*). The batch
+// concatenates the matrices' tiles and long rows; matrix j of a launch owns
+// tiles [tiles.begin[j], tiles.begin[j + 1]) and long rows
+// [longs.begin[j], longs.begin[j + 1]). The begin tables travel in the kernel
+// arguments (entries past `count` hold INT_MAX), so a workgroup finds its
+// matrix with scalar compares and loads its entry and its tile in parallel.
+constexpr int kSpmvBatchMax = 16;  // matrices per launch
+struct alignas(16) SpmvBatchEntry {
+    const int *rowptr;
+    const int *colidx;
+    const void *vals;
+    const void *x;
+    void *y;
+    void *partials;
+    int nnz;        // rowptr[m] (as SpmvArgs::nnz)
+    int vector_ok;  // colidx/vals 16-B aligned
+};
+struct SpmvBatchTable {
+    int begin[kSpmvBatchMax + 1];
+};
+struct SpmvBatchArgs {
+    const SpmvBatchEntry *entries;
+    const SpmvBlock *tiles;
+    const SpmvLongRow *longrows;
+    int count;
+    SpmvBatchTable tiles_at, longs_at;
+    double alpha, beta;
+    int variant;  // bit 0: default-policy loads; bit 3: no per-matrix XCD swizzle
+};
+
 // Level schedule of one dependency DAG. Rows are grouped by level
 // (rows[ptr[l] .. ptr[l+1])); `segs` (host) cover the levels in order, each
 // {lev_begin, lev_end, thin, chunk_begin, chunk_end}: a thin segment is a run
@@ -184,6 +214,7 @@ struct TrsvArgs {
 #define RSP_DECLARE_KERNEL_API(NS)                                                              \
     namespace NS {                                                                              \
     hipError_t spmv_f32(const rsp::SpmvArgs &a, hipStream_t s);                                 \
+    hipError_t spmv_batch_f32(const rsp::SpmvBatchArgs &a, hipStream_t s);                      \
     hipError_t ilu0_factor_f32(const rsp::IluArgs &a, hipStream_t s);                           \
     hipError_t trsv_lower_n_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
     hipError_t trsv_lower_t_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
@@ -199,6 +230,7 @@ hipError_t gather(int elem_bytes, int64_t n, const int64_t *idx, const void *src
 hipError_t scatter(int elem_bytes, int64_t n, const int64_t *idx, const void *src, void *dst,
                    hipStream_t s);
 hipError_t spmv_f64(const rsp::SpmvArgs &a, hipStream_t s);
+hipError_t spmv_batch_f64(const rsp::SpmvBatchArgs &a, hipStream_t s);
 int spmv_tiles_per_cu(int elem_bytes);  // resident spmv_tiles workgroups per CU
 hipError_t ilu0_factor_f64(const rsp::IluArgs &a, hipStream_t s);
 hipError_t trsv_lower_n_f64(const rsp::TrsvArgs &a, hipStream_t s);

@@ -7,6 +7,8 @@ Mapping to the reference's cuSPARSE usage:
   SpMat                  cusparseCreateCsr + SpMV_bufferSize + the caller's
                          workspace cudaMalloc                (GPU/spmv.cu:148-164)
   SpMat.spmv             cusparseSpMV                        (GPU/spmv.cu:184-186)
+  SpmvBatch              cusparseSpMV over several matrices as one launch (no
+                         cuSPARSE counterpart; bits equal to SpMat.spmv each)
   Ilu0.analysis          csrilu02_analysis + 2x csrsv2_analysis (GPU/ilu0.cu:203-252)
   Ilu0.zero_pivot        cusparseXcsrilu02_zeroPivot         (GPU/ilu0.cu:222,278)
   Ilu0.factor            cusparse?csrilu02                   (GPU/ilu0.cu:264-268)
@@ -57,24 +59,6 @@ class Handle:
     def set_ftz(self, on: bool) -> None:
         self.ftz = bool(on)
         check(rsp.rsp_set_ftz(self._h, 1 if on else 0), "rsp_set_ftz")
-
-    def set_local_cols(self, ncols_local: int) -> None:
-        """Split the schedule for halo overlap (rsp_spmat_set_local_cols): tiles
-        reading columns < ncols_local only (the rank's own x) run as part 1."""
-        check(rsp.rsp_spmat_set_local_cols(self._mat, int(ncols_local)), "rsp_spmat_set_local_cols")
-        one, zero = _scalar(1.0, self.dtype), _scalar(0.0, self.dtype)
-        check(rsp.rsp_spmv_preprocess(self.handle.ptr, _lib.OP_N, C.byref(one), self._mat, None,
-                                      C.byref(zero), None, _DT[self.dtype], _ptr(self.buffer)),
-              "rsp_spmv_preprocess")
-
-    def spmv_part(self, x: torch.Tensor, y: torch.Tensor, part: int, alpha: float = 1.0) -> torch.Tensor:
-        """Part 1 (interior tiles) or 2 (the rest + fixup) of y = alpha*A*x (rsp_spmv_part)."""
-        if x.dtype != self.dtype or x.numel() < self.n:
-            raise ValueError("x has the wrong dtype or length")
-        a, b = _scalar(alpha, self.dtype), _scalar(0.0, self.dtype)
-        check(rsp.rsp_spmv_part(self.handle.ptr, C.byref(a), self._mat, _ptr(x), C.byref(b), _ptr(y),
-                                _DT[self.dtype], _ptr(self.buffer), int(part)), "rsp_spmv_part")
-        return y
 
     def close(self) -> None:
         if self._h:
@@ -173,6 +157,49 @@ class SpMat:
             pass
 
 
+class SpmvBatch:
+    """Several independent products y_j = alpha*A_j*x_j (+ beta*y_j) as one
+    launch (rsp_spmv_batch_*): the same bits per matrix as SpMat.spmv /
+    spmv_part, without one kernel ramp and drain per matrix. The x/y tensors
+    are recorded: keep them (and the matrices) alive and in place."""
+
+    def __init__(self, handle: Handle, mats: list[SpMat], xs: list[torch.Tensor],
+                 ys: list[torch.Tensor], part: int = 0):
+        if not (len(mats) == len(xs) == len(ys)):
+            raise ValueError("mats, xs and ys must have the same length")
+        dt = mats[0].dtype if mats else torch.float64
+        for A, x, y in zip(mats, xs, ys):
+            if A.dtype != dt or x.dtype != dt or y.dtype != dt:
+                raise ValueError("one compute type per batch")
+            if x.numel() < A.n or y.numel() < A.m:
+                raise ValueError("x or y too short")
+        self.handle, self.dtype, self.part = handle, dt, int(part)
+        self._keep = (list(mats), list(xs), list(ys))
+        n = len(mats)
+        arr = C.c_void_p * max(n, 1)
+        self._b = C.c_void_p()
+        check(rsp.rsp_spmv_batch_create(
+            handle.ptr, n, arr(*[A._mat.value for A in mats]), arr(*[x.data_ptr() for x in xs]),
+            arr(*[y.data_ptr() for y in ys]), arr(*[A.buffer.data_ptr() for A in mats]),
+            _DT[dt], self.part, C.byref(self._b)), "rsp_spmv_batch_create")
+
+    def run(self, alpha: float = 1.0, beta: float = 0.0) -> None:
+        a, b = _scalar(alpha, self.dtype), _scalar(beta, self.dtype)
+        check(rsp.rsp_spmv_batch_run(self.handle.ptr, self._b, C.byref(a), C.byref(b)),
+              "rsp_spmv_batch_run")
+
+    def close(self) -> None:
+        if self._b:
+            rsp.rsp_spmv_batch_destroy(self._b)
+            self._b = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Ilu0:
     """ILU(0) + unit-lower triangular solves on one analysed pattern."""
 
@@ -224,24 +251,6 @@ class Ilu0:
         a = _scalar(alpha, values.dtype)
         check(rsp.rsp_trsv_upper(self.handle.ptr, C.byref(a), self._info, _DT[values.dtype],
                                  _ptr(values), _ptr(x), _ptr(y)), "rsp_trsv_upper")
-        return y
-
-    def set_local_cols(self, ncols_local: int) -> None:
-        """Split the schedule for halo overlap (rsp_spmat_set_local_cols): tiles
-        reading columns < ncols_local only (the rank's own x) run as part 1."""
-        check(rsp.rsp_spmat_set_local_cols(self._mat, int(ncols_local)), "rsp_spmat_set_local_cols")
-        one, zero = _scalar(1.0, self.dtype), _scalar(0.0, self.dtype)
-        check(rsp.rsp_spmv_preprocess(self.handle.ptr, _lib.OP_N, C.byref(one), self._mat, None,
-                                      C.byref(zero), None, _DT[self.dtype], _ptr(self.buffer)),
-              "rsp_spmv_preprocess")
-
-    def spmv_part(self, x: torch.Tensor, y: torch.Tensor, part: int, alpha: float = 1.0) -> torch.Tensor:
-        """Part 1 (interior tiles) or 2 (the rest + fixup) of y = alpha*A*x (rsp_spmv_part)."""
-        if x.dtype != self.dtype or x.numel() < self.n:
-            raise ValueError("x has the wrong dtype or length")
-        a, b = _scalar(alpha, self.dtype), _scalar(0.0, self.dtype)
-        check(rsp.rsp_spmv_part(self.handle.ptr, C.byref(a), self._mat, _ptr(x), C.byref(b), _ptr(y),
-                                _DT[self.dtype], _ptr(self.buffer), int(part)), "rsp_spmv_part")
         return y
 
     def close(self) -> None:

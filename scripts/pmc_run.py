@@ -7,7 +7,10 @@ collected in separate runs, guide §rocprofv3).
    bytes-per-unit for this kernel's access pattern (the gfx950 FETCH_SIZE
    under-count of wide loads, MI355X_MICROARCH.md §HBM);
 2. the bench workload: `--passes` cycles of fp64 SpMV over every matrix of
-   the set (the same order as bench.py, so no matrix is cache-resident).
+   the set, one launch per matrix (the same order as bench.py, so no matrix
+   is cache-resident);
+3. `--passes` batched launches over the whole set (rsp_spmv_batch, the
+   bench's default step).
 scripts/pmc_summary.py turns the two CSVs into profiles/<tag>_pmc.json.
 """
 from __future__ import annotations
@@ -23,7 +26,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from respasol_amd import csr  # noqa: E402
-from respasol_amd.sparse import Handle, SpMat, upload_csr  # noqa: E402
+from respasol_amd.sparse import Handle, SpMat, SpmvBatch, upload_csr  # noqa: E402
 
 
 def main():
@@ -59,9 +62,14 @@ def main():
         for name, b, M, xx, yy in mats:
             M.spmv(xx, yy)
     torch.cuda.synchronize()
+    B = SpmvBatch(h, [q[2] for q in mats], [q[3] for q in mats], [q[4] for q in mats])
+    for _ in range(args.passes):
+        B.run()
+    torch.cuda.synchronize()
     if args.meta:
         with open(args.meta, "w") as f:
             json.dump({"calibration": calib, "set": args.set, "passes": args.passes,
+                       "batch_launches_per_pass": -(-len(mats) // 16),
                        "matrices": [{"name": n_, "grid": int(M.buffer.numel()), "alg_bytes": b}
                                     for n_, b, M, _, _ in mats]}, f)
 

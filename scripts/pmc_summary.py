@@ -20,12 +20,12 @@ import json
 import os
 
 
-def load(dirname, counter):
+def load(dirname, counter, kernel="spmv_tiles<double"):
     files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
     rows = []
     for f in files:
         for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") == counter and "spmv_tiles<double" in r.get("Kernel_Name", ""):
+            if r.get("Counter_Name") == counter and kernel in r.get("Kernel_Name", ""):
                 rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     rows.sort()
     # one value per dispatch (sum over XCD/agent instances if split)
@@ -66,16 +66,35 @@ def main():
     steady = per[nm:] if launches > nm else per
     hbm = sum(p["hbm_bytes"] for p in steady) / len(steady)
     algb = sum(p["alg_bytes"] for p in steady) / len(steady)
+    per_matrix = {"kernel": "rsp_k::spmv_tiles<double,true,false>",
+                  "hbm_bytes_per_launch": round(hbm), "algorithmic_bytes_per_launch": round(algb),
+                  "traffic_over_algorithmic": round(hbm / algb, 4)}
+    # batched launches (one per <= 16 matrices per pass): same correction
+    fb = load(args.fetch, "FETCH_SIZE", "spmv_tiles_batch<double")
+    wb = load(args.write, "WRITE_SIZE", "spmv_tiles_batch<double")
+    batch = None
+    nb = min(len(fb), len(wb))
+    lpp = meta.get("batch_launches_per_pass", 1)
+    if nb >= 2 * lpp and lpp == 1:
+        hb = [fb[i] * 1024.0 * rf + wb[i] * 1024.0 * wf for i in range(nb)][1:]  # skip the cold pass
+        hbm_b = sum(hb) / len(hb)
+        alg_b = float(sum(alg))
+        batch = {"kernel": "rsp_k::spmv_tiles_batch<double,true,false,true>",
+                 "hbm_bytes_per_launch": round(hbm_b), "algorithmic_bytes_per_launch": round(alg_b),
+                 "traffic_over_algorithmic": round(hbm_b / alg_b, 4), "launches": nb}
+    top = batch or per_matrix
     out = {
         "workload": args.workload,
-        "kernel": "rsp_k::spmv_tiles<double,true,false>",
+        "kernel": top["kernel"],
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs; corrected by a "
-                  "diagonal-matrix calibration launch of the same kernel with exactly known bytes",
+                  "diagonal-matrix calibration launch of the same tile code with exactly known bytes",
         "calibration": {"read_bytes_per_counted_byte": rf, "write_bytes_per_counted_byte": wf,
                         "rows": cal["rows"]},
-        "hbm_bytes_per_launch": round(hbm),
-        "algorithmic_bytes_per_launch": round(algb),
-        "traffic_over_algorithmic": round(hbm / algb, 4),
+        "hbm_bytes_per_launch": top["hbm_bytes_per_launch"],
+        "algorithmic_bytes_per_launch": top["algorithmic_bytes_per_launch"],
+        "traffic_over_algorithmic": top["traffic_over_algorithmic"],
+        "batch": batch,
+        "per_matrix": per_matrix,
         "per_matrix_last_pass": {p["matrix"]: {"hbm_bytes": round(p["hbm_bytes"]),
                                                "alg_bytes": p["alg_bytes"],
                                                "ratio": round(p["hbm_bytes"] / p["alg_bytes"], 3)}
