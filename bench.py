@@ -415,8 +415,8 @@ def main():
                 "nnz_stored_total": int(sum(s.nnz_global for s in slices)),
                 "parallelism": f"row-partition x{world}" if world > 1 else "1 GPU",
                 "launch": "one rsp_spmv per matrix" if args.no_batch else
-                          ("rsp_spmv_batch: interior + boundary launches" if overlap
-                           else "rsp_spmv_batch: one launch per step"),
+                          (f"rsp_spmv_batch ({per_step} launch(es) of <= 16 matrices per step part): "
+                           + ("interior, then boundary" if overlap else "whole step")),
                 "collective": (("halo all_to_all_single" + ("" if args.no_bucket else
                                  " (one per step, bucketed over the matrices)")
                                  + (", interior tiles overlapped" if overlap else "")
