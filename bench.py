@@ -316,6 +316,10 @@ def main():
         kern_ms = k0_.elapsed_time(k1_)
     bytes64 = sum(s.bytes_local(8) for s in slices)
     achieved = bytes64 * args.steps / (kern_ms * 1e-3) / 1e9
+    # the schedule reads 16-bit column offsets for tiles spanning < 65536
+    # columns: 2 B of the CSR's 4-B index per such entry are never moved
+    saved64 = 2 * sum(s.mat64.plan_info()["entries_16bit"] for s in slices)
+    moved_achieved = (bytes64 - saved64) * args.steps / (kern_ms * 1e-3) / 1e9
     # the same K steps as one rsp_spmv launch per matrix (kernel-only), for
     # comparison with the batched launch: what a caller doing one SpMV at a
     # time sees
@@ -439,6 +443,12 @@ def main():
                 "traffic": traffic,
                 "avg_launch_us": round(kern_ms / launches * 1e3, 3),
                 "bytes_per_launch_avg": int(bytes64 / per_step),
+                "note": "achieved/frac count the CSR's algorithmic bytes (SURVEY 8d: 12 B per stored "
+                        "entry fp64); the kernel reads 16-bit column offsets where a tile spans < 65536 "
+                        "columns, so it moves index_bytes_saved fewer: moved_* below",
+                "index_bytes_saved_per_launch": int(saved64 / per_step),
+                "moved_achieved": round(moved_achieved, 1),
+                "moved_frac": round(moved_achieved / HBM_PEAK_GBS, 4),
             },
             "cpu_baseline": cpu,
             "fp32": fp32,

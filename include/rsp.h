@@ -105,8 +105,13 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t handle, rsp_operation_t op, const
                                   rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
                                   size_t *buffer_size);
 /* cusparseSpMV_preprocess analogue: builds the row-block schedule of `mat`
- * into `d_buffer` (host-blocking: reads the row offsets once). rsp_spmv on a
- * buffer that was not preprocessed for `mat` preprocesses it first. */
+ * into `d_buffer` (host-blocking: reads the row offsets and column indices
+ * once, validates the indices, and stores a 16-bit copy of them, relative to
+ * each tile's first column, for tiles spanning < 65536 columns — the
+ * workspace holds 2 B per entry for it). rsp_spmv on a buffer that was not
+ * preprocessed for `mat` preprocesses it first. As with cuSPARSE's
+ * preprocess, the sparsity pattern must not change afterwards without a new
+ * preprocess (values may: they are read from the matrix on every call). */
 rsp_status_t rsp_spmv_preprocess(rsp_handle_t handle, rsp_operation_t op, const void *alpha,
                                  rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
                                  rsp_datatype_t compute_type, void *d_buffer);
@@ -179,6 +184,13 @@ rsp_status_t rsp_gather(rsp_handle_t handle, rsp_datatype_t value_type, int64_t 
 /* Indexed scatter dst[idx[i]] = src[i] for i < n (idx without duplicates). */
 rsp_status_t rsp_scatter(rsp_handle_t handle, rsp_datatype_t value_type, int64_t n,
                          const int64_t *d_idx, const void *d_src, void *d_dst);
+
+/* Schedule facts of the last rsp_spmv_preprocess of `mat` (no cuSPARSE
+ * counterpart; for byte accounting): its tile count, and how many stored
+ * entries it reads through 16-bit column offsets (2 B each instead of the
+ * 4-B colidx: tiles whose columns span < 65536; the rest read colidx).
+ * NOT_INITIALIZED before the first preprocess. */
+rsp_status_t rsp_spmv_plan_info(rsp_spmat_t mat, int64_t *tiles, int64_t *entries_16bit);
 
 /* Overlap of the halo exchange with the SpMV. Columns [0, ncols_local) of
  * `mat` are the rank's own x entries, the others arrive with the exchange.

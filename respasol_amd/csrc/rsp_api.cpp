@@ -42,6 +42,8 @@ struct rsp_spmat {
     int nblocks, nlong, nslots;
     int nnz_s;                  // rowptr[rows] seen by the preprocess
     size_t off_long, off_part;  // byte offsets inside the buffer
+    size_t off_cbase, off_cidx;
+    int64_t nnz_c16;            // entries read through 16-bit column offsets
     int64_t local_cols;         // rsp_spmat_set_local_cols (-1: not split)
     int nint;                   // interior tiles at the front of the schedule
     unsigned plan_gen;          // bumped by every preprocess (batch staleness check)
@@ -231,12 +233,19 @@ static SpmvBounds spmv_bounds(int64_t rows, int64_t nnz, int cap) {
     return b;
 }
 
-static size_t spmv_bytes(const SpmvBounds &b, size_t elem, size_t *off_long, size_t *off_part) {
-    size_t o1 = align256(b.nblocks * sizeof(SpmvBlock));
-    size_t o2 = o1 + align256(b.nlong * sizeof(SpmvLongRow));
-    if (off_long) *off_long = o1;
-    if (off_part) *off_part = o2;
-    return o2 + align256(b.nslots * elem);
+// Workspace: [tiles | long rows | chunk partials | per-tile column base |
+// 16-bit column offsets (2 B per stored entry)].
+struct SpmvLayout {
+    size_t off_long, off_part, off_cbase, off_cidx, bytes;
+};
+static SpmvLayout spmv_layout(const SpmvBounds &b, size_t elem, int64_t nnz) {
+    SpmvLayout l;
+    l.off_long = align256(b.nblocks * sizeof(SpmvBlock));
+    l.off_part = l.off_long + align256(b.nlong * sizeof(SpmvLongRow));
+    l.off_cbase = l.off_part + align256(b.nslots * elem);
+    l.off_cidx = l.off_cbase + align256(b.nblocks * sizeof(int));
+    l.bytes = l.off_cidx + align256((size_t)std::max<int64_t>(nnz, 0) * sizeof(uint16_t));
+    return l;
 }
 
 static int tile_cap(rsp_datatype_t t) {
@@ -257,7 +266,7 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void
     if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
     if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
     SpmvBounds b = spmv_bounds(mat->rows, mat->nnz, chunk_cap(compute_type));
-    *buffer_size = spmv_bytes(b, elem_size(compute_type), nullptr, nullptr);
+    *buffer_size = spmv_layout(b, elem_size(compute_type), mat->nnz).bytes;
     return RSP_STATUS_SUCCESS;
 }
 
@@ -409,12 +418,42 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     if (blocks.size() > b.nblocks || longrows.size() > b.nlong || (size_t)nslots > b.nslots)
         return RSP_STATUS_INVALID_VALUE;
     if (!blocks.empty() && !d_buffer) return RSP_STATUS_INVALID_VALUE;
-    size_t off_long = 0, off_part = 0;
-    spmv_bytes(b, elem_size(compute_type), &off_long, &off_part);
+    const SpmvLayout lay = spmv_layout(b, elem_size(compute_type), mat->nnz);
+    // 16-bit column offsets: a tile whose columns span < 65536 reads
+    // col = cbase + off (2 B per entry instead of 4; the int32 colidx is not
+    // read for it). Built once here, like the schedule; RSP_SPMV_VARIANT bit
+    // 5 keeps every tile on the int32 indices.
+    const int64_t nnz_s = m > 0 ? rp[(size_t)m] : 0;
+    std::vector<int> cbase(blocks.size(), -1);
+    std::vector<uint16_t> c16;
+    int64_t nnz_c16 = 0;
+    if (!(h->spmv_variant & 32) && nnz_s > 0 && nnz_s <= mat->nnz) {
+        c16.assign((size_t)nnz_s, 0);
+        for (size_t t = 0; t < blocks.size(); t++) {
+            const SpmvBlock &bk = blocks[t];
+            if (bk.k1 <= bk.k0) continue;
+            int lo = ci[(size_t)bk.k0], hi = lo;
+            for (int k = bk.k0 + 1; k < bk.k1; k++) {
+                lo = std::min(lo, ci[(size_t)k]);
+                hi = std::max(hi, ci[(size_t)k]);
+            }
+            if (hi - lo > 65535) continue;
+            cbase[t] = lo;
+            nnz_c16 += bk.k1 - bk.k0;
+            for (int k = bk.k0; k < bk.k1; k++) c16[(size_t)k] = (uint16_t)(ci[(size_t)k] - lo);
+        }
+    }
     char *buf = (char *)d_buffer;
-    if (!blocks.empty())
+    if (!blocks.empty()) {
         RSP_CHECK_HIP(hipMemcpyAsync(buf, blocks.data(), blocks.size() * sizeof(SpmvBlock),
                                      hipMemcpyHostToDevice, h->stream));
+        RSP_CHECK_HIP(hipMemcpyAsync(buf + lay.off_cbase, cbase.data(), cbase.size() * sizeof(int),
+                                     hipMemcpyHostToDevice, h->stream));
+    }
+    if (!c16.empty())
+        RSP_CHECK_HIP(hipMemcpyAsync(buf + lay.off_cidx, c16.data(), c16.size() * sizeof(uint16_t),
+                                     hipMemcpyHostToDevice, h->stream));
+    const size_t off_long = lay.off_long, off_part = lay.off_part;
     if (!longrows.empty())
         RSP_CHECK_HIP(hipMemcpyAsync(buf + off_long, longrows.data(),
                                      longrows.size() * sizeof(SpmvLongRow), hipMemcpyHostToDevice,
@@ -430,6 +469,17 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     mat->nnz_s = m > 0 ? rp[(size_t)m] : 0;
     mat->off_long = off_long;
     mat->off_part = off_part;
+    mat->off_cbase = lay.off_cbase;
+    mat->off_cidx = lay.off_cidx;
+    mat->nnz_c16 = nnz_c16;
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_spmv_plan_info(rsp_spmat_t mat, int64_t *tiles, int64_t *entries_16bit) {
+    if (!mat || !tiles || !entries_16bit) return RSP_STATUS_INVALID_VALUE;
+    if (!mat->plan_buffer) return RSP_STATUS_NOT_INITIALIZED;
+    *tiles = mat->nblocks;
+    *entries_16bit = mat->nnz_c16;
     return RSP_STATUS_SUCCESS;
 }
 
@@ -455,6 +505,9 @@ static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alp
     a.y = d_y;
     a.blocks = (const SpmvBlock *)d_buffer;
     a.nblocks = mat->nblocks;
+    a.cbases = (const int *)((char *)d_buffer + mat->off_cbase);
+    a.cidx = (const unsigned short *)((char *)d_buffer + mat->off_cidx);
+    a.cmax = mat->cols > 0 ? (int)(mat->cols - 1) : 0;
     a.longrows = (const SpmvLongRow *)((char *)d_buffer + mat->off_long);
     a.nlong = mat->nlong;
     a.partials = (char *)d_buffer + mat->off_part;
@@ -472,6 +525,7 @@ static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alp
             a.nlong = 0;
         } else {
             a.blocks += mat->nint;
+            a.cbases += mat->nint;
             a.nblocks = mat->nblocks - mat->nint;
         }
     }
@@ -544,11 +598,11 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
     b->type = compute_type;
     b->part = part;
     // layout: per launch [entries | tiles | long rows], each 16-B aligned
-    struct Span { int first, count, t0, t1, l0, l1; size_t off_e, off_t, off_l; };
+    struct Span { int first, count, t0, t1, l0, l1; size_t off_e, off_t, off_c, off_l; };
     std::vector<Span> spans;
     size_t bytes = 0;
     for (int first = 0; first < count; first += rsp::kSpmvBatchMax) {
-        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, 0, 0, 0};
+        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, 0, 0, 0, 0};
         int nt = 0, nl = 0;
         for (int j = first; j < first + sp.count; j++) {
             rsp_spmat_t A = mats[j];
@@ -560,6 +614,8 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         bytes += (size_t)sp.count * sizeof(rsp::SpmvBatchEntry);
         sp.off_t = bytes;
         bytes += (size_t)nt * sizeof(SpmvBlock);
+        sp.off_c = bytes;
+        bytes += ((size_t)nt * sizeof(int) + 15) & ~(size_t)15;
         sp.off_l = bytes;
         bytes += ((size_t)nl * sizeof(SpmvLongRow) + 15) & ~(size_t)15;
         spans.push_back(sp);
@@ -571,6 +627,7 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         rsp::SpmvBatchArgs a{};
         a.entries = (const rsp::SpmvBatchEntry *)((char *)b->d_mem + sp.off_e);
         a.tiles = (const SpmvBlock *)((char *)b->d_mem + sp.off_t);
+        a.cbases = (const int *)((char *)b->d_mem + sp.off_c);
         a.longrows = (const SpmvLongRow *)((char *)b->d_mem + sp.off_l);
         a.count = sp.count;
         for (int q = 0; q <= rsp::kSpmvBatchMax; q++)
@@ -588,6 +645,8 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
             e.x = d_x[sp.first + q];
             e.y = d_y[sp.first + q];
             e.partials = (void *)(buf + A->off_part);
+            e.cidx = (const unsigned short *)(buf + A->off_cidx);
+            e.cmax = A->cols > 0 ? (int)(A->cols - 1) : 0;
             e.nnz = A->nnz_s;
             e.vector_ok = ((((uintptr_t)A->colidx) | ((uintptr_t)A->vals)) & 15) == 0;
             memcpy(host.data() + sp.off_e + (size_t)q * sizeof(e), &e, sizeof(e));
@@ -598,6 +657,10 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
                                         buf + (size_t)t0 * sizeof(SpmvBlock),
                                         (size_t)(t1 - t0) * sizeof(SpmvBlock),
                                         hipMemcpyDeviceToHost));
+            if (t1 > t0)
+                RSP_CHECK_HIP(hipMemcpy(host.data() + sp.off_c + (size_t)nt * sizeof(int),
+                                        buf + A->off_cbase + (size_t)t0 * sizeof(int),
+                                        (size_t)(t1 - t0) * sizeof(int), hipMemcpyDeviceToHost));
             if (nlq > 0)
                 RSP_CHECK_HIP(hipMemcpy(host.data() + sp.off_l + (size_t)nl * sizeof(SpmvLongRow),
                                         buf + A->off_long, (size_t)nlq * sizeof(SpmvLongRow),

@@ -60,6 +60,9 @@ struct SpmvArgs {
     void *y;
     const SpmvBlock *blocks;
     int nblocks;
+    const int *cbases;            // per tile: column base of its 16-bit offsets, -1 = int32 colidx
+    const unsigned short *cidx;   // 16-bit column offsets (tiles with cbases >= 0)
+    int cmax;                     // n - 1 (clamp for neighbour entries of partial vectors)
     const SpmvLongRow *longrows;
     int nlong;
     void *partials;
@@ -84,8 +87,10 @@ struct alignas(16) SpmvBatchEntry {
     const void *x;
     void *y;
     void *partials;
+    const unsigned short *cidx;  // 16-bit column offsets (SpmvArgs::cidx)
     int nnz;        // rowptr[m] (as SpmvArgs::nnz)
     int vector_ok;  // colidx/vals 16-B aligned
+    int cmax;       // n - 1
 };
 struct SpmvBatchTable {
     int begin[kSpmvBatchMax + 1];
@@ -93,6 +98,7 @@ struct SpmvBatchTable {
 struct SpmvBatchArgs {
     const SpmvBatchEntry *entries;
     const SpmvBlock *tiles;
+    const int *cbases;  // per tile, parallel to `tiles`
     const SpmvLongRow *longrows;
     int count;
     SpmvBatchTable tiles_at, longs_at;

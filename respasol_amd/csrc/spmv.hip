@@ -76,11 +76,13 @@ template <>
 struct VecT<double, 2> {
     typedef double __attribute__((ext_vector_type(2))) V;
     typedef int __attribute__((ext_vector_type(2))) I;
+    typedef unsigned short __attribute__((ext_vector_type(2))) H;
 };
 template <>
 struct VecT<float, 4> {
     typedef float __attribute__((ext_vector_type(4))) V;
     typedef int __attribute__((ext_vector_type(4))) I;
+    typedef unsigned short __attribute__((ext_vector_type(4))) H;
 };
 
 // Logical tile for workgroup `bid`: each of the 8 XCDs (round-robin dispatch)
@@ -109,24 +111,35 @@ __device__ __forceinline__ P ld(const P *p) {
 // touch in-bounds neighbours whose LDS slots are never read. Requires a
 // non-empty tile whose last vector does not straddle the end of the arrays
 // (the caller takes stream_products_scalar otherwise).
-template <typename T, bool NT, int NTH = kSpmvThreads,
+// C16: the column indices come from the schedule's 16-bit copy, col = cbase
+// + off (the tile's columns span < 65536; rsp_spmv_preprocess): 2 B instead
+// of 4 B per entry. A partial vector's neighbour entries belong to another
+// tile and another base, so their decoded column is clamped to cmax = n - 1
+// (in bounds; their products are never read).
+template <typename T, bool NT, bool C16 = false, int NTH = kSpmvThreads,
           int IT = SpmvTile<T>::kSlots / (kSpmvThreads * (16 / sizeof(T)))>
 __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
-                                                const T *__restrict__ vals,
+                                                const unsigned short *__restrict__ cidx, int cbase,
+                                                int cmax, const T *__restrict__ vals,
                                                 const T *__restrict__ x, int kb, int k1,
                                                 T *__restrict__ lds) {
     constexpr int VW = 16 / sizeof(T);
     typedef typename VecT<T, VW>::V V;
     typedef typename VecT<T, VW>::I I;
+    typedef typename VecT<T, VW>::H H;
     const int tid = threadIdx.x;
     const int last = (k1 - 1) & ~(VW - 1);
     I ci[IT];
-    V vv[IT];
+    H ch[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int e = min(kb + (it * NTH + tid) * VW, last);
-        ci[it] = ld<NT>(reinterpret_cast<const I *>(colidx + e));
+        if constexpr (C16)
+            ch[it] = ld<NT>(reinterpret_cast<const H *>(cidx + e));
+        else
+            ci[it] = ld<NT>(reinterpret_cast<const I *>(colidx + e));
     }
+    V vv[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int e = min(kb + (it * NTH + tid) * VW, last);
@@ -142,7 +155,14 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
-        for (int j = 0; j < VW; ++j) xv[it][j] = x[(RSP_PROBE == 1 || RSP_PROBE == 3) ? (ci[it][j] & 4095) : ci[it][j]];
+        for (int j = 0; j < VW; ++j) {
+            int c;
+            if constexpr (C16)
+                c = min(cbase + (int)ch[it][j], cmax);
+            else
+                c = ci[it][j];
+            xv[it][j] = x[(RSP_PROBE == 1 || RSP_PROBE == 3) ? (c & 4095) : c];
+        }
     __builtin_amdgcn_sched_barrier(0);
     // every slot (it*256 + tid)*VW lies inside the tile's LDS image, so the
     // stores are unpredicated too; slots at or past k1 - kb are never read
@@ -250,6 +270,7 @@ __device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
 template <typename T, bool NT, bool BETA>
 __device__ __forceinline__ void spmv_tile(
     const SpmvBlock blk, const int *__restrict__ rowptr, const int *__restrict__ colidx,
+    const unsigned short *__restrict__ cidx, int cbase, int cmax,
     const T *__restrict__ vals, const T *__restrict__ x, T *__restrict__ y,
     T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, T *lds,
     T *wsum, int *rp_lds) {
@@ -299,8 +320,10 @@ __device__ __forceinline__ void spmv_tile(
         return;
     }
 #endif
-    if (vec)
-        stream_products<T, NT>(colidx, vals, x, kb, k1, lds);
+    if (vec && cbase >= 0)
+        stream_products<T, NT, true>(colidx, cidx, cbase, cmax, vals, x, kb, k1, lds);
+    else if (vec)
+        stream_products<T, NT>(colidx, cidx, 0, 0, vals, x, kb, k1, lds);
     else
         stream_products_scalar<T>(colidx, vals, x, k0, kb, k1, lds);
 #pragma unroll
@@ -348,6 +371,7 @@ template <typename T, bool NT, bool BETA>
 __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
     const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
+    const int *__restrict__ cbases, const unsigned short *__restrict__ cidx, int cmax,
     T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
@@ -360,7 +384,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
 #if RSP_PROBE_PRIO
     __builtin_amdgcn_s_setprio(RSP_PROBE_PRIO);
 #endif
-    spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, vals, x, y,
+    spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, cidx, cbases[b], cmax, vals, x, y,
                            partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds);
 }
 
@@ -390,7 +414,7 @@ __global__ __launch_bounds__(64) void spmv_longrow_fixup(const SpmvLongRow *__re
 template <typename T, bool NT, bool BETA, bool SWZ>
 __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     const SpmvBatchEntry *__restrict__ entries, const SpmvBlock *__restrict__ tiles,
-    SpmvBatchTable at, T alpha, T beta) {
+    const int *__restrict__ cbases, SpmvBatchTable at, T alpha, T beta) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
@@ -405,7 +429,8 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
         }
     const int t = lo + (SWZ ? xcd_swizzle(b - lo, hi - lo) : b - lo);
     const SpmvBatchEntry e = entries[j];
-    spmv_tile<T, NT, BETA>(tiles[t], e.rowptr, e.colidx, (const T *)e.vals, (const T *)e.x,
+    spmv_tile<T, NT, BETA>(tiles[t], e.rowptr, e.colidx, e.cidx, cbases[t], e.cmax,
+                           (const T *)e.vals, (const T *)e.x,
                            (T *)e.y, (T *)e.partials, alpha, beta, BETA, e.nnz, e.vector_ok, lds,
                            wsum, rp_lds);
 }
@@ -446,7 +471,7 @@ static hipError_t launch_spmv_batch(const SpmvBatchArgs &a, hipStream_t s) {
                               : (swz ? spmv_tiles_batch<T, false, false, true>
                                      : spmv_tiles_batch<T, false, false, false>));
         hipLaunchKernelGGL(kern, dim3(ntiles), dim3(kSpmvThreads), 0, s, a.entries, a.tiles,
-                           a.tiles_at, alpha, beta);
+                           a.cbases, a.tiles_at, alpha, beta);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -478,8 +503,8 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     auto kern = (a.variant & 1) ? (bnz ? spmv_tiles<T, false, true> : spmv_tiles<T, false, false>)
                                 : (bnz ? spmv_tiles<T, true, true> : spmv_tiles<T, true, false>);
     hipLaunchKernelGGL(kern, dim3(a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
-                       (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks,
-                       (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok);
+                       (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks, a.cbases,
+                       a.cidx, a.cmax, (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.nlong > 0) {

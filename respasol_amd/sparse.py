@@ -136,6 +136,12 @@ class SpMat:
                                       C.byref(zero), None, _DT[self.dtype], _ptr(self.buffer)),
               "rsp_spmv_preprocess")
 
+    def plan_info(self) -> dict:
+        """{"tiles", "entries_16bit"} of the current schedule (rsp_spmv_plan_info)."""
+        t, e = C.c_int64(), C.c_int64()
+        check(rsp.rsp_spmv_plan_info(self._mat, C.byref(t), C.byref(e)), "rsp_spmv_plan_info")
+        return {"tiles": t.value, "entries_16bit": e.value}
+
     def spmv_part(self, x: torch.Tensor, y: torch.Tensor, part: int, alpha: float = 1.0) -> torch.Tensor:
         """Part 1 (interior tiles) or 2 (the rest + fixup) of y = alpha*A*x (rsp_spmv_part)."""
         if x.dtype != self.dtype or x.numel() < self.n:

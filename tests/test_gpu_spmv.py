@@ -207,10 +207,37 @@ def test_invalid_inputs_are_status_codes(handle):
     assert e.value.status == 3
 
 
-@pytest.mark.parametrize("variant", [1, 16, 17])
+def test_column_offset_tiles(handle):
+    """16-bit column offsets: tiles spanning < 65536 columns read them, wider
+    tiles the int32 indices, in one matrix; a partial vector at a tile edge
+    decodes its neighbour's offset against the wrong base (clamped to n - 1,
+    never read). Rows of 3 put tile edges mid-vector."""
+    n = 200003
+    rows = []
+    for i in range(3001):  # offsets up to 60000 from base 0
+        rows.append([0, 30000 + i % 7, 60000])
+    for i in range(2999):  # base n - 3
+        rows.append([n - 3, n - 2, n - 1])
+    for i in range(3000):  # span > 65535: int32 indices
+        rows.append([i, 100000 + i, n - 1 - i])
+    for i in range(n - len(rows)):  # short banded rows
+        r = len(rows)
+        rows.append(sorted({max(r - 1, 0), r, min(r + 1, n - 1)}))
+    rp = np.zeros(n + 1, np.int32)
+    np.cumsum([len(r) for r in rows], out=rp[1:])
+    ci = np.concatenate([np.array(r, np.int32) for r in rows])
+    rng = np.random.default_rng(11)
+    A = csr.CsrMatrix(0, n, n, len(ci), rp, ci, rng.uniform(-1, 1, len(ci)))
+    x = rng.uniform(-1, 1, n)
+    for dt in (torch.float64, torch.float32):
+        check(A, x, dt, handle)
+
+
+@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33])
 def test_kernel_variants_same_bits(monkeypatch, variant):
     """Every kernel / plan variant (RSP_SPMV_VARIANT: default-policy instead of
-    non-temporal loads; small plans not spread over the chip) gives the same
+    non-temporal loads; small plans not spread over the chip; int32 column
+    indices only, no 16-bit offsets) gives the same
     bits as the canonical-order oracle, on matrices with short rows, rows
     just above the 256 threshold and chunked hub rows."""
     monkeypatch.setenv("RSP_SPMV_VARIANT", str(variant))

@@ -101,9 +101,10 @@ def test_batch_parts_equal_whole(handle, dtype):
     assert e.value.status == 3
 
 
-@pytest.mark.parametrize("variant", [1, 8, 9])
+@pytest.mark.parametrize("variant", [1, 8, 9, 32])
 def test_batch_variants_same_bits(monkeypatch, variant):
-    """Default-policy loads (bit 0) and no per-matrix XCD swizzle (bit 3)."""
+    """Default-policy loads (bit 0), no per-matrix XCD swizzle (bit 3), int32
+    column indices only (bit 5)."""
     monkeypatch.setenv("RSP_SPMV_VARIANT", str(variant))
     h = Handle()
     try:
