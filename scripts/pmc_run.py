@@ -2,8 +2,8 @@
 collected in separate runs, guide §rocprofv3).
 
 1. calibration: y = D x with a 32 M-row DIAGONAL matrix (fp64). Every byte
-   is streamed exactly once (vals 8 B + colidx 4 B + rowptr 4 B + x 8 B read,
-   y 8 B written per row), so its FETCH_SIZE/WRITE_SIZE give the counter's
+   is streamed exactly once (vals 8 B + column index 2 B (16-bit offsets) or
+   4 B + rowptr 4 B + x 8 B read, y 8 B written per row), so its FETCH_SIZE/WRITE_SIZE give the counter's
    bytes-per-unit for this kernel's access pattern (the gfx950 FETCH_SIZE
    under-count of wide loads, MI355X_MICROARCH.md §HBM);
 2. the bench workload: `--passes` cycles of fp64 SpMV over every matrix of
@@ -47,7 +47,11 @@ def main():
     for _ in range(3):
         D.spmv(x, y)
     torch.cuda.synchronize()
-    calib = {"rows": n, "read_bytes": n * (8 + 4 + 4 + 8) + 4, "write_bytes": n * 8, "launches": 3}
+    # vals 8 + rowptr 4 + x 8 B per row, plus the column index: 2 B where the
+    # schedule reads 16-bit offsets (rsp_spmv_plan_info), else 4 B
+    e16 = D.plan_info()["entries_16bit"]
+    calib = {"rows": n, "read_bytes": n * (8 + 4 + 4 + 8) - 2 * e16 + 4, "write_bytes": n * 8,
+             "launches": 3, "entries_16bit": e16}
     del D, rp, ci, va, x, y
     names = csr.surrogate_names(1 if args.set == "big" else 0)
     mats = []
@@ -70,7 +74,8 @@ def main():
         with open(args.meta, "w") as f:
             json.dump({"calibration": calib, "set": args.set, "passes": args.passes,
                        "batch_launches_per_pass": -(-len(mats) // 16),
-                       "matrices": [{"name": n_, "grid": int(M.buffer.numel()), "alg_bytes": b}
+                       "matrices": [{"name": n_, "grid": int(M.buffer.numel()), "alg_bytes": b,
+                                     "entries_16bit": M.plan_info()["entries_16bit"]}
                                     for n_, b, M, _, _ in mats]}, f)
 
 

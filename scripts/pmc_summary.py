@@ -79,9 +79,12 @@ def main():
         hb = [fb[i] * 1024.0 * rf + wb[i] * 1024.0 * wf for i in range(nb)][1:]  # skip the cold pass
         hbm_b = sum(hb) / len(hb)
         alg_b = float(sum(alg))
+        moved_b = alg_b - 2.0 * sum(m.get("entries_16bit", 0) for m in meta["matrices"])
         batch = {"kernel": "rsp_k::spmv_tiles_batch<double,true,false,true>",
                  "hbm_bytes_per_launch": round(hbm_b), "algorithmic_bytes_per_launch": round(alg_b),
-                 "traffic_over_algorithmic": round(hbm_b / alg_b, 4), "launches": nb}
+                 "traffic_over_algorithmic": round(hbm_b / alg_b, 4),
+                 "moved_bytes_per_launch": round(moved_b), "traffic_over_moved": round(hbm_b / moved_b, 4),
+                 "launches": nb}
     top = batch or per_matrix
     out = {
         "workload": args.workload,
