@@ -285,7 +285,7 @@ __global__ __launch_bounds__(NTH) void trsv_thin(TrsvArgs a, T alpha, int c0, in
     __shared__ T lval[rsp::kChunkTerms], lyv[rsp::kChunkTerms];
     __shared__ int lsrc[rsp::kChunkTerms];
     __shared__ rsp::RowTask ltask[rsp::kChunkRows];
-    __shared__ T lx[rsp::kChunkRows], ldg[rsp::kChunkRows];
+    __shared__ T lx[rsp::kChunkRows], ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
     __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];  // a chunk has <= kChunkRows levels
     const int tid = threadIdx.x;
     const T *vals = (const T *)a.vals, *x = (const T *)a.x;
@@ -293,14 +293,13 @@ __global__ __launch_bounds__(NTH) void trsv_thin(TrsvArgs a, T alpha, int c0, in
     const int *ptr = a.plan.ptr_dev;
     for (int c = c0; c < c1; ++c) {
         const rsp::LevelChunk ch = a.plan.chunks[c];
-        const int x0 = ptr[ch.l0], x1 = ptr[ch.l1];
-        const int k0 = a.plan.tasks[x0].t0, k1 = a.plan.tasks[x1 - 1].t1;
+        const int x0 = ch.x0, x1 = ch.x1, k0 = ch.k0, k1 = ch.k1;
         __syncthreads();  // the previous chunk's y stores are visible, LDS is free
         for (int r = tid; r < x1 - x0; r += NTH) {
             const rsp::RowTask t = a.plan.tasks[x0 + r];
             ltask[r] = t;
             lx[r] = alpha * x[t.i];
-            ldg[r] = (KIND == 2 && t.d >= 0) ? vals[t.d] : T(0);
+            if constexpr (KIND == 2) ldg[r] = t.d >= 0 ? vals[t.d] : T(0);
         }
         for (int k = tid; k < k1 - k0; k += NTH) {
             const int sc = a.plan.src[k0 + k];
@@ -342,6 +341,139 @@ __global__ __launch_bounds__(NTH) void trsv_thin(TrsvArgs a, T alpha, int c0, in
     }
 }
 
+// Prefetching form of trsv_thin for 1024-thread runs. A chunk holds <= 1024
+// rows and <= 2048 terms: one row and two terms per thread. Its staging data
+// comes in two dependent loads — the plan (task, sources, term positions,
+// level offsets), then the gathers that need it (alpha*x_i, u_ii, term
+// values, staged y) — so the prefetch is two chunks deep: while chunk c's
+// levels run on LDS, the gathers of chunk c+1 (whose plan arrived during
+// chunk c-1) and the plan of chunk c+2 are in flight, and a chunk switch
+// costs two barriers and LDS writes instead of a chain of global round
+// trips. Every prefetch load is unpredicated (indices clamped into range,
+// unused values never stored), so nothing waits for them before the next
+// chunk switch. A term that stages y (src >= 0) has its producer > kYWin
+// rows before its level ends, i.e. before chunk c began (chunks have
+// <= kChunkRows << kYWin rows): that y is final, and its store is visible
+// since chunk c's first barrier.
+template <typename T, int KIND, int B>
+__global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T alpha, int c0,
+                                                                  int c1, int base) {
+    constexpr int NTH = rsp::kThinThreads;
+    constexpr int TPT = (rsp::kChunkTerms + NTH - 1) / NTH;  // terms of a chunk per thread
+    static_assert(rsp::kChunkRows <= NTH, "one row of a chunk per thread");
+    __shared__ T ywin[rsp::kYWin];
+    __shared__ T lval[rsp::kChunkTerms], lyv[rsp::kChunkTerms];
+    __shared__ int lsrc[rsp::kChunkTerms];
+    __shared__ rsp::RowTask ltask[rsp::kChunkRows];
+    __shared__ T lx[rsp::kChunkRows], ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
+    __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];
+    const int tid = threadIdx.x;
+    const T *vals = (const T *)a.vals, *x = (const T *)a.x;
+    T *y = (T *)a.y;
+    const int *ptr = a.plan.ptr_dev;
+    struct Plan {  // this thread's share of a chunk's plan
+        rsp::RowTask t;
+        int sc[TPT], tp[TPT];
+        int lp, ln, lpe;
+    };
+    struct Vals {  // ... and of its gathers
+        T xv, dg, v[TPT], y[TPT];
+    };
+    auto load_plan = [&](const rsp::LevelChunk ch) {
+        Plan p;
+        const int kl = max(ch.k1 - 1, 0), nl = ch.l1 - ch.l0;
+        p.t = a.plan.tasks[min(ch.x0 + tid, max(ch.x1 - 1, 0))];
+#pragma unroll
+        for (int j = 0; j < TPT; ++j) {
+            p.sc[j] = a.plan.src[min(ch.k0 + tid + j * NTH, kl)];
+            p.tp[j] = a.plan.tpos[min(ch.k0 + tid + j * NTH, kl)];
+        }
+        p.lp = ptr[ch.l0 + min(tid, nl)];
+        p.ln = a.plan.nshort[ch.l0 + min(tid, max(nl - 1, 0))];
+        p.lpe = ptr[ch.l1];
+        return p;
+    };
+    auto load_vals = [&](const Plan &p) {
+        Vals v;
+        v.xv = x[p.t.i];  // alpha applied when staged: no arithmetic on a pending load
+        v.dg = KIND == 2 ? vals[max(p.t.d, 0)] : T(0);
+#pragma unroll
+        for (int j = 0; j < TPT; ++j) {
+            v.v[j] = vals[p.tp[j]];
+            v.y[j] = y[max(p.sc[j], 0)];
+        }
+        return v;
+    };
+    auto stage = [&](const rsp::LevelChunk &ch, const Plan &p, const Vals &v) {
+        const int nk = ch.k1 - ch.k0, nl = ch.l1 - ch.l0;
+        __syncthreads();  // the previous chunk's levels are done with LDS
+        if (tid < ch.x1 - ch.x0) {
+            ltask[tid] = p.t;
+            lx[tid] = alpha * v.xv;
+            if constexpr (KIND == 2) ldg[tid] = p.t.d >= 0 ? v.dg : T(0);
+        }
+#pragma unroll
+        for (int j = 0; j < TPT; ++j)
+            if (tid + j * NTH < nk) {
+                lsrc[tid + j * NTH] = p.sc[j];
+                lval[tid + j * NTH] = v.v[j];
+                lyv[tid + j * NTH] = p.sc[j] >= 0 ? v.y[j] : T(0);
+            }
+        if (tid <= nl) lptr[tid] = p.lp;
+        if (tid < nl) lns[tid] = p.ln;
+        if (tid == 0 && nl == NTH) lptr[NTH] = p.lpe;
+        __syncthreads();
+    };
+    auto levels = [&](const rsp::LevelChunk &ch) {
+        const int x0 = ch.x0, k0 = ch.k0;
+        for (int l = ch.l0; l < ch.l1; ++l) {
+            const int lp = lptr[l - ch.l0], off = lp - x0, cnt = lptr[l - ch.l0 + 1] - lp,
+                      ns = lns[l - ch.l0];
+            auto vat = [&](int k) { return lval[k]; };
+            auto yat = [&](int k) {
+                const int sc = lsrc[k];
+                return sc < 0 ? ywin[-sc - 1] : lyv[k];
+            };
+            if (tid < ns) {
+                const rsp::RowTask t = ltask[off + tid];
+                T s = fma_chain<T, B>(lx[off + tid], t.t0 - k0, t.t1 - k0, vat, yat);
+                if constexpr (KIND == 2) s = s / ldg[off + tid];
+                y[t.i] = s;
+                ywin[(lp + tid - base) & (rsp::kYWin - 1)] = s;
+            }
+            for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
+                const rsp::RowTask t = ltask[off + r];
+                T s = wave_chain<T>(lx[off + r], t.t0 - k0, t.t1 - k0, tid & 63, vat, yat);
+                if constexpr (KIND == 2) s = s / ldg[off + r];
+                if ((tid & 63) == 0) {
+                    y[t.i] = s;
+                    ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
+                }
+            }
+            lds_barrier();
+        }
+    };
+    // two register sets, A and B, alternate between even and odd chunks (no
+    // copies of pending loads); chunk indices past the run are clamped, so
+    // every prefetch is unconditional
+    const int cl = c1 - 1;
+    Plan pa = load_plan(a.plan.chunks[c0]), pb = load_plan(a.plan.chunks[min(c0 + 1, cl)]);
+    Vals va = load_vals(pa), vb;
+    for (int c = c0; c < c1; c += 2) {
+        const rsp::LevelChunk ca = a.plan.chunks[c];
+        stage(ca, pa, va);
+        vb = load_vals(pb);                            // chunk c+1's gathers
+        pa = load_plan(a.plan.chunks[min(c + 2, cl)]);  // chunk c+2's plan
+        levels(ca);
+        if (c + 1 >= c1) break;
+        const rsp::LevelChunk cb = a.plan.chunks[c + 1];
+        stage(cb, pb, vb);
+        va = load_vals(pa);
+        pb = load_plan(a.plan.chunks[min(c + 3, cl)]);
+        levels(cb);
+    }
+}
+
 // --------------------------------------------------------------- launchers
 
 template <typename T, int B>
@@ -377,6 +509,9 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             else if (sg.nth <= 256)
                 hipLaunchKernelGGL((trsv_thin<T, KIND, B, 256>), dim3(1), dim3(256), 0, s, a, alpha,
                                    sg.c0, sg.c1, base);
+            else if (a.thin_prefetch)
+                hipLaunchKernelGGL((trsv_thin_pf<T, KIND, B>), dim3(1), dim3(kThinThreads), 0, s, a,
+                                   alpha, sg.c0, sg.c1, base);
             else
                 hipLaunchKernelGGL((trsv_thin<T, KIND, B, kThinThreads>), dim3(1), dim3(kThinThreads),
                                    0, s, a, alpha, sg.c0, sg.c1, base);

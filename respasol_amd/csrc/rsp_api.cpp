@@ -903,7 +903,7 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
             const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
             if (sp.chunks.size() == (size_t)sg.c0 || crow + cnt > rsp::kChunkRows ||
                 cterm + lterms[(size_t)l] > rsp::kChunkTerms) {
-                sp.chunks.push_back({l, l + 1});
+                sp.chunks.push_back({l, l + 1, 0, 0, 0, 0, 0, 0});
                 crow = 0;
                 cterm = 0;
             } else {
@@ -929,7 +929,13 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
         sp.tpos.push_back(0);
         sp.src.push_back(0);
     }
-    if (sp.chunks.empty()) sp.chunks.push_back({0, 0});
+    for (rsp::LevelChunk &ch : sp.chunks) {  // slot and term ranges, read by the kernel up front
+        ch.x0 = ptr[(size_t)ch.l0];
+        ch.x1 = ptr[(size_t)ch.l1];
+        ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
+        ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
+    }
+    if (sp.chunks.empty()) sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
 }
 
 template <typename V>
@@ -1393,6 +1399,7 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.y = y;
     a.alpha = (t == RSP_R_64F) ? *(const double *)alpha : (double)*(const float *)alpha;
     a.plan = level_plan(f->L, f->L.segs, f->L.batch);
+    a.thin_prefetch = env_int("RSP_ILU_THIN_PF", 1) != 0;
     return a;
 }
 

@@ -123,8 +123,11 @@ struct LevelSeg {
 struct alignas(16) RowTask {
     int i, t0, t1, d;
 };
-struct alignas(8) LevelChunk {  // levels [l0, l1) of a thin solve run, staged in LDS together
+struct alignas(16) LevelChunk {  // levels [l0, l1) of a thin solve run, staged in LDS together
     int l0, l1;
+    int x0, x1;  // its level-order slots: ptr[l0], ptr[l1]
+    int k0, k1;  // its flat terms: tasks[x0].t0, tasks[x1 - 1].t1
+    int pad0, pad1;
 };
 
 struct LevelPlan {
@@ -145,9 +148,9 @@ struct LevelPlan {
     const int *nshort_host;
 };
 constexpr int kLongTerms = 64;       // solve rows with more terms are done by a whole wave
-constexpr int kYWin = 8192;          // LDS y window of a thin solve run (entries, power of 2)
+constexpr int kYWin = 4096;          // LDS y window of a thin solve run (entries, power of 2)
 constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin)
-constexpr int kChunkTerms = 2048;    // terms staged per thin-run chunk
+constexpr int kChunkTerms = 4096;    // terms staged per thin-run chunk
 constexpr int kThinThreads = 1024;   // workgroup of a thin segment
 constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels)
 constexpr int kThinSolveRows = 1024; // solve levels this small (and <= kChunkTerms terms) run thin
@@ -213,6 +216,7 @@ struct TrsvArgs {
     void *y;
     double alpha;
     LevelPlan plan;       // the DAG of the solve (L, L^T or U), with its flat terms
+    int thin_prefetch;    // 1024-thread thin runs: next chunk loaded under the current one
 };
 
 }  // namespace rsp
