@@ -404,9 +404,26 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T 
         }
         return v;
     };
-    auto stage = [&](const rsp::LevelChunk &ch, const Plan &p, const Vals &v) {
+    // Chunk switch. The levels write y to the LDS window only; the previous
+    // chunk's rows go to global y here, one store per thread, so no global
+    // store is pending while levels run and the wait below only ever finds
+    // operations issued a whole chunk ago (this chunk's prefetch, the flush
+    // before). After it and the barrier, every flush up to the previous switch
+    // is complete — the staged y a prefetch reads (producer > kYWin rows back,
+    // i.e. in a chunk flushed at least one switch before) is in memory.
+    auto mark = [&](int c, int j) {  // diagnostics only (RSP_ILU_TRACE)
+        if (a.trace && tid == 0 && 4 * c + j < a.trace_cap) a.trace[4 * c + j] = wall_clock64();
+    };
+    auto stage = [&](int c, int px0, int px1, const rsp::LevelChunk &ch, const Plan &p,
+                     const Vals &v) {
         const int nk = ch.k1 - ch.k0, nl = ch.l1 - ch.l0;
-        __syncthreads();  // the previous chunk's levels are done with LDS
+        mark(c, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();  // the previous chunk's levels are done with LDS
+        mark(c, 1);
+        const bool flush = tid < px1 - px0;
+        const int fi = ltask[tid].i;  // read before this thread restages its slot
+        const T fv = ywin[(px0 + tid - base) & (rsp::kYWin - 1)];
         if (tid < ch.x1 - ch.x0) {
             ltask[tid] = p.t;
             lx[tid] = alpha * v.xv;
@@ -422,7 +439,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T 
         if (tid <= nl) lptr[tid] = p.lp;
         if (tid < nl) lns[tid] = p.ln;
         if (tid == 0 && nl == NTH) lptr[NTH] = p.lpe;
-        __syncthreads();
+        if (flush) y[fi] = fv;  // after the last use of the prefetched registers
+        lds_barrier();
+        mark(c, 2);
     };
     auto levels = [&](const rsp::LevelChunk &ch) {
         const int x0 = ch.x0, k0 = ch.k0;
@@ -438,40 +457,68 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T 
                 const rsp::RowTask t = ltask[off + tid];
                 T s = fma_chain<T, B>(lx[off + tid], t.t0 - k0, t.t1 - k0, vat, yat);
                 if constexpr (KIND == 2) s = s / ldg[off + tid];
-                y[t.i] = s;
                 ywin[(lp + tid - base) & (rsp::kYWin - 1)] = s;
             }
             for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
                 const rsp::RowTask t = ltask[off + r];
                 T s = wave_chain<T>(lx[off + r], t.t0 - k0, t.t1 - k0, tid & 63, vat, yat);
                 if constexpr (KIND == 2) s = s / ldg[off + r];
-                if ((tid & 63) == 0) {
-                    y[t.i] = s;
-                    ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
-                }
+                if ((tid & 63) == 0) ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
             }
             lds_barrier();
+            if (a.trace && tid == 0 && l < a.trace_cap / 2)  // diagnostics: level end stamps
+                a.trace[a.trace_cap / 2 + l] = wall_clock64();
         }
     };
     // two register sets, A and B, alternate between even and odd chunks (no
     // copies of pending loads); chunk indices past the run are clamped, so
     // every prefetch is unconditional
     const int cl = c1 - 1;
-    Plan pa = load_plan(a.plan.chunks[c0]), pb = load_plan(a.plan.chunks[min(c0 + 1, cl)]);
+    // chunk records through the constant address space: scalar loads, which
+    // the y stores cannot alias and which leave vmcnt to the prefetch; each is
+    // fetched one chunk before its plan is
+    typedef const __attribute__((address_space(4))) int *ChunkPtr;
+    const ChunkPtr chunks = (ChunkPtr)a.plan.chunks;
+    auto chunk = [&](int c) {
+        const ChunkPtr q = chunks + (size_t)c * (sizeof(rsp::LevelChunk) / sizeof(int));
+        rsp::LevelChunk r;
+        r.l0 = q[0];
+        r.l1 = q[1];
+        r.x0 = q[2];
+        r.x1 = q[3];
+        r.k0 = q[4];
+        r.k1 = q[5];
+        return r;
+    };
+    rsp::LevelChunk ra = chunk(c0), rb = chunk(min(c0 + 1, cl)), rn = chunk(min(c0 + 2, cl));
+    Plan pa = load_plan(ra), pb = load_plan(rb);
     Vals va = load_vals(pa), vb;
+    int px0 = 0, px1 = 0;  // the chunk to flush at the next switch
     for (int c = c0; c < c1; c += 2) {
-        const rsp::LevelChunk ca = a.plan.chunks[c];
-        stage(ca, pa, va);
-        vb = load_vals(pb);                            // chunk c+1's gathers
-        pa = load_plan(a.plan.chunks[min(c + 2, cl)]);  // chunk c+2's plan
+        const rsp::LevelChunk ca = ra;
+        stage(c, px0, px1, ca, pa, va);
+        vb = load_vals(pb);  // chunk c+1's gathers
+        pa = load_plan(rn);  // chunk c+2's plan
+        ra = rn;
+        rn = chunk(min(c + 3, cl));
         levels(ca);
+        mark(c, 3);
+        px0 = ca.x0;
+        px1 = ca.x1;
         if (c + 1 >= c1) break;
-        const rsp::LevelChunk cb = a.plan.chunks[c + 1];
-        stage(cb, pb, vb);
-        va = load_vals(pa);
-        pb = load_plan(a.plan.chunks[min(c + 3, cl)]);
+        const rsp::LevelChunk cb = rb;
+        stage(c + 1, px0, px1, cb, pb, vb);
+        va = load_vals(pa);  // chunk c+2's gathers
+        pb = load_plan(rn);  // chunk c+3's plan
+        rb = rn;
+        rn = chunk(min(c + 4, cl));
         levels(cb);
+        mark(c + 1, 3);
+        px0 = cb.x0;
+        px1 = cb.x1;
     }
+    // the last chunk's rows (its levels ended with a barrier)
+    if (tid < px1 - px0) y[ltask[tid].i] = ywin[(px0 + tid - base) & (rsp::kYWin - 1)];
 }
 
 // --------------------------------------------------------------- launchers

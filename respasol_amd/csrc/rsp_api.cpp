@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 #include <limits.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1400,6 +1401,8 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.alpha = (t == RSP_R_64F) ? *(const double *)alpha : (double)*(const float *)alpha;
     a.plan = level_plan(f->L, f->L.segs, f->L.batch);
     a.thin_prefetch = env_int("RSP_ILU_THIN_PF", 1) != 0;
+    a.trace = nullptr;
+    a.trace_cap = 0;
     return a;
 }
 
@@ -1411,6 +1414,17 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
+    // diagnostics: RSP_ILU_TRACE=<file> appends per-chunk timestamps of the
+    // prefetching thin kernel (host-blocking; never set in timed runs)
+    const char *trace_file = getenv("RSP_ILU_TRACE");
+    static unsigned long long *d_trace = nullptr;
+    const int trace_cap = 4 << 20;
+    if (trace_file) {
+        if (!d_trace) RSP_CHECK_HIP(hipMalloc((void **)&d_trace, trace_cap * sizeof(unsigned long long)));
+        RSP_CHECK_HIP(hipMemsetAsync(d_trace, 0, trace_cap * sizeof(unsigned long long), h->stream));
+        a.trace = d_trace;
+        a.trace_cap = trace_cap;
+    }
     hipError_t e;
     const bool f64 = value_type == RSP_R_64F, ftz = h->ftz != 0;
     if (op == RSP_OPERATION_NON_TRANSPOSE) {
@@ -1422,6 +1436,23 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
                 : (ftz ? rsp_k_ftz::trsv_lower_t_f32(a, h->stream) : rsp_k::trsv_lower_t_f32(a, h->stream));
     } else {
         return RSP_STATUS_INVALID_VALUE;
+    }
+    if (trace_file && e == hipSuccess) {
+        std::vector<unsigned long long> t(trace_cap);
+        RSP_CHECK_HIP(hipMemcpyAsync(t.data(), d_trace, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost,
+                                     h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+        if (FILE *fp = fopen(trace_file, "a")) {
+            fprintf(fp, "# solve op=%d n=%d\n", (int)op, f->n);
+            for (int l = 0; l < trace_cap / 2; l++)
+                if (t[(size_t)trace_cap / 2 + l])
+                    fprintf(fp, "L %d %llu\n", l, t[(size_t)trace_cap / 2 + l]);
+            for (int c = 0; c < trace_cap / 8; c++)
+                if (t[4 * (size_t)c] || t[4 * (size_t)c + 3])
+                    fprintf(fp, "%d %llu %llu %llu %llu\n", c, t[4 * (size_t)c], t[4 * (size_t)c + 1],
+                            t[4 * (size_t)c + 2], t[4 * (size_t)c + 3]);
+            fclose(fp);
+        }
     }
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
 }

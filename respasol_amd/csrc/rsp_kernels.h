@@ -217,6 +217,8 @@ struct TrsvArgs {
     double alpha;
     LevelPlan plan;       // the DAG of the solve (L, L^T or U), with its flat terms
     int thin_prefetch;    // 1024-thread thin runs: next chunk loaded under the current one
+    unsigned long long *trace;  // diagnostics (RSP_ILU_TRACE): 4 timestamps per chunk, or null
+    int trace_cap;
 };
 
 }  // namespace rsp
