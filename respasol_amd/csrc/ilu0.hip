@@ -269,140 +269,138 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, T alpha, int off, 
     y[t.i] = s;
 }
 
-// Thin run (levels [lb, le) cut into chunks [c0, c1)), one 1024-thread
-// workgroup. Per chunk: a full barrier (every earlier y store visible), then
-// the chunk's tasks, x_i, u_ii, term values and — for terms whose y was
-// produced before the chunk and has left the LDS window — those y values are
-// staged in LDS by all threads at once (one memory round trip per chunk);
-// then the chunk's levels run on LDS alone: thread r computes row r of the
-// level, reading each y from the LDS window (src < 0: produced earlier in the
-// run, slot = run index mod kYWin) or from the staged copy, writes y to
-// global memory and to its window slot, and an LDS-only barrier separates
-// the levels. Same operation order as trsv_level.
-template <typename T, int KIND, int B, int NTH>
-__global__ __launch_bounds__(NTH) void trsv_thin(TrsvArgs a, T alpha, int c0, int c1, int base) {
-    __shared__ T ywin[rsp::kYWin];
-    __shared__ T lval[rsp::kChunkTerms], lyv[rsp::kChunkTerms];
-    __shared__ int lsrc[rsp::kChunkTerms];
-    __shared__ rsp::RowTask ltask[rsp::kChunkRows];
-    __shared__ T lx[rsp::kChunkRows], ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
-    __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];  // a chunk has <= kChunkRows levels
-    const int tid = threadIdx.x;
-    const T *vals = (const T *)a.vals, *x = (const T *)a.x;
-    T *y = (T *)a.y;
-    const int *ptr = a.plan.ptr_dev;
-    for (int c = c0; c < c1; ++c) {
-        const rsp::LevelChunk ch = a.plan.chunks[c];
-        const int x0 = ch.x0, x1 = ch.x1, k0 = ch.k0, k1 = ch.k1;
-        __syncthreads();  // the previous chunk's y stores are visible, LDS is free
-        for (int r = tid; r < x1 - x0; r += NTH) {
-            const rsp::RowTask t = a.plan.tasks[x0 + r];
-            ltask[r] = t;
-            lx[r] = alpha * x[t.i];
-            if constexpr (KIND == 2) ldg[r] = t.d >= 0 ? vals[t.d] : T(0);
-        }
-        for (int k = tid; k < k1 - k0; k += NTH) {
-            const int sc = a.plan.src[k0 + k];
-            lsrc[k] = sc;
-            lval[k] = vals[a.plan.tpos[k0 + k]];
-            lyv[k] = sc >= 0 ? y[sc] : T(0);
-        }
-        for (int q = tid; q <= ch.l1 - ch.l0; q += NTH) {
-            lptr[q] = ptr[ch.l0 + q];
-            if (q < ch.l1 - ch.l0) lns[q] = a.plan.nshort[ch.l0 + q];
-        }
-        __syncthreads();
-        for (int l = ch.l0; l < ch.l1; ++l) {
-            const int lp = lptr[l - ch.l0], off = lp - x0, cnt = lptr[l - ch.l0 + 1] - lp,
-                      ns = lns[l - ch.l0];
-            auto vat = [&](int k) { return lval[k]; };
-            auto yat = [&](int k) {
-                const int sc = lsrc[k];
-                return sc < 0 ? ywin[-sc - 1] : lyv[k];
-            };
-            for (int r = tid; r < ns; r += NTH) {
-                const rsp::RowTask t = ltask[off + r];
-                T s = fma_chain<T, B>(lx[off + r], t.t0 - k0, t.t1 - k0, vat, yat);
-                if constexpr (KIND == 2) s = s / ldg[off + r];
-                y[t.i] = s;
-                ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
-            }
-            for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
-                const rsp::RowTask t = ltask[off + r];
-                T s = wave_chain<T>(lx[off + r], t.t0 - k0, t.t1 - k0, tid & 63, vat, yat);
-                if constexpr (KIND == 2) s = s / ldg[off + r];
-                if ((tid & 63) == 0) {
-                    y[t.i] = s;
-                    ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
-                }
-            }
-            lds_barrier();
-        }
+// Thin run (levels cut into LDS-staged chunks [c0, c1)), one 1024-thread
+// workgroup. A chunk holds <= kChunkRows rows and <= kChunkTerms term slots;
+// every row of a thin run has its terms padded to whole groups of G = 4 (or 2,
+// for DAGs of short chains)
+// (pads: a zero value times the zero slot of the y buffer, an exact no-op), so
+// a row is read as groups of four terms with vector LDS loads and no length
+// tests. LDS per chunk:
+//   lrow[r]  = {alpha x_i, first group | groups << 16, y slot}  (one 16-B load)
+//   lval[k], lidx[k] = term value, byte offset of its y in ybuf (row order)
+//   ybuf     = [ y window (kYWin slots, run index mod kYWin) | 0 | y staged
+//               for slot k at kYWin + 1 + k (producers before the run or
+//               already out of the window) ]
+// The chunk's data reaches LDS through registers, two chunks deep: while chunk
+// c's levels run, the plan loads of chunk c+2 (task, term positions and
+// sources, level offsets: one row and four slots per thread) and the gathers
+// of chunk c+1 (x_i, term values, staged y) are in flight, unpredicated with
+// clamped indices, so nothing waits on them before the switch; y is written to
+// global memory only at chunk switches (one store per thread), so no store is
+// pending under the levels. A staged y has its producer > kYWin rows back —
+// at least two switches earlier — so it is in memory when prefetched.
+//
+// Levels: a narrow level (<= 64 rows, all short) is computed by wave 0 alone,
+// and consecutive narrow levels are ordered by the wave's in-order LDS
+// accesses instead of workgroup barriers; the wave runs them software-
+// pipelined — while level q's y loads, fma chain and y store are on the
+// critical path, the first term group of level q+1 and the row records of
+// level q+2 are already loading — so a level costs about one LDS round trip.
+// The other waves skip to the barrier after the run. (Deep-level circuits are
+// ~10^4 levels of ~10 rows: nearly every level is narrow.) Wider levels use
+// all waves, one row per thread, long rows (> kLongTerms terms) a wave each,
+// and an LDS-only barrier after each level.
+template <typename T>
+struct alignas(16) ThinRow {  // LDS row record of a thin chunk
+    T x;                      // alpha * x_i
+    int g;                    // first group (chunk-relative) | groups << 16
+    int out;                  // byte offset of the row's y window slot in ybuf
+};
+template <typename T, int G>
+struct alignas(sizeof(T) * G) TermGroup {  // values of one group of terms
+    T v[G];
+};
+template <int G>
+struct alignas(4 * G) TermIds {  // byte offsets of their y in ybuf
+    int v[G];
+};
+
+// Solve streams, one pass over the DAG before its thin runs: per flat term
+// its value (0 for a pad), per level-order slot alpha x_i (and u_ii for the U
+// solve) — so a thin run stages contiguous streams instead of gathering.
+template <typename T, int KIND>
+__global__ __launch_bounds__(256) void trsv_stream(TrsvArgs a, T alpha) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const T *vals = (const T *)a.vals;
+    if (k < a.plan.nterms) {
+        const int tp = a.plan.tpos[k];
+        ((T *)a.sval)[k] = tp >= 0 ? vals[tp] : T(0);
+    }
+    if (k < a.n) {
+        const rsp::RowTask t = a.plan.tasks[k];
+        ((T *)a.sx)[k] = alpha * ((const T *)a.x)[t.i];
+        if constexpr (KIND == 2) ((T *)a.sdg)[k] = t.d >= 0 ? vals[t.d] : T(0);
     }
 }
 
-// Prefetching form of trsv_thin for 1024-thread runs. A chunk holds <= 1024
-// rows and <= 2048 terms: one row and two terms per thread. Its staging data
-// comes in two dependent loads — the plan (task, sources, term positions,
-// level offsets), then the gathers that need it (alpha*x_i, u_ii, term
-// values, staged y) — so the prefetch is two chunks deep: while chunk c's
-// levels run on LDS, the gathers of chunk c+1 (whose plan arrived during
-// chunk c-1) and the plan of chunk c+2 are in flight, and a chunk switch
-// costs two barriers and LDS writes instead of a chain of global round
-// trips. Every prefetch load is unpredicated (indices clamped into range,
-// unused values never stored), so nothing waits for them before the next
-// chunk switch. A term that stages y (src >= 0) has its producer > kYWin
-// rows before its level ends, i.e. before chunk c began (chunks have
-// <= kChunkRows << kYWin rows): that y is final, and its store is visible
-// since chunk c's first barrier.
-template <typename T, int KIND, int B>
-__global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T alpha, int c0,
-                                                                  int c1, int base) {
+template <typename T, int KIND, int G>
+__global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, int c0, int c1, int base) {
     constexpr int NTH = rsp::kThinThreads;
-    constexpr int TPT = (rsp::kChunkTerms + NTH - 1) / NTH;  // terms of a chunk per thread
+    constexpr int TPT = rsp::kChunkTerms / NTH;  // terms of a chunk per thread: tid + j NTH
+    static_assert(TPT * NTH == rsp::kChunkTerms && G <= rsp::kGroup, "chunk terms per thread");
     static_assert(rsp::kChunkRows <= NTH, "one row of a chunk per thread");
-    __shared__ T ywin[rsp::kYWin];
-    __shared__ T lval[rsp::kChunkTerms], lyv[rsp::kChunkTerms];
-    __shared__ int lsrc[rsp::kChunkTerms];
-    __shared__ rsp::RowTask ltask[rsp::kChunkRows];
-    __shared__ T lx[rsp::kChunkRows], ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
+    constexpr int kZero = rsp::kYWin, kStaged = rsp::kYWin + 1;
+    __shared__ T ybuf[rsp::kYWin + 1 + rsp::kChunkTerms];
+    __shared__ TermGroup<T, G> lval[rsp::kChunkTerms / G];
+    __shared__ TermIds<G> lidx[rsp::kChunkTerms / G];
+    __shared__ ThinRow<T> lrow[rsp::kChunkRows];
+    __shared__ int lrowi[rsp::kChunkRows];
+    __shared__ T ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
     __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];
     const int tid = threadIdx.x;
-    const T *vals = (const T *)a.vals, *x = (const T *)a.x;
+    const T *sval = (const T *)a.sval, *sx = (const T *)a.sx, *sdg = (const T *)a.sdg;
     T *y = (T *)a.y;
     const int *ptr = a.plan.ptr_dev;
-    struct Plan {  // this thread's share of a chunk's plan
-        rsp::RowTask t;
-        int sc[TPT], tp[TPT];
+    if (tid == 0) ybuf[kZero] = T(0);
+    struct Pre {  // this thread's share of a chunk: row tid, terms tid + j NTH (all streams)
+        rsp::ThinRowPlan r;
+        T xv, dg, v[TPT];
+        int id[TPT];
         int lp, ln, lpe;
     };
-    struct Vals {  // ... and of its gathers
-        T xv, dg, v[TPT], y[TPT];
+    struct Stg {  // staged terms tid + j NTH of a chunk
+        int slot[TPT], j[TPT];
     };
-    auto load_plan = [&](const rsp::LevelChunk ch) {
-        Plan p;
-        const int kl = max(ch.k1 - 1, 0), nl = ch.l1 - ch.l0;
-        p.t = a.plan.tasks[min(ch.x0 + tid, max(ch.x1 - 1, 0))];
+    struct StgY {  // ... and their y
+        int slot[TPT];
+        T y[TPT];
+    };
+    auto load_pre = [&](const rsp::LevelChunk &ch) {
+        Pre p;
+        const int x = min(ch.x0 + tid, max(ch.x1 - 1, 0)), kl = max(ch.k1 - 1, 0), nl = ch.l1 - ch.l0;
+        p.r = a.plan.trow[x];
+        p.xv = sx[x];
+        p.dg = KIND == 2 ? sdg[x] : T(0);
 #pragma unroll
         for (int j = 0; j < TPT; ++j) {
-            p.sc[j] = a.plan.src[min(ch.k0 + tid + j * NTH, kl)];
-            p.tp[j] = a.plan.tpos[min(ch.k0 + tid + j * NTH, kl)];
+            const int k = min(ch.k0 + tid + j * NTH, kl);
+            p.v[j] = sval[k];
+            p.id[j] = a.plan.sid[k];
         }
         p.lp = ptr[ch.l0 + min(tid, nl)];
         p.ln = a.plan.nshort[ch.l0 + min(tid, max(nl - 1, 0))];
         p.lpe = ptr[ch.l1];
         return p;
     };
-    auto load_vals = [&](const Plan &p) {
-        Vals v;
-        v.xv = x[p.t.i];  // alpha applied when staged: no arithmetic on a pending load
-        v.dg = KIND == 2 ? vals[max(p.t.d, 0)] : T(0);
+    auto load_stg = [&](const rsp::LevelChunk &ch) {
+        Stg q;
+        const int el = max(ch.st1 - 1, 0);
 #pragma unroll
         for (int j = 0; j < TPT; ++j) {
-            v.v[j] = vals[p.tp[j]];
-            v.y[j] = y[max(p.sc[j], 0)];
+            const rsp::StagedTerm t = a.plan.stg[max(min(ch.st0 + tid + j * NTH, el), 0)];
+            q.slot[j] = t.slot;
+            q.j[j] = t.j;
         }
-        return v;
+        return q;
+    };
+    auto load_stgy = [&](const Stg &q) {
+        StgY w;
+#pragma unroll
+        for (int j = 0; j < TPT; ++j) {
+            w.slot[j] = q.slot[j];
+            w.y[j] = y[q.j[j]];
+        }
+        return w;
     };
     // Chunk switch. The levels write y to the LDS window only; the previous
     // chunk's rows go to global y here, one store per thread, so no global
@@ -411,31 +409,37 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T 
     // before). After it and the barrier, every flush up to the previous switch
     // is complete — the staged y a prefetch reads (producer > kYWin rows back,
     // i.e. in a chunk flushed at least one switch before) is in memory.
-    auto mark = [&](int c, int j) {  // diagnostics only (RSP_ILU_TRACE)
-        if (a.trace && tid == 0 && 4 * c + j < a.trace_cap) a.trace[4 * c + j] = wall_clock64();
+    auto mark_by = [&](int c, int j, int t) {  // diagnostics only (RSP_ILU_TRACE)
+        if (a.trace && tid == t && 8 * c + j < a.trace_cap / 2) a.trace[8 * c + j] = wall_clock64();
     };
-    auto stage = [&](int c, int px0, int px1, const rsp::LevelChunk &ch, const Plan &p,
-                     const Vals &v) {
-        const int nk = ch.k1 - ch.k0, nl = ch.l1 - ch.l0;
+    auto mark = [&](int c, int j) { mark_by(c, j, 0); };
+    auto stage = [&](int c, int px0, int px1, const rsp::LevelChunk &ch, const Pre &p, const StgY &w) {
+        const int nk = ch.k1 - ch.k0, nl = ch.l1 - ch.l0, ns = ch.st1 - ch.st0;
         mark(c, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();  // the previous chunk's levels are done with LDS
         mark(c, 1);
         const bool flush = tid < px1 - px0;
-        const int fi = ltask[tid].i;  // read before this thread restages its slot
-        const T fv = ywin[(px0 + tid - base) & (rsp::kYWin - 1)];
+        const int fi = lrowi[tid];  // read before this thread restages its slot
+        const T fv = ybuf[(px0 + tid - base) & (rsp::kYWin - 1)];
         if (tid < ch.x1 - ch.x0) {
-            ltask[tid] = p.t;
-            lx[tid] = alpha * v.xv;
-            if constexpr (KIND == 2) ldg[tid] = p.t.d >= 0 ? v.dg : T(0);
+            ThinRow<T> r;
+            r.x = p.xv;
+            r.g = p.r.g;
+            r.out = p.r.out * (int)sizeof(T);
+            lrow[tid] = r;
+            lrowi[tid] = p.r.i;
+            if constexpr (KIND == 2) ldg[tid] = p.dg;
         }
 #pragma unroll
         for (int j = 0; j < TPT; ++j)
             if (tid + j * NTH < nk) {
-                lsrc[tid + j * NTH] = p.sc[j];
-                lval[tid + j * NTH] = v.v[j];
-                lyv[tid + j * NTH] = p.sc[j] >= 0 ? v.y[j] : T(0);
+                ((T *)lval)[tid + j * NTH] = p.v[j];
+                ((int *)lidx)[tid + j * NTH] = p.id[j] * (int)sizeof(T);
             }
+#pragma unroll
+        for (int j = 0; j < TPT; ++j)
+            if (tid + j * NTH < ns) ybuf[kStaged + w.slot[j]] = w.y[j];
         if (tid <= nl) lptr[tid] = p.lp;
         if (tid < nl) lns[tid] = p.ln;
         if (tid == 0 && nl == NTH) lptr[NTH] = p.lpe;
@@ -443,40 +447,125 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T 
         lds_barrier();
         mark(c, 2);
     };
+    // s += -sum over the terms of one group (in order; pads are exact no-ops)
+    auto yb = [&](int off) { return *(const T *)((const char *)ybuf + off); };
+    auto put = [&](int off, T v) { *(T *)((char *)ybuf + off) = v; };
+    auto group_fma = [&](T s, const TermGroup<T, G> &g, const TermIds<G> &id) {
+        T yv[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) yv[j] = yb(id.v[j]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) s = __builtin_fma(-g.v[j], yv[j], s);
+        return s;
+    };
+    auto row_value = [&](const ThinRow<T> &r) {  // one short row, groups in order
+        T s = r.x;
+        const int g0 = r.g & 0xffff, ng = r.g >> 16;
+        for (int g = 0; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+        return s;
+    };
+    auto narrow = [&](int q) {
+        const int cnt = lptr[q + 1] - lptr[q];
+        return cnt <= 64 && lns[q] == cnt;
+    };
+    auto run_end = [&](int q, int nl) {  // first level >= q that is not narrow, or nl
+        for (int b = q;; b += 64) {
+            const int qq = b + (tid & 63);
+            const unsigned long long m = __ballot(!(qq < nl && narrow(qq)));
+            if (m) return b + __builtin_ctzll(m);
+        }
+    };
+    // A lane past a narrow level's last row reads that last row's record (its
+    // index is clamped) and so computes the same value into the same slot: no
+    // store predicate.
+    auto narrow_run = [&](const rsp::LevelChunk &ch, int q0, int q1) {  // wave 0
+        const int lane = tid, x0 = ch.x0, nl = ch.l1 - ch.l0;
+        auto lpt = [&](int q) { return lptr[min(q, nl)]; };
+        auto ld_row = [&](int p0, int p1) { return max(p0 - x0 + min(lane, p1 - p0 - 1), 0); };
+        // level pointers p1..p3 = lptr[q+1 .. q+3] (clamped), rolling
+        int p1 = lpt(q0 + 1), p2 = lpt(q0 + 2), p3 = lpt(q0 + 3);
+        int cr = ld_row(lpt(q0), p1);
+        ThinRow<T> cR = lrow[cr];
+        TermGroup<T, G> cV = lval[cR.g & 0xffff];
+        TermIds<G> cI = lidx[cR.g & 0xffff];
+        int nr = ld_row(p1, p2);
+        ThinRow<T> nR = lrow[nr];
+        for (int q = q0; q < q1; ++q) {
+            // loads for later levels: none of them depends on a y
+            const int p4 = lpt(q + 4);
+            TermGroup<T, G> nV = cV;
+            TermIds<G> nI = cI;
+            ThinRow<T> mR = nR;
+            int mr = nr;
+            if (q + 1 < q1) {
+                nV = lval[nR.g & 0xffff];
+                nI = lidx[nR.g & 0xffff];
+            }
+            if (q + 2 < q1) {
+                mr = ld_row(p2, p3);
+                mR = lrow[mr];
+            }
+            // level q: y loads -> fma chain -> y store (the critical path)
+            T s = group_fma(cR.x, cV, cI);
+            if (cR.g >= 2 << 16) {  // more than one group
+                const int g0 = cR.g & 0xffff, ng = cR.g >> 16;
+                for (int g = 1; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+            }
+            if constexpr (KIND == 2) s = s / ldg[cr];
+            put(cR.out, s);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            if (a.trace) {  // diagnostics: level end stamps
+                if (lane == 0 && ch.l0 + q < a.trace_cap / 2)
+                    a.trace[a.trace_cap / 2 + ch.l0 + q] = a.trace_clk ? clock64() : wall_clock64();
+            }
+            cR = nR;
+            cr = nr;
+            cV = nV;
+            cI = nI;
+            nR = mR;
+            nr = mr;
+            p1 = p2;
+            p2 = p3;
+            p3 = p4;
+        }
+    };
     auto levels = [&](const rsp::LevelChunk &ch) {
-        const int x0 = ch.x0, k0 = ch.k0;
-        for (int l = ch.l0; l < ch.l1; ++l) {
-            const int lp = lptr[l - ch.l0], off = lp - x0, cnt = lptr[l - ch.l0 + 1] - lp,
-                      ns = lns[l - ch.l0];
-            auto vat = [&](int k) { return lval[k]; };
-            auto yat = [&](int k) {
-                const int sc = lsrc[k];
-                return sc < 0 ? ywin[-sc - 1] : lyv[k];
-            };
+        const int x0 = ch.x0, nl = ch.l1 - ch.l0;
+        auto vat = [&](int k) { return lval[k / G].v[k % G]; };
+        auto yat = [&](int k) { return yb(lidx[k / G].v[k % G]); };
+        for (int q = 0; q < nl;) {
+            if (narrow(q)) {
+                const int qe = run_end(q, nl);
+                if (tid < 64) narrow_run(ch, q, qe);
+                lds_barrier();
+                q = qe;
+                continue;
+            }
+            const int l = ch.l0 + q;
+            const int lp = lptr[q], off = lp - x0, cnt = lptr[q + 1] - lp, ns = lns[q];
             if (tid < ns) {
-                const rsp::RowTask t = ltask[off + tid];
-                T s = fma_chain<T, B>(lx[off + tid], t.t0 - k0, t.t1 - k0, vat, yat);
+                const ThinRow<T> r = lrow[off + tid];
+                T s = row_value(r);
                 if constexpr (KIND == 2) s = s / ldg[off + tid];
-                ywin[(lp + tid - base) & (rsp::kYWin - 1)] = s;
+                put(r.out, s);
             }
             for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
-                const rsp::RowTask t = ltask[off + r];
-                T s = wave_chain<T>(lx[off + r], t.t0 - k0, t.t1 - k0, tid & 63, vat, yat);
+                const ThinRow<T> t = lrow[off + r];
+                const int k0 = G * (t.g & 0xffff);
+                T s = wave_chain<T>(t.x, k0, k0 + G * (t.g >> 16), tid & 63, vat, yat);
                 if constexpr (KIND == 2) s = s / ldg[off + r];
-                if ((tid & 63) == 0) ywin[(lp + r - base) & (rsp::kYWin - 1)] = s;
+                if ((tid & 63) == 0) put(t.out, s);
             }
             lds_barrier();
             if (a.trace && tid == 0 && l < a.trace_cap / 2)  // diagnostics: level end stamps
-                a.trace[a.trace_cap / 2 + l] = wall_clock64();
+                a.trace[a.trace_cap / 2 + l] = a.trace_clk ? clock64() : wall_clock64();
+            ++q;
         }
     };
-    // two register sets, A and B, alternate between even and odd chunks (no
-    // copies of pending loads); chunk indices past the run are clamped, so
-    // every prefetch is unconditional
-    const int cl = c1 - 1;
     // chunk records through the constant address space: scalar loads, which
-    // the y stores cannot alias and which leave vmcnt to the prefetch; each is
-    // fetched one chunk before its plan is
+    // the y stores cannot alias and which leave vmcnt to the prefetch
     typedef const __attribute__((address_space(4))) int *ChunkPtr;
     const ChunkPtr chunks = (ChunkPtr)a.plan.chunks;
     auto chunk = [&](int c) {
@@ -488,37 +577,40 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, T 
         r.x1 = q[3];
         r.k0 = q[4];
         r.k1 = q[5];
+        r.st0 = q[6];
+        r.st1 = q[7];
         return r;
     };
-    rsp::LevelChunk ra = chunk(c0), rb = chunk(min(c0 + 1, cl)), rn = chunk(min(c0 + 2, cl));
-    Plan pa = load_plan(ra), pb = load_plan(rb);
-    Vals va = load_vals(pa), vb;
+    // Pipeline: while chunk c's levels run, the streams of chunk c+1 and the y
+    // of its staged terms (their list loaded one chunk earlier) are loading,
+    // and the staged-term list of chunk c+2. Streams have no dependent loads,
+    // so one chunk of lead hides them.
+    const int cl = c1 - 1;
+    rsp::LevelChunk rc = chunk(c0), rn = chunk(min(c0 + 1, cl));
+    Pre p = load_pre(rc);
+    StgY w = load_stgy(load_stg(rc));
+    Stg sn = load_stg(rn);
     int px0 = 0, px1 = 0;  // the chunk to flush at the next switch
-    for (int c = c0; c < c1; c += 2) {
-        const rsp::LevelChunk ca = ra;
-        stage(c, px0, px1, ca, pa, va);
-        vb = load_vals(pb);  // chunk c+1's gathers
-        pa = load_plan(rn);  // chunk c+2's plan
-        ra = rn;
-        rn = chunk(min(c + 3, cl));
-        levels(ca);
+    for (int c = c0; c < c1; ++c) {
+        stage(c, px0, px1, rc, p, w);
+        const rsp::LevelChunk cur = rc;
+        if (c + 1 < c1) {
+            const rsp::LevelChunk r2 = chunk(min(c + 2, cl));
+            p = load_pre(rn);     // chunk c+1's streams
+            w = load_stgy(sn);    // ... and its staged y
+            if (r2.st1 > r2.st0) sn = load_stg(r2);  // chunk c+2's staged terms
+            rc = rn;
+            rn = r2;
+        }
+        mark_by(c, 4, 0);  // diagnostics: prefetch issued (wave 0 / last wave)
+        mark_by(c, 5, NTH - 64);
+        levels(cur);
         mark(c, 3);
-        px0 = ca.x0;
-        px1 = ca.x1;
-        if (c + 1 >= c1) break;
-        const rsp::LevelChunk cb = rb;
-        stage(c + 1, px0, px1, cb, pb, vb);
-        va = load_vals(pa);  // chunk c+2's gathers
-        pb = load_plan(rn);  // chunk c+3's plan
-        rb = rn;
-        rn = chunk(min(c + 4, cl));
-        levels(cb);
-        mark(c + 1, 3);
-        px0 = cb.x0;
-        px1 = cb.x1;
+        px0 = cur.x0;
+        px1 = cur.x1;
     }
     // the last chunk's rows (its levels ended with a barrier)
-    if (tid < px1 - px0) y[ltask[tid].i] = ywin[(px0 + tid - base) & (rsp::kYWin - 1)];
+    if (tid < px1 - px0) y[lrowi[tid]] = ybuf[(px0 + tid - base) & (rsp::kYWin - 1)];
 }
 
 // --------------------------------------------------------------- launchers
@@ -546,22 +638,22 @@ template <typename T, int KIND, int B>
 static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
     const LevelPlan &P = a.plan;
     const T alpha = (T)a.alpha;
+    bool any_thin = false;
+    for (int g = 0; g < P.nseg; ++g) any_thin |= P.segs[g].thin != 0;
+    if (any_thin) {  // the streams the thin runs stage
+        const int nk = max(P.nterms, a.n);
+        hipLaunchKernelGGL((trsv_stream<T, KIND>), dim3((nk + 255) / 256), dim3(256), 0, s, a, alpha);
+    }
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
-            const int base = P.ptr_host[sg.lb];
-            if (sg.nth <= 64)
-                hipLaunchKernelGGL((trsv_thin<T, KIND, B, 64>), dim3(1), dim3(64), 0, s, a, alpha,
-                                   sg.c0, sg.c1, base);
-            else if (sg.nth <= 256)
-                hipLaunchKernelGGL((trsv_thin<T, KIND, B, 256>), dim3(1), dim3(256), 0, s, a, alpha,
-                                   sg.c0, sg.c1, base);
-            else if (a.thin_prefetch)
-                hipLaunchKernelGGL((trsv_thin_pf<T, KIND, B>), dim3(1), dim3(kThinThreads), 0, s, a,
-                                   alpha, sg.c0, sg.c1, base);
+            // term groups of 2 for DAGs of short chains (the plan padded them so)
+            if (P.group == 2)
+                hipLaunchKernelGGL((trsv_thin_pf<T, KIND, 2>), dim3(1), dim3(kThinThreads), 0, s, a,
+                                   sg.c0, sg.c1, P.ptr_host[sg.lb]);
             else
-                hipLaunchKernelGGL((trsv_thin<T, KIND, B, kThinThreads>), dim3(1), dim3(kThinThreads),
-                                   0, s, a, alpha, sg.c0, sg.c1, base);
+                hipLaunchKernelGGL((trsv_thin_pf<T, KIND, 4>), dim3(1), dim3(kThinThreads), 0, s, a,
+                                   sg.c0, sg.c1, P.ptr_host[sg.lb]);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

@@ -67,12 +67,18 @@ struct rsp_ilu0_info {
         rsp::RowTask *d_tasks = nullptr;       // solve: task per level-order slot
         int *d_tpos = nullptr, *d_src = nullptr;  // solve: flat terms
         rsp::LevelChunk *d_chunks = nullptr;   // solve: LDS-staged chunks of thin runs
+        rsp::ThinRowPlan *d_trow = nullptr;    // solve: thin-run row records
+        int *d_sid = nullptr;                  // solve: thin-run y indices per term
+        rsp::StagedTerm *d_stg = nullptr;      // solve: thin-run staged terms
+        int nterms = 0;                        // solve: flat terms
         int *d_nshort = nullptr;               // solve: short rows per level (device)
         std::vector<int> nshort;               // (host)
         std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
         int batch = 8;                         // solve fma-chain batch
+        int group = 4;                         // thin-run term groups (2 or 4)
     } L, LT, U;
     std::vector<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
+    void *d_sval = nullptr, *d_sx = nullptr, *d_sdg = nullptr;  // solve streams (trsv_stream)
     rsp::FacChunk *d_fchunks = nullptr;        // LDS-staged factor chunks (thin runs)
     rsp::FacRow *d_frows = nullptr;
     int *d_fpos = nullptr, *d_fu0 = nullptr, *d_fsend = nullptr, *d_fd = nullptr;
@@ -745,6 +751,10 @@ static void ilu_free_device(rsp_ilu0_info *f) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
+    for (void **p : {&f->d_sval, &f->d_sx, &f->d_sdg}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
     for (void **p : {(void **)&f->d_fchunks, (void **)&f->d_frows, (void **)&f->d_fpos,
                      (void **)&f->d_fu0, (void **)&f->d_fsend, (void **)&f->d_fd, (void **)&f->d_fpl,
                      (void **)&f->d_fpu}) {
@@ -753,7 +763,8 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     }
     for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) {
         for (void **p : {(void **)&d->d_tasks, (void **)&d->d_tpos, (void **)&d->d_src,
-                         (void **)&d->d_chunks, (void **)&d->d_nshort}) {
+                         (void **)&d->d_chunks, (void **)&d->d_nshort, (void **)&d->d_trow,
+                         (void **)&d->d_sid, (void **)&d->d_stg}) {
             if (*p) (void)hipFree(*p);
             *p = nullptr;
         }
@@ -834,13 +845,16 @@ struct SolvePlan {
     std::vector<int> tpos, src;
     std::vector<rsp::LevelSeg> segs;
     std::vector<rsp::LevelChunk> chunks;
+    std::vector<rsp::ThinRowPlan> trow;
+    std::vector<int> sid;
+    std::vector<rsp::StagedTerm> stg;
 };
 
 // row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
 template <typename RowTerms>
 static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
-                             int thin_rows, const std::vector<int> &diag, RowTerms row_terms,
-                             SolvePlan &sp) {
+                             int thin_rows, int group, const std::vector<int> &diag,
+                             RowTerms row_terms, SolvePlan &sp) {
     const int nlev = (int)ptr.size() - 1;
     // within each level: rows of <= kLongTerms terms first (a thread each),
     // longer rows after them (a wave each)
@@ -855,43 +869,63 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
         });
         sp.nshort[(size_t)l] = (int)(mid - b);
     }
-    std::vector<int> col;
-    sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
-    sp.tpos.clear();
-    for (size_t x = 0; x < order.size(); x++) {
-        const int i = order[x];
-        rsp::RowTask &t = sp.tasks[x];
-        t.i = i;
-        t.t0 = (int)sp.tpos.size();
-        row_terms(i, [&](int tp, int c) {
-            sp.tpos.push_back(tp);
-            col.push_back(c);
-        });
-        t.t1 = (int)sp.tpos.size();
-        t.d = diag.empty() ? -1 : diag[(size_t)i];
-    }
-    sp.src = col;
-    // segments: runs of thin levels / fat levels
-    std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
+    // segments: runs of thin levels / fat levels. A thin level's rows have
+    // their terms padded to whole groups of `group` (at least one group):
+    // pads are (position -1, source kPadSrc), i.e. a zero value times the zero
+    // slot of the LDS y buffer — an exact no-op fma — so the thin kernel reads
+    // a row as whole groups with vector loads and no length tests.
+    auto nterms = [&](int i) {
+        int cnt = 0;
+        row_terms(i, [&](int, int) { cnt++; });
+        return cnt;
+    };
+    auto padded = [&](int cnt) { return std::max(1, (cnt + group - 1) / group) * group; };
+    std::vector<int> lpad((size_t)std::max(nlev, 1), 0);
     for (int l = 0; l < nlev; l++)
-        if (ptr[(size_t)l + 1] > ptr[(size_t)l])
-            lterms[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l + 1] - 1].t1 - sp.tasks[(size_t)ptr[(size_t)l]].t0;
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) lpad[(size_t)l] += padded(nterms(order[(size_t)x]));
     sp.segs.clear();
     for (int l = 0; l < nlev; l++) {
         const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
         const int thin = (cnt <= thin_rows && cnt <= rsp::kThinThreads && cnt <= rsp::kChunkRows &&
-                          lterms[(size_t)l] <= rsp::kChunkTerms) ? 1 : 0;
+                          lpad[(size_t)l] <= rsp::kChunkTerms) ? 1 : 0;
         if (!sp.segs.empty() && sp.segs.back().thin == thin && sp.segs.back().le == l)
             sp.segs.back().le = l + 1;
         else
             sp.segs.push_back({l, l + 1, thin, 0, 0, 0});
     }
-    // workgroup of a thin run: 1024 threads (the chunk staging is spread over
-    // all of them; 64 / 256-thread runs measured 27 % / 35 % slower on the
-    // moderate set). RSP_ILU_THIN_NTH: A/B knob (64 / 256 / 1024).
-    const int nth = env_int("RSP_ILU_THIN_NTH", rsp::kThinThreads);
+    std::vector<char> thin_lev((size_t)std::max(nlev, 1), 0);
+    for (const rsp::LevelSeg &sg : sp.segs)
+        for (int l = sg.lb; l < sg.le; l++) thin_lev[(size_t)l] = (char)sg.thin;
+    std::vector<int> col;
+    sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
+    sp.tpos.clear();
+    for (int l = 0; l < nlev; l++)
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
+            const int i = order[(size_t)x];
+            rsp::RowTask &t = sp.tasks[(size_t)x];
+            t.i = i;
+            t.t0 = (int)sp.tpos.size();
+            row_terms(i, [&](int tp, int c) {
+                sp.tpos.push_back(tp);
+                col.push_back(c);
+            });
+            if (thin_lev[(size_t)l])
+                while ((int)sp.tpos.size() - t.t0 < padded((int)sp.tpos.size() - t.t0)) {
+                    sp.tpos.push_back(-1);
+                    col.push_back(-1);
+                }
+            t.t1 = (int)sp.tpos.size();
+            t.d = diag.empty() ? -1 : diag[(size_t)i];
+        }
+    std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
+    for (int l = 0; l < nlev; l++)
+        if (ptr[(size_t)l + 1] > ptr[(size_t)l])
+            lterms[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l + 1] - 1].t1 - sp.tasks[(size_t)ptr[(size_t)l]].t0;
+    sp.src = col;
+    for (size_t k = 0; k < col.size(); k++)
+        if (col[k] < 0) sp.src[k] = rsp::kPadSrc;
     for (rsp::LevelSeg &sg : sp.segs)
-        if (sg.thin) sg.nth = nth;
+        if (sg.thin) sg.nth = rsp::kThinThreads;
     // chunks of the thin runs + term sources
     std::vector<int> slot_of((size_t)n, -1);
     for (size_t x = 0; x < order.size(); x++) slot_of[(size_t)order[x]] = (int)x;
@@ -919,6 +953,7 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
             const int r_end = ptr[(size_t)l + 1] - base;
             for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++)
                 for (int k = sp.tasks[(size_t)x].t0; k < sp.tasks[(size_t)x].t1; k++) {
+                    if (col[(size_t)k] < 0) continue;  // pad
                     const int sj = slot_of[(size_t)col[(size_t)k]];
                     if (sj < base || sj >= ptr[(size_t)l]) continue;  // before the run
                     const int rj = sj - base;
@@ -930,12 +965,40 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
         sp.tpos.push_back(0);
         sp.src.push_back(0);
     }
-    for (rsp::LevelChunk &ch : sp.chunks) {  // slot and term ranges, read by the kernel up front
-        ch.x0 = ptr[(size_t)ch.l0];
-        ch.x1 = ptr[(size_t)ch.l1];
-        ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
-        ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
+    // per chunk: slot and term ranges, the static row records (first group,
+    // y window slot), each term's y index in the LDS y buffer (window slot,
+    // the zero slot for pads, or its staged slot) and the staged terms
+    sp.trow.assign(std::max<size_t>(rows.size(), 1), rsp::ThinRowPlan{0, 0, 0, -1});
+    sp.sid.assign(sp.tpos.size(), rsp::kYWin);
+    sp.stg.clear();
+    for (const rsp::LevelSeg &sg : sp.segs) {
+        if (!sg.thin) continue;
+        const int base = ptr[(size_t)sg.lb];
+        for (int c = sg.c0; c < sg.c1; c++) {
+            rsp::LevelChunk &ch = sp.chunks[(size_t)c];
+            ch.x0 = ptr[(size_t)ch.l0];
+            ch.x1 = ptr[(size_t)ch.l1];
+            ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
+            ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
+            ch.st0 = (int)sp.stg.size();
+            for (int x = ch.x0; x < ch.x1; x++) {
+                const rsp::RowTask &t = sp.tasks[(size_t)x];
+                sp.trow[(size_t)x] = {(t.t0 - ch.k0) / group | ((t.t1 - t.t0) / group) << 16,
+                                      (x - base) & (rsp::kYWin - 1), t.i, t.d};
+                for (int k = t.t0; k < t.t1; k++) {
+                    const int sc = sp.src[(size_t)k];
+                    if (sc < 0) {
+                        sp.sid[(size_t)k] = -sc - 1;  // window slot, or the zero slot for a pad
+                    } else {
+                        sp.sid[(size_t)k] = rsp::kYWin + 1 + (k - ch.k0);
+                        sp.stg.push_back({k - ch.k0, sc});
+                    }
+                }
+            }
+            ch.st1 = (int)sp.stg.size();
+        }
     }
+    if (sp.stg.empty()) sp.stg.push_back({0, 0});
     if (sp.chunks.empty()) sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
 }
 
@@ -1240,6 +1303,8 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         }
         f->L.batch = f->LT.batch = chain_batch(nl, n);
         f->U.batch = chain_batch(nu, n);
+        for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U})  // thin-run term groups
+            d->group = env_int("RSP_ILU_GROUP", d->batch == 2 ? 2 : 4) == 2 ? 2 : 4;
         f->fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
     }
     hipError_t e = hipSuccess;
@@ -1271,15 +1336,15 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         rsp_ilu0_info::Dag &d = kind == 0 ? f->L : (kind == 1 ? f->LT : f->U);
         SolvePlan sp;
         if (kind == 0)
-            build_solve_plan(n, d.ptr, rows_l, thin_solve, std::vector<int>(), [&](int i, auto emit) {
+            build_solve_plan(n, d.ptr, rows_l, thin_solve, d.group, std::vector<int>(), [&](int i, auto emit) {
                 for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
             }, sp);
         else if (kind == 1)
-            build_solve_plan(n, d.ptr, rows_lt, thin_solve, std::vector<int>(), [&](int i, auto emit) {
+            build_solve_plan(n, d.ptr, rows_lt, thin_solve, d.group, std::vector<int>(), [&](int i, auto emit) {
                 for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++) emit(lts[(size_t)q], ltc[(size_t)q]);
             }, sp);
         else
-            build_solve_plan(n, d.ptr, rows_u, thin_solve, udiag, [&](int i, auto emit) {
+            build_solve_plan(n, d.ptr, rows_u, thin_solve, d.group, udiag, [&](int i, auto emit) {
                 for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++)
                     emit(p, ci[(size_t)p]);
             }, sp);
@@ -1290,6 +1355,16 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         if (e == hipSuccess) e = upload_vec(&d.d_tpos, sp.tpos);
         if (e == hipSuccess) e = upload_vec(&d.d_src, sp.src);
         if (e == hipSuccess) e = upload_vec(&d.d_chunks, sp.chunks);
+        if (e == hipSuccess) e = upload_vec(&d.d_trow, sp.trow);
+        if (e == hipSuccess) e = upload_vec(&d.d_sid, sp.sid);
+        if (e == hipSuccess) e = upload_vec(&d.d_stg, sp.stg);
+        d.nterms = (int)sp.tpos.size();
+    }
+    {  // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
+        const size_t nt = (size_t)std::max({f->L.nterms, f->LT.nterms, f->U.nterms, 1});
+        if (e == hipSuccess) e = hipMalloc(&f->d_sval, nt * sizeof(double));
+        if (e == hipSuccess) e = hipMalloc(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
+        if (e == hipSuccess) e = hipMalloc(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
     }
     if (e == hipSuccess) e = hipMalloc((void **)&f->d_zero, sizeof(int));
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
@@ -1341,10 +1416,15 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<
     p.segs = segs.data();
     p.nseg = (int)segs.size();
     p.batch = batch;
+    p.group = d.group;
     p.tasks = d.d_tasks;
     p.tpos = d.d_tpos;
     p.src = d.d_src;
     p.chunks = d.d_chunks;
+    p.trow = d.d_trow;
+    p.sid = d.d_sid;
+    p.stg = d.d_stg;
+    p.nterms = d.nterms;
     p.nshort = d.d_nshort;
     p.nshort_host = d.nshort.data();
     return p;
@@ -1400,9 +1480,12 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.y = y;
     a.alpha = (t == RSP_R_64F) ? *(const double *)alpha : (double)*(const float *)alpha;
     a.plan = level_plan(f->L, f->L.segs, f->L.batch);
-    a.thin_prefetch = env_int("RSP_ILU_THIN_PF", 1) != 0;
+    a.sval = f->d_sval;
+    a.sx = f->d_sx;
+    a.sdg = f->d_sdg;
     a.trace = nullptr;
     a.trace_cap = 0;
+    a.trace_clk = 0;
     return a;
 }
 
@@ -1424,6 +1507,7 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
         RSP_CHECK_HIP(hipMemsetAsync(d_trace, 0, trace_cap * sizeof(unsigned long long), h->stream));
         a.trace = d_trace;
         a.trace_cap = trace_cap;
+        a.trace_clk = env_int("RSP_ILU_TRACE_CLK", 0);
     }
     hipError_t e;
     const bool f64 = value_type == RSP_R_64F, ftz = h->ftz != 0;
@@ -1447,10 +1531,11 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
             for (int l = 0; l < trace_cap / 2; l++)
                 if (t[(size_t)trace_cap / 2 + l])
                     fprintf(fp, "L %d %llu\n", l, t[(size_t)trace_cap / 2 + l]);
-            for (int c = 0; c < trace_cap / 8; c++)
-                if (t[4 * (size_t)c] || t[4 * (size_t)c + 3])
-                    fprintf(fp, "%d %llu %llu %llu %llu\n", c, t[4 * (size_t)c], t[4 * (size_t)c + 1],
-                            t[4 * (size_t)c + 2], t[4 * (size_t)c + 3]);
+            for (int c = 0; c < trace_cap / 16; c++)
+                if (t[8 * (size_t)c] || t[8 * (size_t)c + 3])
+                    fprintf(fp, "%d %llu %llu %llu %llu %llu %llu\n", c, t[8 * (size_t)c],
+                            t[8 * (size_t)c + 1], t[8 * (size_t)c + 2], t[8 * (size_t)c + 3],
+                            t[8 * (size_t)c + 4], t[8 * (size_t)c + 5]);
             fclose(fp);
         }
     }

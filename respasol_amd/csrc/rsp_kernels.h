@@ -125,9 +125,19 @@ struct alignas(16) RowTask {
 };
 struct alignas(16) LevelChunk {  // levels [l0, l1) of a thin solve run, staged in LDS together
     int l0, l1;
-    int x0, x1;  // its level-order slots: ptr[l0], ptr[l1]
-    int k0, k1;  // its flat terms: tasks[x0].t0, tasks[x1 - 1].t1
-    int pad0, pad1;
+    int x0, x1;    // its level-order slots: ptr[l0], ptr[l1]
+    int k0, k1;    // its flat terms: tasks[x0].t0, tasks[x1 - 1].t1
+    int st0, st1;  // its staged terms: stg[st0 .. st1)
+};
+// Static LDS record of a thin-run row (per level-order slot): first term group
+// (chunk-relative) | groups << 16, its y window slot, the row, its diagonal.
+struct alignas(16) ThinRowPlan {
+    int g, out, i, d;
+};
+// A thin-run term whose y is staged at the chunk start: its chunk-relative
+// slot and the row j whose y it needs.
+struct alignas(8) StagedTerm {
+    int slot, j;
 };
 
 struct LevelPlan {
@@ -138,12 +148,17 @@ struct LevelPlan {
     const LevelSeg *segs; // host
     int nseg;
     int batch;            // fma-chain load batch (2, 4, 8) from the mean chain length
+    int group;            // thin runs: terms padded to groups of this many (2 or 4)
     // solve DAGs only (device):
     const RowTask *tasks; // task of rows[x] at slot x
     const int *tpos;      // flat term -> position in vals
     const int *src;       // flat term -> y source: >= 0 the column (global y, or its value
                           // staged at the chunk start), < 0 slot -(s+1) of the LDS y window
     const LevelChunk *chunks;
+    const ThinRowPlan *trow;  // thin runs: static row records (per level-order slot)
+    const int *sid;       // thin runs: per term, its y's index in the LDS y buffer
+    const StagedTerm *stg;  // thin runs: staged terms, per chunk [st0, st1)
+    int nterms;           // flat terms
     const int *nshort;    // per level: rows with <= kLongTerms terms come first (host copy: nshort_host)
     const int *nshort_host;
 };
@@ -152,6 +167,8 @@ constexpr int kYWin = 4096;          // LDS y window of a thin solve run (entrie
 constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin)
 constexpr int kChunkTerms = 4096;    // terms staged per thin-run chunk
 constexpr int kThinThreads = 1024;   // workgroup of a thin segment
+constexpr int kGroup = 4;            // thin-run rows: terms padded to whole groups of (at most) this many
+constexpr int kPadSrc = -(kYWin + 1); // source of a pad term: the zero slot after the y window
 constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels)
 constexpr int kThinSolveRows = 1024; // solve levels this small (and <= kChunkTerms terms) run thin
 constexpr int kThinFactorRows = 64;  // factor levels this small (and fitting a chunk) run thin
@@ -216,9 +233,12 @@ struct TrsvArgs {
     void *y;
     double alpha;
     LevelPlan plan;       // the DAG of the solve (L, L^T or U), with its flat terms
-    int thin_prefetch;    // 1024-thread thin runs: next chunk loaded under the current one
-    unsigned long long *trace;  // diagnostics (RSP_ILU_TRACE): 4 timestamps per chunk, or null
+    void *sval;           // per flat term: vals[tpos] (0 for a pad), written by trsv_stream
+    void *sx;             // per level-order slot: alpha * x_i, written by trsv_stream
+    void *sdg;            // per level-order slot: u_ii (U solve), written by trsv_stream
+    unsigned long long *trace;  // diagnostics (RSP_ILU_TRACE): 8 timestamps per chunk, or null
     int trace_cap;
+    int trace_clk;              // level stamps in shader clock cycles (s_memtime) instead
 };
 
 }  // namespace rsp

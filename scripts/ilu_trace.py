@@ -57,8 +57,9 @@ def main():
             levs.append(np.array(curl, np.int64))
         for bi, L in enumerate(levs):
             if len(L) > 2:
-                d = np.diff(L[:, 1]) * 10.0
-                print(f"{name} solve {bi}: level-to-level ns: median {np.median(d):.0f} "
+                clk = os.environ.get("RSP_ILU_TRACE_CLK", "0") != "0"
+                d = np.diff(L[:, 1]) * (1.0 if clk else 10.0)
+                print(f"{name} solve {bi}: level-to-level {'cycles' if clk else 'ns'}: median {np.median(d):.0f} "
                       f"p10 {np.percentile(d, 10):.0f} p90 {np.percentile(d, 90):.0f} (n={len(d)})")
         for bi, b in enumerate(blocks):
             t = b[:, 1:]
@@ -70,6 +71,10 @@ def main():
             stg = (t[:, 2] - t[:, 1]) * 10.0
             lev = (t[:, 3] - t[:, 2]) * 10.0
             gap = np.diff(t[:, 0]) * 10.0
+            if t.shape[1] >= 6:  # prefetch issued by wave 0 / the last wave, after the stage
+                i0 = (t[:, 4] - t[:, 2]) * 10.0
+                i1 = (t[:, 5] - t[:, 2]) * 10.0
+                print(f"{name} solve {bi}: prefetch issue ns: wave0 mean {i0.mean():.0f} last wave mean {i1.mean():.0f}")
             print(f"{name} solve {bi}: chunks {len(t)}  mean ns: wait {wait.mean():.0f} "
                   f"stage {stg.mean():.0f} levels {lev.mean():.0f} chunk-to-chunk "
                   f"{gap.mean() if len(gap) else 0:.0f}; total {(wait.sum() + stg.sum() + lev.sum()) / 1e6:.3f} ms",
