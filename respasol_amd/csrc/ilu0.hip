@@ -365,17 +365,24 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         int slot[TPT];
         T y[TPT];
     };
+    // Loads past the chunk's rows / terms are predicated off (a whole wave
+    // past them issues nothing): the staging is bound by this CU's load
+    // bandwidth, and a chunk of short rows fills a fraction of its term slots.
     auto load_pre = [&](const rsp::LevelChunk &ch) {
         Pre p;
-        const int x = min(ch.x0 + tid, max(ch.x1 - 1, 0)), kl = max(ch.k1 - 1, 0), nl = ch.l1 - ch.l0;
-        p.r = a.plan.trow[x];
-        p.xv = sx[x];
-        p.dg = KIND == 2 ? sdg[x] : T(0);
+        const int x = ch.x0 + tid, nl = ch.l1 - ch.l0;
+        if (x < ch.x1) {
+            p.r = a.plan.trow[x];
+            p.xv = sx[x];
+            p.dg = KIND == 2 ? sdg[x] : T(0);
+        }
 #pragma unroll
         for (int j = 0; j < TPT; ++j) {
-            const int k = min(ch.k0 + tid + j * NTH, kl);
-            p.v[j] = sval[k];
-            p.id[j] = a.plan.sid[k];
+            const int k = ch.k0 + tid + j * NTH;
+            if (k < ch.k1) {
+                p.v[j] = sval[k];
+                p.id[j] = a.plan.sid[k];
+            }
         }
         p.lp = ptr[ch.l0 + min(tid, nl)];
         p.ln = a.plan.nshort[ch.l0 + min(tid, max(nl - 1, 0))];
@@ -596,9 +603,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         const rsp::LevelChunk cur = rc;
         if (c + 1 < c1) {
             const rsp::LevelChunk r2 = chunk(min(c + 2, cl));
-            p = load_pre(rn);     // chunk c+1's streams
-            w = load_stgy(sn);    // ... and its staged y
-            if (r2.st1 > r2.st0) sn = load_stg(r2);  // chunk c+2's staged terms
+            p = load_pre(rn);                           // chunk c+1's streams
+            if (rn.st1 > rn.st0) w = load_stgy(sn);     // ... and its staged y
+            if (r2.st1 > r2.st0) sn = load_stg(r2);     // chunk c+2's staged terms
             rc = rn;
             rn = r2;
         }
