@@ -146,10 +146,26 @@ def test_levels_reported(handle):
     assert up == _levels(A.rowptr, A.colidx, True)
 
 
-def test_full_size_moderate(handle):
-    """A full moderate-set surrogate (config 3 size) fp64, bitwise vs oracle."""
-    A = csr.surrogate("FEM_3D_thermal2")
+@pytest.mark.parametrize("name", ["FEM_3D_thermal2", "dc1", "ecology2"])
+def test_full_size_moderate(handle, name):
+    """Full moderate-set surrogates (config 3 size) fp64, bitwise vs oracle:
+    fat levels (FEM), ~10^4 narrow levels with staged long-range terms (dc1),
+    thin runs of single-level chunks (ecology2)."""
+    A = csr.surrogate(name)
     compare(A, torch.float64, handle)
+
+
+@pytest.mark.parametrize("group", [2, 4])
+@pytest.mark.parametrize("name,scale", [("dc1", 0.2), ("ecology2", 0.05), ("stomach", 0.05),
+                                        ("ASIC_320ks", 0.1)])
+def test_term_group_variants(handle, monkeypatch, group, name, scale):
+    """Thin-run rows padded to term groups of 2 or 4 (pads are exact no-op
+    fmas) give the same bits, for L, L^T and the U extension."""
+    monkeypatch.setenv("RSP_ILU_GROUP", str(group))
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float64, handle, x=x)
+    compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
 @pytest.mark.parametrize("thin_solve,thin_factor", [(0, 0), (1024, 1 << 30), (1, 1)])
