@@ -149,90 +149,172 @@ __global__ __launch_bounds__(64 * kIluWaves) void ilu0_level(IluArgs a, int off,
     factor_row<T, B>(a, a.plan.rows[off + w], threadIdx.x & 63);
 }
 
-// Thin run of the factor, chunk by chunk (rsp::FacChunk), one 1024-thread
-// workgroup. Per chunk: a full barrier (every earlier factor value is in
-// global memory and visible), then all threads stage in LDS the values of
-// the chunk's rows (cv, one slot per item), the item / update-pair index
-// lists, and the values of every u_kk / u_kj that comes from a row before the
-// chunk; the chunk's levels then run on LDS alone: wave w takes rows w, w+16,
-// ... of a level, each row stage by stage exactly as factor_row (same fma
-// order), writing every finished value to its LDS slot and to vals; an
-// LDS-only barrier separates the levels.
+// Thin run of the factor in ROUNDS (plan: build_factor_plan; rsp::RndChunk,
+// rsp::RndItem), one 1024-thread workgroup. A round's items (positions) are
+// independent: each is v = a_ij - sum_k l_ik u_kj over its update pairs (k
+// ascending, one fma each — the oracle's rounding sequence), then / u_kk for
+// a lower item; its operands are earlier rounds' values. Per chunk, LDS holds
+// V = [chunk slots, buffer 0 | chunk slots, buffer 1 | staged | 0] (this
+// chunk's and the previous chunk's values alternate buffers), the item
+// records, the update pairs as operand indices, and the round starts.
+// Staging is pipelined like the solve's: while chunk c's rounds run, the
+// a_ij and staged values of chunk c+1 (gathers by the positions loaded a
+// chunk earlier; staged producers are two or more chunks back, so their
+// stores completed at this chunk's switch) and the records of chunk c+2 are
+// in flight. Rounds of <= 64 items run on wave 0 alone, consecutive narrow
+// rounds without workgroup barriers (in-order LDS of one wave); wider rounds
+// use every thread and an LDS-only barrier.
 template <typename T>
-__global__ __launch_bounds__(kThinThreads) void ilu0_chunked(IluArgs a, int c0, int c1) {
-    __shared__ T cv[rsp::kFacItems];
-    __shared__ T dpre[rsp::kFacItems];
-    __shared__ int lpos[rsp::kFacItems], lu0[rsp::kFacItems + 1], lsend[rsp::kFacItems], ld[rsp::kFacItems];
-    __shared__ T upre[rsp::kFacPairs];
-    __shared__ int lpl[rsp::kFacPairs], lpu[rsp::kFacPairs];
-    __shared__ rsp::FacRow lrow[rsp::kFacRows];
-    __shared__ int lptr[rsp::kFacRows + 1];  // a chunk has <= kFacRows levels
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+__global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, int c1) {
+    constexpr int NTH = kThinThreads, K = rsp::kRndItems, S = rsp::kRndStaged;
+    constexpr int IPT = K / NTH, PPT = rsp::kRndPairs / NTH, SPT = S / NTH, RPT = rsp::kRndRounds / NTH;
+    static_assert((K & (K - 1)) == 0 && IPT * NTH == K && PPT * NTH == rsp::kRndPairs &&
+                      SPT * NTH == S && RPT * NTH == rsp::kRndRounds, "chunk budgets per thread");
+    constexpr int kZero = 2 * K + S;
+    __shared__ T V[2 * K + S + 1];
+    __shared__ int4 litem[K];               // pos, pairs (start | count << 16), divisor index, zr
+    __shared__ int lpair[rsp::kRndPairs];   // operand indices l_ik | u_kj << 16
+    __shared__ int lrnd[rsp::kRndRounds + 1];
+    const int tid = threadIdx.x, lane = tid & 63;
     T *vals = (T *)a.vals;
-    const int *ptr = a.plan.ptr_dev;
-    for (int c = c0; c < c1; ++c) {
-        const rsp::FacChunk ch = a.fchunks[c];
-        const int ni = ch.item1 - ch.item0, np = ch.pair1 - ch.pair0;
-        __syncthreads();  // earlier chunks' values visible, LDS free
-        for (int x = tid; x < ni; x += kThinThreads) {
-            const int g = ch.item0 + x;
-            const int pos = a.fpos[g], d = a.fd[g];
-            lpos[x] = pos;
-            cv[x] = vals[pos];
-            lu0[x] = a.fu0[g];
-            lsend[x] = a.fsend[g];
-            ld[x] = d;
-            dpre[x] = (d < 0 && d != INT_MIN) ? vals[-d - 1] : T(0);
-        }
-        if (tid == 0) lu0[ni] = np;
-        const int x0 = ptr[ch.l0], nr = ptr[ch.l1] - x0;
-        for (int r = tid; r < nr; r += kThinThreads) lrow[r] = a.frows[x0 + r];
-        for (int q = tid; q <= ch.l1 - ch.l0; q += kThinThreads) lptr[q] = ptr[ch.l0 + q];
-        for (int u = tid; u < np; u += kThinThreads) {
-            const int g = ch.pair0 + u;
-            const int pu = a.fpu[g];
-            lpl[u] = a.fpl[g];
-            lpu[u] = pu;
-            upre[u] = pu < 0 ? vals[-pu - 1] : T(0);
-        }
-        __syncthreads();
-        for (int l = ch.l0; l < ch.l1; ++l) {
-            const int xe = lptr[l - ch.l0 + 1];
-            for (int x = lptr[l - ch.l0] + wave; x < xe; x += kThinThreads / 64) {
-                const rsp::FacRow r = lrow[x - x0];
-                const int nitem = r.nitem_hd & ((1 << 30) - 1), hd = r.nitem_hd >> 30;
-                const int lo_end = r.item0 + r.nlow, end = r.item0 + nitem;
-                auto item = [&](int it) {
-                    T v = cv[it];
-                    for (int u = lu0[it]; u < lu0[it + 1]; ++u) {
-                        const int pu = lpu[u];
-                        v = __builtin_fma(-cv[lpl[u]], pu >= 0 ? cv[pu] : upre[u], v);
-                    }
-                    return v;
-                };
-                for (int st = r.item0; st < lo_end;) {
-                    const int e = lsend[st];
-                    for (int it = st + lane; it < e; it += 64) {
-                        const int d = ld[it];
-                        const T v = item(it) / (d >= 0 ? cv[d] : dpre[it]);
-                        cv[it] = v;
-                        vals[lpos[it]] = v;
-                    }
-                    // this stage's l_ik visible to the wave's next stage
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-                    st = e;
-                }
-                for (int it = lo_end + lane; it < end; it += 64) {
-                    const T v = item(it);
-                    cv[it] = v;
-                    vals[lpos[it]] = v;
-                    if (it == lo_end && hd && v == T(0)) atomicMin(a.zero_pivot, r.i);
-                }
+    if (tid == 0) V[kZero] = T(0);
+    typedef const __attribute__((address_space(4))) int *ChunkPtr;  // scalar loads
+    const ChunkPtr chunks = (ChunkPtr)a.rchunks;
+    auto chunk = [&](int c) {
+        const ChunkPtr q = chunks + (size_t)c * (sizeof(rsp::RndChunk) / sizeof(int));
+        return rsp::RndChunk{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
+    };
+    struct Recs {  // item records and staged positions of a chunk (this thread's share)
+        rsp::RndItem it[IPT];
+        int q[SPT];
+    };
+    struct Pre {  // ... its a_ij and staged values, pairs, round starts
+        T aij[IPT], sv[SPT];
+        int pr[PPT], rs[RPT];
+    };
+    auto load_recs = [&](const rsp::RndChunk &ch) {
+        Recs R;
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            if (ch.i0 + tid + j * NTH < ch.i1) R.it[j] = a.ritems[ch.i0 + tid + j * NTH];
+#pragma unroll
+        for (int j = 0; j < SPT; ++j)
+            if (ch.s0 + tid + j * NTH < ch.s1) R.q[j] = a.rstaged[ch.s0 + tid + j * NTH];
+        return R;
+    };
+    auto load_pre = [&](const rsp::RndChunk &ch, const Recs &R) {
+        Pre P;
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            if (ch.i0 + tid + j * NTH < ch.i1) P.aij[j] = vals[R.it[j].pos];
+#pragma unroll
+        for (int j = 0; j < SPT; ++j)
+            if (ch.s0 + tid + j * NTH < ch.s1) P.sv[j] = vals[R.q[j]];
+#pragma unroll
+        for (int j = 0; j < PPT; ++j)
+            if (ch.p0 + tid + j * NTH < ch.p1) P.pr[j] = a.rpairs[ch.p0 + tid + j * NTH];
+#pragma unroll
+        for (int j = 0; j < RPT; ++j)
+            if (ch.r0 + tid + j * NTH < ch.r1) P.rs[j] = a.rrounds[ch.r0 + tid + j * NTH];
+        return P;
+    };
+    // plan operand class -> LDS index for chunk parity par
+    auto idx = [&](int x, int par) { return x < 2 * K ? (((x >= K) ^ par) * K + (x & (K - 1))) : x; };
+    auto stage = [&](int c, const rsp::RndChunk &ch, const Recs &R, const Pre &P) {
+        const int ni = ch.i1 - ch.i0, ns = ch.s1 - ch.s0, np = ch.p1 - ch.p0, nr = ch.r1 - ch.r0;
+        const int par = c & 1, cb = par * K;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // earlier chunks' values stored and visible; LDS free
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            if (tid + j * NTH < ni) {
+                const rsp::RndItem r = R.it[j];
+                litem[tid + j * NTH] = make_int4(r.pos, r.u, r.d >= 0 ? idx(r.d, par) : -1, r.zr);
+                V[cb + tid + j * NTH] = P.aij[j];
             }
-            lds_barrier();
+#pragma unroll
+        for (int j = 0; j < SPT; ++j)
+            if (tid + j * NTH < ns) V[2 * K + tid + j * NTH] = P.sv[j];
+#pragma unroll
+        for (int j = 0; j < PPT; ++j)
+            if (tid + j * NTH < np)
+                lpair[tid + j * NTH] = idx(P.pr[j] & 0xffff, par) | idx(P.pr[j] >> 16, par) << 16;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j)
+            if (tid + j * NTH < nr) lrnd[tid + j * NTH] = P.rs[j];
+        if (tid == 0) lrnd[nr] = ni;
+        lds_barrier();
+    };
+    auto process = [&](int it, int cb) {
+        const int4 r = litem[it];
+        T v = V[cb + it];
+        const int u0 = r.y & 0xffff, u1 = u0 + (r.y >> 16);
+        for (int u = u0; u < u1; u += 4) {  // operands of 4 pairs loaded together (clamped)
+            int pr[4];
+            T l[4], w[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) pr[b] = lpair[min(u + b, u1 - 1)];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                l[b] = V[pr[b] & 0xffff];
+                w[b] = V[pr[b] >> 16];
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (u + b < u1) v = __builtin_fma(-l[b], w[b], v);
         }
+        if (r.z >= 0) v = v / V[r.z];
+        V[cb + it] = v;
+        vals[r.x] = v;
+        if (r.w >= 0 && v == T(0)) atomicMin(a.zero_pivot, r.w);
+    };
+    auto narrow = [&](int q) { return lrnd[q + 1] - lrnd[q] <= 64; };
+    auto run_end = [&](int q, int nr) {  // first round >= q that is not narrow, or nr
+        for (int b = q;; b += 64) {
+            const int qq = b + lane;
+            const unsigned long long m = __ballot(!(qq < nr && narrow(qq)));
+            if (m) return b + __builtin_ctzll(m);
+        }
+    };
+    auto rounds = [&](int c, const rsp::RndChunk &ch) {
+        const int nr = ch.r1 - ch.r0, cb = (c & 1) * K;
+        for (int q = 0; q < nr;) {
+            if (narrow(q)) {
+                const int qe = run_end(q, nr);
+                if (tid < 64)
+                    for (int qq = q; qq < qe; ++qq) {
+                        const int b0 = lrnd[qq];
+                        if (b0 + lane < lrnd[qq + 1]) process(b0 + lane, cb);
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                    }
+                lds_barrier();
+                q = qe;
+                continue;
+            }
+            for (int it = lrnd[q] + tid; it < lrnd[q + 1]; it += NTH) process(it, cb);
+            lds_barrier();
+            ++q;
+        }
+    };
+    const int cl = c1 - 1;
+    rsp::RndChunk rc = chunk(c0), rn = chunk(min(c0 + 1, cl));
+    Recs R = load_recs(rc);
+    Pre P = load_pre(rc, R);
+    Recs Rn = load_recs(rn);
+    for (int c = c0; c < c1; ++c) {
+        stage(c, rc, R, P);
+        const rsp::RndChunk cur = rc;
+        if (c + 1 < c1) {
+            const rsp::RndChunk r2 = chunk(min(c + 2, cl));
+            P = load_pre(rn, Rn);  // chunk c+1's gathers
+            R = Rn;
+            Rn = load_recs(r2);    // chunk c+2's records
+            rc = rn;
+            rn = r2;
+        }
+        rounds(c, cur);
     }
 }
 
@@ -628,7 +710,7 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
-            hipLaunchKernelGGL((ilu0_chunked<T>), dim3(1), dim3(kThinThreads), 0, s, a, sg.c0, sg.c1);
+            hipLaunchKernelGGL((ilu0_rounds<T>), dim3(1), dim3(kThinThreads), 0, s, a, sg.c0, sg.c1);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

@@ -79,10 +79,9 @@ struct rsp_ilu0_info {
     } L, LT, U;
     std::vector<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
     void *d_sval = nullptr, *d_sx = nullptr, *d_sdg = nullptr;  // solve streams (trsv_stream)
-    rsp::FacChunk *d_fchunks = nullptr;        // LDS-staged factor chunks (thin runs)
-    rsp::FacRow *d_frows = nullptr;
-    int *d_fpos = nullptr, *d_fu0 = nullptr, *d_fsend = nullptr, *d_fd = nullptr;
-    int *d_fpl = nullptr, *d_fpu = nullptr;
+    rsp::RndChunk *d_rchunks = nullptr;        // round-based factor chunks (thin runs)
+    rsp::RndItem *d_ritems = nullptr;
+    int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
     int fac_batch;
 };
 
@@ -755,9 +754,8 @@ static void ilu_free_device(rsp_ilu0_info *f) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
-    for (void **p : {(void **)&f->d_fchunks, (void **)&f->d_frows, (void **)&f->d_fpos,
-                     (void **)&f->d_fu0, (void **)&f->d_fsend, (void **)&f->d_fd, (void **)&f->d_fpl,
-                     (void **)&f->d_fpu}) {
+    for (void **p : {(void **)&f->d_rchunks, (void **)&f->d_ritems, (void **)&f->d_rpairs,
+                     (void **)&f->d_rstaged, (void **)&f->d_rrounds}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -1014,6 +1012,7 @@ static hipError_t upload_vec(V **dst, const std::vector<V> &v) {
 // Symbolic ILU(0) data (built by ilu_symbolic below).
 struct IluSymbolic {
     std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
+    std::vector<int> stage;  // per lower position: its intra-row stage
 };
 
 // Factor plan of the L DAG (see IluArgs): segments (a level is thin if it
@@ -1022,11 +1021,24 @@ struct IluSymbolic {
 // of its rows: lower ones in intra-row stage order, then upper ones) and update
 // pairs with their sources: a chunk-local item when the producing row is in
 // the chunk, else the position (its final value is staged at the chunk start).
+// Factor plan of the L DAG (see IluArgs): segments (fat levels: one launch
+// each; thin levels: one single-workgroup launch per run) and, for the thin
+// runs, ROUNDS: a level's positions ("items") grouped so that a round's items
+// are independent — a lower item of intra-row stage s is in round s, a row's
+// upper items (diagonal included) in the round after its last lower stage.
+// Every item depends only on earlier rounds (its own row's l_ik) and earlier
+// levels (u_kj, u_kk). The run's items, in round order, are cut into LDS
+// chunks (<= kRndItems items, kRndPairs update pairs, kRndStaged staged
+// values, kRndRounds rounds; a round may be split between chunks). An item's
+// operands are indices into the kernel's LDS value buffer by class: its own
+// chunk's slots, the previous chunk's slots (kept in the other LDS buffer),
+// values staged from vals at the chunk start (producers two or more chunks
+// back, or before the run), or the zero slot (a missing u_kk).
 struct FacPlan {
     std::vector<rsp::LevelSeg> segs;
-    std::vector<rsp::FacChunk> chunks;
-    std::vector<rsp::FacRow> rows;  // per level-order slot
-    std::vector<int> pos, u0, send, d, pl, pu;
+    std::vector<rsp::RndChunk> chunks;
+    std::vector<rsp::RndItem> items;
+    std::vector<int> pairs, staged, rounds;
 };
 
 static void build_factor_plan(int n, const std::vector<int> &rp, const std::vector<int> &ci,
@@ -1034,94 +1046,147 @@ static void build_factor_plan(int n, const std::vector<int> &rp, const std::vect
                               const IluSymbolic &sym, const std::vector<int> &ptr,
                               const std::vector<int> &rows, int thin_rows, FacPlan &fp) {
     const int nlev = (int)ptr.size() - 1;
-    auto row_items = [&](int i) { return rp[(size_t)i + 1] - rp[(size_t)i]; };
-    auto row_pairs = [&](int i) {
-        return sym.upd_ptr[(size_t)rp[(size_t)i + 1]] - sym.upd_ptr[(size_t)rp[(size_t)i]];
-    };
-    std::vector<long long> litems((size_t)std::max(nlev, 1), 0), lpairs((size_t)std::max(nlev, 1), 0);
-    for (int l = 0; l < nlev; l++)
-        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-            litems[(size_t)l] += row_items(rows[(size_t)x]);
-            lpairs[(size_t)l] += row_pairs(rows[(size_t)x]);
-        }
+    const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
+    const int thin_items = env_int("RSP_ILU_THIN_FACTOR_ITEMS", rsp::kRndLevelItems);
+    auto npairs = [&](int p) { return sym.upd_ptr[(size_t)p + 1] - sym.upd_ptr[(size_t)p]; };
     fp.segs.clear();
     for (int l = 0; l < nlev; l++) {
         const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
-        const int thin = (cnt <= thin_rows && cnt <= rsp::kFacRows && litems[(size_t)l] <= rsp::kFacItems &&
-                          lpairs[(size_t)l] <= rsp::kFacPairs) ? 1 : 0;
+        long long items = 0;
+        int maxp = 0;
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
+            const int i = rows[(size_t)x];
+            items += rp[(size_t)i + 1] - rp[(size_t)i];
+            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) maxp = std::max(maxp, npairs(p));
+        }
+        const int thin = (cnt <= thin_rows && items <= thin_items && maxp <= rsp::kRndItemPairs) ? 1 : 0;
         if (!fp.segs.empty() && fp.segs.back().thin == thin && fp.segs.back().le == l)
             fp.segs.back().le = l + 1;
         else
             fp.segs.push_back({l, l + 1, thin, 0, 0, kThinThreadsHost});
     }
-    fp.rows.assign(std::max<size_t>(rows.size(), 1), rsp::FacRow{0, 0, 0, 0});
     fp.chunks.clear();
-    fp.pos.clear(); fp.u0.clear(); fp.send.clear(); fp.d.clear(); fp.pl.clear(); fp.pu.clear();
-    std::vector<int> item_of((size_t)rp[(size_t)n], -1);
-    auto close_chunk = [&](rsp::FacChunk &ch) {
-        // items of the chunk's rows, then their update pairs and u_kk sources
-        for (int x = ptr[(size_t)ch.l0]; x < ptr[(size_t)ch.l1]; x++) {
-            const int i = rows[(size_t)x], rs = rp[(size_t)i], di = dpos[(size_t)i], re = rp[(size_t)i + 1];
-            const int b = (int)fp.pos.size() - ch.item0;
-            fp.rows[(size_t)x] = {i, b, di - rs, (re - rs) | (hasdiag[(size_t)i] << 30)};
-            for (int s2 = rs; s2 < di; s2++) {
-                const int p2 = sym.lord[(size_t)s2], k = ci[(size_t)p2];
-                item_of[(size_t)p2] = (int)fp.pos.size() - ch.item0;
-                fp.pos.push_back(p2);
-                fp.send.push_back(b + (sym.lend[(size_t)s2] - rs));
-                int dc = INT_MIN;  // u_kk of the lower item: row k is in an earlier level
-                if (hasdiag[(size_t)k]) {
-                    const int dk = dpos[(size_t)k];
-                    dc = item_of[(size_t)dk] >= 0 ? item_of[(size_t)dk] : -(dk + 1);
-                }
-                fp.d.push_back(dc);
-            }
-            for (int p2 = di; p2 < re; p2++) {
-                item_of[(size_t)p2] = (int)fp.pos.size() - ch.item0;
-                fp.pos.push_back(p2);
-                fp.send.push_back(0);
-                fp.d.push_back(INT_MIN);
-            }
-        }
-        ch.item1 = (int)fp.pos.size();
-        ch.pair0 = (int)fp.pl.size();
-        for (int it = ch.item0; it < ch.item1; it++) {
-            const int p2 = fp.pos[(size_t)it];
-            fp.u0.push_back((int)fp.pl.size() - ch.pair0);
-            for (int u = sym.upd_ptr[(size_t)p2]; u < sym.upd_ptr[(size_t)p2 + 1]; u++) {
-                fp.pl.push_back(item_of[(size_t)sym.upd_l[(size_t)u]]);
-                const int q = sym.upd_u[(size_t)u];
-                fp.pu.push_back(item_of[(size_t)q] >= 0 ? item_of[(size_t)q] : -(q + 1));
-            }
-        }
-        ch.pair1 = (int)fp.pl.size();
-        for (int it = ch.item0; it < ch.item1; it++) item_of[(size_t)fp.pos[(size_t)it]] = -1;
-        fp.chunks.push_back(ch);
+    fp.items.clear();
+    fp.pairs.clear();
+    fp.staged.clear();
+    fp.rounds.clear();
+    // where each position was placed: chunk and slot (-1: not in this run yet)
+    std::vector<int> pchunk((size_t)rp[(size_t)n], -1), pslot((size_t)rp[(size_t)n], 0);
+    std::vector<int> stg_of((size_t)rp[(size_t)n], -1);  // staged slot in the current chunk
+    std::vector<int> stg_list;                            // positions staged in the current chunk
+    struct RItem {
+        int round, pos, row;
     };
+    std::vector<RItem> ritems;  // a level's items
     for (rsp::LevelSeg &sg : fp.segs) {
         if (!sg.thin) continue;
         sg.c0 = (int)fp.chunks.size();
-        rsp::FacChunk ch{sg.lb, sg.lb, (int)fp.pos.size(), 0, 0, 0};
-        long long crow = 0, citem = 0, cpair = 0;
+        rsp::RndChunk ch{};
+        int c = -1;  // current chunk id
+        auto open_chunk = [&]() {
+            for (int q : stg_list) stg_of[(size_t)q] = -1;
+            stg_list.clear();
+            c = (int)fp.chunks.size();
+            ch = rsp::RndChunk{(int)fp.items.size(), (int)fp.items.size(), (int)fp.pairs.size(),
+                               (int)fp.pairs.size(), (int)fp.staged.size(), (int)fp.staged.size(),
+                               (int)fp.rounds.size(), (int)fp.rounds.size()};
+            fp.chunks.push_back(ch);
+        };
+        auto close_chunk = [&]() {
+            ch.i1 = (int)fp.items.size();
+            ch.p1 = (int)fp.pairs.size();
+            ch.s1 = (int)fp.staged.size();
+            ch.r1 = (int)fp.rounds.size();
+            fp.chunks[(size_t)c] = ch;
+        };
+        // operand class index of position q for an item of chunk c (new staged
+        // values are appended to `fresh`; the caller commits or rolls back)
+        auto ref = [&](int q, std::vector<int> &fresh) {
+            const int qc = pchunk[(size_t)q];
+            if (qc == c) return pslot[(size_t)q];
+            if (qc >= 0 && qc == c - 1) return K + pslot[(size_t)q];
+            if (stg_of[(size_t)q] >= 0) return 2 * K + stg_of[(size_t)q];
+            for (size_t f = 0; f < fresh.size(); f++)
+                if (fresh[f] == q) return 2 * K + (int)(stg_list.size() + f);
+            fresh.push_back(q);
+            return 2 * K + (int)(stg_list.size() + fresh.size() - 1);
+        };
+        open_chunk();
+        long long last_round_key = -1;  // (level, round) of the chunk's last round
+        std::vector<int> fresh, ipairs;
         for (int l = sg.lb; l < sg.le; l++) {
-            const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
-            if (ch.l1 > ch.l0 && (crow + cnt > rsp::kFacRows || citem + litems[(size_t)l] > rsp::kFacItems ||
-                                  cpair + lpairs[(size_t)l] > rsp::kFacPairs)) {
-                close_chunk(ch);
-                ch = rsp::FacChunk{l, l, (int)fp.pos.size(), 0, 0, 0};
-                crow = citem = cpair = 0;
+            ritems.clear();
+            for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
+                const int i = rows[(size_t)x], rs = rp[(size_t)i], di = dpos[(size_t)i];
+                int nst = 0;
+                for (int p = rs; p < di; p++) {
+                    ritems.push_back({sym.stage[(size_t)p], p, i});
+                    nst = std::max(nst, sym.stage[(size_t)p] + 1);
+                }
+                for (int p = di; p < rp[(size_t)i + 1]; p++) ritems.push_back({nst, p, i});
             }
-            ch.l1 = l + 1;
-            crow += cnt;
-            citem += litems[(size_t)l];
-            cpair += lpairs[(size_t)l];
+            std::stable_sort(ritems.begin(), ritems.end(),
+                             [](const RItem &u, const RItem &v) { return u.round < v.round; });
+            for (const RItem &ri : ritems) {
+                const int p = ri.pos, i = ri.row;
+                const long long key = (long long)(l - sg.lb) * 1000000007LL + ri.round;
+                const bool lower = p < dpos[(size_t)i];
+                for (int attempt = 0; attempt < 2; attempt++) {
+                    fresh.clear();
+                    ipairs.clear();
+                    for (int u = sym.upd_ptr[(size_t)p]; u < sym.upd_ptr[(size_t)p + 1]; u++) {
+                        const int lc = ref(sym.upd_l[(size_t)u], fresh), uc = ref(sym.upd_u[(size_t)u], fresh);
+                        ipairs.push_back(lc | uc << 16);
+                    }
+                    int d = -1;
+                    if (lower) {
+                        const int k = ci[(size_t)p];
+                        d = hasdiag[(size_t)k] ? ref(dpos[(size_t)k], fresh) : kZero;
+                    }
+                    const int slot = (int)fp.items.size() - ch.i0;
+                    const bool new_round = key != last_round_key;
+                    const bool fits = slot < K && (int)(fp.pairs.size() - ch.p0 + ipairs.size()) <= rsp::kRndPairs &&
+                                      (int)(stg_list.size() + fresh.size()) <= S &&
+                                      (int)(fp.rounds.size() - ch.r0) + (new_round ? 1 : 0) <= rsp::kRndRounds;
+                    if (!fits && attempt == 0 && slot > 0) {  // next chunk (references re-resolved there)
+                        close_chunk();
+                        open_chunk();
+                        last_round_key = -1;
+                        continue;
+                    }
+                    // commit the item
+                    for (int q : fresh) {
+                        stg_of[(size_t)q] = (int)stg_list.size();
+                        stg_list.push_back(q);
+                        fp.staged.push_back(q);
+                    }
+                    if (new_round) {
+                        fp.rounds.push_back(slot);
+                        last_round_key = key;
+                    }
+                    const int pstart = (int)fp.pairs.size() - ch.p0;
+                    fp.pairs.insert(fp.pairs.end(), ipairs.begin(), ipairs.end());
+                    const int zr = (!lower && p == dpos[(size_t)i] && hasdiag[(size_t)i]) ? i : -1;
+                    fp.items.push_back({p, pstart | (int)ipairs.size() << 16, d, zr});
+                    pchunk[(size_t)p] = c;
+                    pslot[(size_t)p] = slot;
+                    break;
+                }
+            }
         }
-        close_chunk(ch);
+        close_chunk();
         sg.c1 = (int)fp.chunks.size();
+        for (int x = ptr[(size_t)sg.lb]; x < ptr[(size_t)sg.le]; x++) {  // positions leave the run
+            const int i = rows[(size_t)x];
+            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) pchunk[(size_t)p] = -1;
+        }
+        for (int q : stg_list) stg_of[(size_t)q] = -1;
+        stg_list.clear();
     }
-    for (std::vector<int> *v : {&fp.pos, &fp.u0, &fp.send, &fp.d, &fp.pl, &fp.pu})
+    if (fp.items.empty()) fp.items.push_back({0, 0, -1, -1});
+    for (std::vector<int> *v : {&fp.pairs, &fp.staged, &fp.rounds})
         if (v->empty()) v->push_back(0);
-    if (fp.chunks.empty()) fp.chunks.push_back(rsp::FacChunk{0, 0, 0, 0, 0, 0});
+    if (fp.chunks.empty()) fp.chunks.push_back(rsp::RndChunk{});
 }
 
 extern "C" {
@@ -1167,7 +1232,8 @@ static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<in
     s.upd_u.resize((size_t)total);
     std::vector<int> fill(s.upd_ptr.begin(), s.upd_ptr.end() - 1);
     // pass 2: fill (k ascending per target, since p ascends) + stages
-    std::vector<int> stage((size_t)nnz, 0);
+    std::vector<int> &stage = s.stage;
+    stage.assign((size_t)nnz, 0);
     s.lord.assign((size_t)nnz, 0);
     s.lend.assign((size_t)nnz, 0);
     std::vector<int> order;
@@ -1308,14 +1374,11 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         f->fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
     }
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = upload_vec(&f->d_fchunks, fplan.chunks);
-    if (e == hipSuccess) e = upload_vec(&f->d_frows, fplan.rows);
-    if (e == hipSuccess) e = upload_vec(&f->d_fpos, fplan.pos);
-    if (e == hipSuccess) e = upload_vec(&f->d_fu0, fplan.u0);
-    if (e == hipSuccess) e = upload_vec(&f->d_fsend, fplan.send);
-    if (e == hipSuccess) e = upload_vec(&f->d_fd, fplan.d);
-    if (e == hipSuccess) e = upload_vec(&f->d_fpl, fplan.pl);
-    if (e == hipSuccess) e = upload_vec(&f->d_fpu, fplan.pu);
+    if (e == hipSuccess) e = upload_vec(&f->d_rchunks, fplan.chunks);
+    if (e == hipSuccess) e = upload_vec(&f->d_ritems, fplan.items);
+    if (e == hipSuccess) e = upload_vec(&f->d_rpairs, fplan.pairs);
+    if (e == hipSuccess) e = upload_vec(&f->d_rstaged, fplan.staged);
+    if (e == hipSuccess) e = upload_vec(&f->d_rrounds, fplan.rounds);
     if (e == hipSuccess) e = upload(&f->d_upd_ptr, sym.upd_ptr);
     if (e == hipSuccess) e = upload(&f->d_upd_l, sym.upd_l);
     if (e == hipSuccess) e = upload(&f->d_upd_u, sym.upd_u);
@@ -1449,14 +1512,11 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.upd_u = f->d_upd_u;
     a.lord = f->d_lord;
     a.lend = f->d_lend;
-    a.fchunks = f->d_fchunks;
-    a.frows = f->d_frows;
-    a.fpos = f->d_fpos;
-    a.fu0 = f->d_fu0;
-    a.fsend = f->d_fsend;
-    a.fd = f->d_fd;
-    a.fpl = f->d_fpl;
-    a.fpu = f->d_fpu;
+    a.rchunks = f->d_rchunks;
+    a.ritems = f->d_ritems;
+    a.rpairs = f->d_rpairs;
+    a.rstaged = f->d_rstaged;
+    a.rrounds = f->d_rrounds;
     a.plan = level_plan(f->L, f->fac_segs, f->fac_batch);
     hipError_t e;
     if (value_type == RSP_R_64F)

@@ -171,22 +171,29 @@ constexpr int kGroup = 4;            // thin-run rows: terms padded to whole gro
 constexpr int kPadSrc = -(kYWin + 1); // source of a pad term: the zero slot after the y window
 constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels)
 constexpr int kThinSolveRows = 1024; // solve levels this small (and <= kChunkTerms terms) run thin
-constexpr int kThinFactorRows = 64;  // factor levels this small (and fitting a chunk) run thin
+constexpr int kThinFactorRows = 1024; // factor levels this small (and within kRndLevelItems) run thin
 // LDS-staged factor chunks (ilu0_chunked): a chunk is a run of levels whose
 // rows' positions ("items") and update pairs fit these budgets.
-constexpr int kFacRows = 512;
-constexpr int kFacItems = 2048;
-constexpr int kFacPairs = 4096;
-struct alignas(8) FacChunk {
-    int l0, l1;        // levels
-    int item0, item1;  // flat item range
-    int pair0, pair1;  // flat update-pair range
+// Round-based thin factor runs (ilu0_rounds): budgets of one LDS chunk, and
+// which levels run thin (<= kRndLevelItems positions, every position's update
+// list <= kRndItemPairs pairs; RSP_ILU_THIN_FACTOR / _ITEMS knobs).
+constexpr int kRndItems = 2048;
+constexpr int kRndPairs = 4096;
+constexpr int kRndStaged = 4096;
+constexpr int kRndRounds = 2048;
+constexpr int kRndLevelItems = 6144;
+constexpr int kRndItemPairs = 1024;
+struct alignas(16) RndChunk {  // flat ranges of a chunk's items, pairs, staged values, rounds
+    int i0, i1, p0, p1, s0, s1, r0, r1;
 };
-// Factor row of a thin run, per level-order slot: its items are chunk-local
-// [item0, item0 + nitem), the first nlow in intra-row stage order (lower
-// positions), then the upper positions; hd = row has a diagonal.
-struct alignas(16) FacRow {
-    int i, item0, nlow, nitem_hd;  // nitem | hd << 30
+// One position of a thin factor run: its position in vals, its update pairs
+// (chunk-relative start | count << 16), its divisor u_kk as an operand index
+// (-1: upper, no division), the row if it is that row's diagonal (else -1).
+// Operand indices: [0, K) this chunk's slots, [K, 2K) the previous chunk's,
+// [2K, 2K + kRndStaged) staged values, 2K + kRndStaged the zero slot
+// (K = kRndItems); a pair packs (l_ik | u_kj << 16).
+struct alignas(16) RndItem {
+    int pos, u, d, zr;
 };
 
 struct IluArgs {
@@ -210,16 +217,10 @@ struct IluArgs {
     const int *lord;
     const int *lend;
     LevelPlan plan;       // L DAG, factor thresholds
-    // LDS-staged thin runs (ilu0_chunked). Items: fpos = position in vals,
-    // fu0 = first update pair (chunk-local), fsend = end of the item's
-    // intra-row stage (chunk-local, lower items), fd = u_kk source of a lower
-    // item (>= 0 chunk-local item, INT_MIN none (u_kk = 0), else -(pos + 1):
-    // staged from vals). Pairs: fpl = chunk-local item of l_ik, fpu = u_kj
-    // source (>= 0 chunk-local item, else -(pos + 1): staged).
-    const FacChunk *fchunks;
-    const FacRow *frows;  // per level-order slot of the L DAG
-    const int *fpos, *fu0, *fsend, *fd;
-    const int *fpl, *fpu;
+    // round-based thin runs (ilu0_rounds), see RndChunk / RndItem
+    const RndChunk *rchunks;
+    const RndItem *ritems;
+    const int *rpairs, *rstaged, *rrounds;
 };
 
 struct TrsvArgs {
