@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
         for (int q = 0; q < nr;) {
             if (narrow(q)) {
                 const int qe = run_end(q, nr);
-                if (tid < 64)
+                if (tid < 64)  // (a software-pipelined form of this loop measured slower)
                     for (int qq = q; qq < qe; ++qq) {
                         const int b0 = lrnd[qq];
                         if (b0 + lane < lrnd[qq + 1]) process(b0 + lane, cb);

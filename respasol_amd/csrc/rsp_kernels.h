@@ -181,7 +181,7 @@ constexpr int kRndItems = 2048;
 constexpr int kRndPairs = 4096;
 constexpr int kRndStaged = 4096;
 constexpr int kRndRounds = 2048;
-constexpr int kRndLevelItems = 6144;
+constexpr int kRndLevelItems = 2048;
 constexpr int kRndItemPairs = 1024;
 struct alignas(16) RndChunk {  // flat ranges of a chunk's items, pairs, staged values, rounds
     int i0, i1, p0, p1, s0, s1, r0, r1;
