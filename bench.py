@@ -302,7 +302,7 @@ def main():
     # dominant kernel, this rank: algorithmic bytes / average launch duration.
     # N = 1: the timed region is nothing but back-to-back launches of it; N > 1:
     # the same K steps again without the exchange (kernel-only), same stream.
-    per_step = -(-len(slices) // 16) if batches else len(slices)  # 16 matrices per batch launch
+    per_step = -(-len(slices) // 32) if batches else len(slices)  # 32 matrices per batch launch
     launches = args.steps * per_step
     if world == 1:
         kern_ms = e_start.elapsed_time(e_end)
@@ -419,7 +419,7 @@ def main():
                 "nnz_stored_total": int(sum(s.nnz_global for s in slices)),
                 "parallelism": f"row-partition x{world}" if world > 1 else "1 GPU",
                 "launch": "one rsp_spmv per matrix" if args.no_batch else
-                          (f"rsp_spmv_batch ({per_step} launch(es) of <= 16 matrices per step part): "
+                          (f"rsp_spmv_batch ({per_step} launch(es) of <= 32 matrices per step part): "
                            + ("interior, then boundary" if overlap else "whole step")),
                 "collective": (("halo all_to_all_single" + ("" if args.no_bucket else
                                  " (one per step, bucketed over the matrices)")

@@ -207,7 +207,7 @@ rsp_status_t rsp_spmv_part(rsp_handle_t handle, const void *alpha, rsp_spmat_t m
 
 /* Batched SpMV: y_j = alpha*A_j*x_j + beta*y_j for `count` independent
  * matrices of one compute type, as ONE kernel launch (plus one long-row
- * fixup launch when any A_j has rows longer than a tile) per 16 matrices.
+ * fixup launch when any A_j has rows longer than a tile) per 32 matrices.
  * No cuSPARSE counterpart: the reference calls cusparseSpMV once per matrix
  * (GPU/spmv.cu:179-186); this is the same product per matrix, bit for bit
  * equal to rsp_spmv / rsp_spmv_part on each, without the per-launch ramp and

@@ -79,7 +79,7 @@ struct SpmvArgs {
 // [longs.begin[j], longs.begin[j + 1]). The begin tables travel in the kernel
 // arguments (entries past `count` hold INT_MAX), so a workgroup finds its
 // matrix with scalar compares and loads its entry and its tile in parallel.
-constexpr int kSpmvBatchMax = 16;  // matrices per launch
+constexpr int kSpmvBatchMax = 32;  // matrices per launch
 struct alignas(16) SpmvBatchEntry {
     const int *rowptr;
     const int *colidx;

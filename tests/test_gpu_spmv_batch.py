@@ -1,7 +1,7 @@
 """GPU tests of the batched SpMV (rsp_spmv_batch_*, respasol_amd.sparse.SpmvBatch):
 every matrix of a batch gets exactly the bits of its own rsp_spmv /
 rsp_spmv_part call (which test_gpu_spmv.py pins to the oracle), for batches
-spanning several launches (> 16 matrices), long-row fixups, empty matrices,
+spanning several launches (> 32 matrices), long-row fixups, empty matrices,
 alpha/beta, fp32 with and without FTZ, the halo split (part 1 + part 2) and
 the kernel variants; a matrix re-planned after the batch was built is a
 status code, not a stale launch."""
@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 NP = {torch.float64: np.float64, torch.float32: np.float32}
 
 # short rows, rows just above the 256-thread threshold, chunked hub rows,
-# scattered columns, banded stencils; repeated to pass 16 matrices per launch
+# scattered columns, banded stencils; repeated to pass 32 matrices per launch
 NAMES = [("ecology2", 0.02), ("ASIC_320ks", 0.2), ("G2_circuit", 0.1), ("Serena", 0.01),
          ("cage13", 0.02), ("atmosmodd", 0.02), ("Si87H76", 0.05), ("af_shell10", 0.005)]
 
@@ -26,7 +26,7 @@ def same_bits(a, b):
                           b.view(np.uint64 if b.dtype == np.float64 else np.uint32))
 
 
-def build(handle, dtype, count=21, local_frac=None):
+def build(handle, dtype, count=37, local_frac=None):
     mats, xs, hosts = [], [], []
     for k in range(count):
         if k == 3:  # all-empty rows
