@@ -5,7 +5,7 @@
  * Build flags matter: -ffp-contract=off so `s += v * x` is a rounded
  * product then a rounded sum (the order the GPU tiles reproduce), and fma()
  * is called explicitly where the restated algorithm fuses (ILU updates and
- * triangular solves), which the GPU kernels mirror with __builtin_fma.
+ * triangular solves), which the GPU kernels mirror with v_fma_f64 / v_fma_f32 (fma_t).
  */
 #include "rsp_oracle.h"
 

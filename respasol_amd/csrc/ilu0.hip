@@ -49,6 +49,12 @@ using rsp::TrsvArgs;
 
 // ------------------------------------------------------------ per-row work
 
+// Fused multiply-add in the working precision: v_fma_f64 / v_fma_f32 (one
+// rounding), as the oracle's fma / fmaf. (__builtin_fma on float operands
+// would compute in double and round twice.)
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
 // s - sum_p v_p y_p as a serial fma chain over p = p0 .. p1-1, ascending.
 // The operands of B consecutive terms are loaded together (clamped,
 // unpredicated) so the loads of a batch overlap instead of serialising
@@ -67,7 +73,7 @@ __device__ __forceinline__ T fma_chain(T s, int p0, int p1, FV vat, FY yat) {
         }
 #pragma unroll
         for (int b = 0; b < B; ++b)
-            if (b0 + b < n) s = __builtin_fma(-v[b], y[b], s);
+            if (b0 + b < n) s = fma_t(-v[b], y[b], s);
     }
     return s;
 }
@@ -90,7 +96,7 @@ __device__ __forceinline__ T wave_chain(T s, int k0, int k1, int lane, FV vat, F
         const int k = min(base + lane, k1 - 1);
         const T v = vat(k), yv = yat(k);
         const int cnt = min(64, k1 - base);
-        for (int j = 0; j < cnt; ++j) s = __builtin_fma(-wave_read(v, j), wave_read(yv, j), s);
+        for (int j = 0; j < cnt; ++j) s = fma_t(-wave_read(v, j), wave_read(yv, j), s);
     }
     return s;
 }
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
             }
 #pragma unroll
             for (int b = 0; b < 4; ++b)
-                if (u + b < u1) v = __builtin_fma(-l[b], w[b], v);
+                if (u + b < u1) v = fma_t(-l[b], w[b], v);
         }
         if (r.z >= 0) v = v / V[r.z];
         V[cb + it] = v;
@@ -544,7 +550,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
 #pragma unroll
         for (int j = 0; j < G; ++j) yv[j] = yb(id.v[j]);
 #pragma unroll
-        for (int j = 0; j < G; ++j) s = __builtin_fma(-g.v[j], yv[j], s);
+        for (int j = 0; j < G; ++j) s = fma_t(-g.v[j], yv[j], s);
         return s;
     };
     auto row_value = [&](const ThinRow<T> &r) {  // one short row, groups in order
