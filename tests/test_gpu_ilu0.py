@@ -206,3 +206,26 @@ def test_empty_matrix(handle):
     il.factor(va)
     assert il.zero_pivot() == -1
     assert A.n == 0
+
+
+@pytest.mark.parametrize("thin_solve", [1024, 0])
+def test_fp32_fma_single_rounding(handle, monkeypatch, thin_solve):
+    """fp32 solves fuse in fp32 (one rounding, fmaf), not in double: for
+    a*b + c = 1 + 2^-23 + 2^-24 - 2^-60 (just below a float midpoint) fmaf
+    gives 1 + 2^-23, a double fma rounded to float gives 1 + 2^-22."""
+    monkeypatch.setenv("RSP_ILU_THIN_SOLVE", str(thin_solve))
+    a = np.float32(2.0 ** -12 * (1 + 2.0 ** -18))
+    b = np.float32(2.0 ** -12 * (1 - 2.0 ** -18))
+    c = np.float32(1 + 2.0 ** -23)
+    rp = np.array([0, 1, 3], np.int32)
+    ci = np.array([0, 0, 1], np.int32)
+    va_h = np.array([1.0, -float(a), 1.0], np.float64)  # L = [[1, 0], [-a, 1]]
+    rpd, cid, va = upload_csr(rp, ci, va_h, torch.float32)
+    il = Ilu0(handle, rpd, cid)
+    il.analysis()
+    il.factor(va)
+    x = torch.tensor([b, c], dtype=torch.float32, device="cuda")
+    z = il.solve_lower(va, x).cpu().numpy()
+    assert z[1] == np.float32(1 + 2.0 ** -23), z[1]
+    v, _, _ = ob.ilu0(rp, ci, va_h.astype(np.float32))
+    assert np.array_equal(z, ob.trsv("lower_n", rp, ci, v, np.array([b, c], np.float32)))
