@@ -69,7 +69,7 @@ def main():
     per_matrix = {"kernel": "rsp_k::spmv_tiles<double,true,false>",
                   "hbm_bytes_per_launch": round(hbm), "algorithmic_bytes_per_launch": round(algb),
                   "traffic_over_algorithmic": round(hbm / algb, 4)}
-    # batched launches (one per <= 16 matrices per pass): same correction
+    # batched launches (one per <= 32 matrices per pass): same correction
     fb = load(args.fetch, "FETCH_SIZE", "spmv_tiles_batch<double")
     wb = load(args.write, "WRITE_SIZE", "spmv_tiles_batch<double")
     batch = None
