@@ -15,6 +15,9 @@
 #include <algorithm>
 #include <memory>
 #include <new>
+#include <chrono>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "rsp_kernels.h"
@@ -1204,73 +1207,117 @@ static hipError_t upload(int **dst, const std::vector<int> &v) {
 // column -> position map, then each lower k (ascending) walks row k's upper
 // part; a hit at column j appends (pos l_ik, pos u_kj) to position (i, j).
 
+// Host worker threads for the analysis: OMP_NUM_THREADS (the box's share of
+// its cores; the machine may have many more) or the hardware count, <= 64.
+static int host_threads() {
+    int t = env_int("OMP_NUM_THREADS", 0);
+    if (t <= 0) t = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 64));
+}
+
+// f(r0, r1) over contiguous row blocks of [0, n) on host_threads() threads.
+}  // extern "C"
+template <typename F>
+static void parallel_rows(int n, F f) {
+    const int nt = n < 8192 ? 1 : host_threads();
+    if (nt == 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+        th.emplace_back(f, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
+    for (std::thread &x : th) x.join();
+}
+extern "C" {
+
 static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<int> &ci,
                          const std::vector<int> &dpos, const std::vector<int> &hasdiag,
                          IluSymbolic &s) {
     const int nnz = rp[(size_t)n];
-    std::vector<int> map((size_t)n, -1), cnt((size_t)nnz, 0);
-    // pass 1: counts
+    std::vector<int> cnt((size_t)nnz, 0);
+    // pass 1: counts (rows are independent: a row writes only its own
+    // positions' counts; each worker scatters its rows into its own map)
+    std::mutex mu;
     long long total = 0;
-    for (int i = 0; i < n; i++) {
-        for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
-        for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) {
-            const int k = ci[(size_t)p];
-            for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
-                const int t = map[(size_t)ci[(size_t)q]];
-                if (t > p) {
-                    cnt[(size_t)t]++;
-                    total++;
+    parallel_rows(n, [&](int r0, int r1) {
+        std::vector<int> map((size_t)n, -1);
+        long long part = 0;
+        for (int i = r0; i < r1; i++) {
+            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
+            for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) {
+                const int k = ci[(size_t)p];
+                for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
+                    const int t = map[(size_t)ci[(size_t)q]];
+                    if (t > p) {
+                        cnt[(size_t)t]++;
+                        part++;
+                    }
                 }
             }
+            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
         }
-        for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
-    }
+        std::lock_guard<std::mutex> g(mu);
+        total += part;
+    });
     if (total > INT_MAX) return false;
     s.upd_ptr.assign((size_t)nnz + 1, 0);
     for (int p = 0; p < nnz; p++) s.upd_ptr[(size_t)p + 1] = s.upd_ptr[(size_t)p] + cnt[(size_t)p];
     s.upd_l.resize((size_t)total);
     s.upd_u.resize((size_t)total);
-    std::vector<int> fill(s.upd_ptr.begin(), s.upd_ptr.end() - 1);
     // pass 2: fill (k ascending per target, since p ascends) + stages
     std::vector<int> &stage = s.stage;
     stage.assign((size_t)nnz, 0);
     s.lord.assign((size_t)nnz, 0);
     s.lend.assign((size_t)nnz, 0);
-    std::vector<int> order;
-    for (int i = 0; i < n; i++) {
-        const int rs = rp[(size_t)i], di = dpos[(size_t)i];
-        for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
-        for (int p = rs; p < di; p++) {
-            const int k = ci[(size_t)p];
-            for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
-                const int t = map[(size_t)ci[(size_t)q]];
-                if (t > p) {
-                    const int u = fill[(size_t)t]++;
-                    s.upd_l[(size_t)u] = p;
-                    s.upd_u[(size_t)u] = q;
-                    if (t < di) stage[(size_t)t] = std::max(stage[(size_t)t], stage[(size_t)p] + 1);
+    parallel_rows(n, [&](int r0, int r1) {
+        std::vector<int> map((size_t)n, -1), order;
+        for (int i = r0; i < r1; i++) {
+            const int rs = rp[(size_t)i], di = dpos[(size_t)i];
+            for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
+            for (int p = rs; p < rp[(size_t)i + 1]; p++) cnt[(size_t)p] = s.upd_ptr[(size_t)p];  // fill
+            for (int p = rs; p < di; p++) {
+                const int k = ci[(size_t)p];
+                for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
+                    const int t = map[(size_t)ci[(size_t)q]];
+                    if (t > p) {
+                        const int u = cnt[(size_t)t]++;
+                        s.upd_l[(size_t)u] = p;
+                        s.upd_u[(size_t)u] = q;
+                        if (t < di) stage[(size_t)t] = std::max(stage[(size_t)t], stage[(size_t)p] + 1);
+                    }
                 }
             }
+            for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
+            // lower positions by (stage, column)
+            order.assign((size_t)(di - rs), 0);
+            for (int p = rs; p < di; p++) order[(size_t)(p - rs)] = p;
+            std::stable_sort(order.begin(), order.end(),
+                             [&](int a, int b) { return stage[(size_t)a] < stage[(size_t)b]; });
+            for (int x = 0; x < di - rs; x++) s.lord[(size_t)(rs + x)] = order[(size_t)x];
+            for (int x = di - rs - 1; x >= 0; x--) {
+                const bool last = x == di - rs - 1 ||
+                                  stage[(size_t)order[(size_t)x]] != stage[(size_t)order[(size_t)x + 1]];
+                s.lend[(size_t)(rs + x)] = last ? rs + x + 1 : s.lend[(size_t)(rs + x + 1)];
+            }
         }
-        for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
-        // lower positions by (stage, column)
-        order.assign((size_t)(di - rs), 0);
-        for (int p = rs; p < di; p++) order[(size_t)(p - rs)] = p;
-        std::stable_sort(order.begin(), order.end(),
-                         [&](int a, int b) { return stage[(size_t)a] < stage[(size_t)b]; });
-        for (int x = 0; x < di - rs; x++) s.lord[(size_t)(rs + x)] = order[(size_t)x];
-        for (int x = di - rs - 1; x >= 0; x--) {
-            const bool last = x == di - rs - 1 ||
-                              stage[(size_t)order[(size_t)x]] != stage[(size_t)order[(size_t)x + 1]];
-            s.lend[(size_t)(rs + x)] = last ? rs + x + 1 : s.lend[(size_t)(rs + x + 1)];
-        }
-    }
+    });
     return true;
 }
 
 rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_offsets,
                                const int *d_col_ind, rsp_ilu0_info_t f) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    // diagnostics: RSP_ILU_TIMING=1 prints the wall time of each analysis phase
+    const bool timing = env_int("RSP_ILU_TIMING", 0) != 0;
+    auto t_last = std::chrono::steady_clock::now();
+    auto phase = [&](const char *what) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "rsp_ilu0_analysis n=%d %-14s %8.2f ms\n", n, what,
+                std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     if (!f || n < 0 || nnz < 0 || (n > 0 && !d_row_offsets)) return RSP_STATUS_INVALID_VALUE;
     ilu_free_device(f);
     f->analysed = 0;
@@ -1349,6 +1396,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         nlu = std::max(nlu, l + 1);
     }
     std::vector<int> rows_l, rows_lt, rows_u;
+    phase("copy+levels");
     group_levels(lv, nl, f->L.ptr, rows_l);
     group_levels(lvt, nlt, f->LT.ptr, rows_lt);
     group_levels(lvu, nlu, f->U.ptr, rows_u);
@@ -1356,10 +1404,9 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
     const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
     IluSymbolic sym;
+    phase("group");
     if (!ilu_symbolic(n, rp, ci, dpos, hasdiag, sym)) return RSP_STATUS_ALLOC_FAILED;
-    FacPlan fplan;
-    build_factor_plan(n, rp, ci, dpos, hasdiag, sym, f->L.ptr, rows_l, thin_factor, fplan);
-    f->fac_segs = fplan.segs;
+    phase("symbolic");
     f->n_updates = (long long)sym.upd_l.size();
     {
         long long nl = 0, nu = 0;
@@ -1373,6 +1420,40 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
             d->group = env_int("RSP_ILU_GROUP", d->batch == 2 ? 2 : 4) == 2 ? 2 : 4;
         f->fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
     }
+    // the factor plan and the three solve plans (flat terms in level order,
+    // thin-run chunks, y sources) are independent: built concurrently
+    FacPlan fplan;
+    SolvePlan sps[3];
+    std::vector<int> udiag((size_t)n);
+    for (int i = 0; i < n; i++) udiag[(size_t)i] = hasdiag[(size_t)i] ? dpos[(size_t)i] : -1;
+    {
+        std::vector<std::thread> th;
+        th.emplace_back([&] {
+            build_factor_plan(n, rp, ci, dpos, hasdiag, sym, f->L.ptr, rows_l, thin_factor, fplan);
+        });
+        th.emplace_back([&] {
+            build_solve_plan(n, f->L.ptr, rows_l, thin_solve, f->L.group, std::vector<int>(),
+                             [&](int i, auto emit) {
+                                 for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
+                             }, sps[0]);
+        });
+        th.emplace_back([&] {
+            build_solve_plan(n, f->LT.ptr, rows_lt, thin_solve, f->LT.group, std::vector<int>(),
+                             [&](int i, auto emit) {
+                                 for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++)
+                                     emit(lts[(size_t)q], ltc[(size_t)q]);
+                             }, sps[1]);
+        });
+        th.emplace_back([&] {
+            build_solve_plan(n, f->U.ptr, rows_u, thin_solve, f->U.group, udiag, [&](int i, auto emit) {
+                for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++)
+                    emit(p, ci[(size_t)p]);
+            }, sps[2]);
+        });
+        for (std::thread &x : th) x.join();
+    }
+    phase("plans");
+    f->fac_segs = fplan.segs;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = upload_vec(&f->d_rchunks, fplan.chunks);
     if (e == hipSuccess) e = upload_vec(&f->d_ritems, fplan.items);
@@ -1392,25 +1473,9 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     if (e == hipSuccess) e = upload(&f->LT.d_ptr, f->LT.ptr);
     if (e == hipSuccess) e = upload(&f->U.d_rows, rows_u);
     if (e == hipSuccess) e = upload(&f->U.d_ptr, f->U.ptr);
-    // solve plans (flat terms in level order, thin-run chunks, y sources)
-    std::vector<int> udiag((size_t)n);
-    for (int i = 0; i < n; i++) udiag[(size_t)i] = hasdiag[(size_t)i] ? dpos[(size_t)i] : -1;
     for (int kind = 0; kind < 3 && e == hipSuccess; kind++) {
         rsp_ilu0_info::Dag &d = kind == 0 ? f->L : (kind == 1 ? f->LT : f->U);
-        SolvePlan sp;
-        if (kind == 0)
-            build_solve_plan(n, d.ptr, rows_l, thin_solve, d.group, std::vector<int>(), [&](int i, auto emit) {
-                for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
-            }, sp);
-        else if (kind == 1)
-            build_solve_plan(n, d.ptr, rows_lt, thin_solve, d.group, std::vector<int>(), [&](int i, auto emit) {
-                for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++) emit(lts[(size_t)q], ltc[(size_t)q]);
-            }, sp);
-        else
-            build_solve_plan(n, d.ptr, rows_u, thin_solve, d.group, udiag, [&](int i, auto emit) {
-                for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++)
-                    emit(p, ci[(size_t)p]);
-            }, sp);
+        SolvePlan &sp = sps[kind];
         d.segs = sp.segs;
         d.nshort = sp.nshort;
         e = upload_vec(&d.d_tasks, sp.tasks);
@@ -1431,6 +1496,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     }
     if (e == hipSuccess) e = hipMalloc((void **)&f->d_zero, sizeof(int));
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
+    phase("uploads");
     if (e != hipSuccess) {
         ilu_free_device(f);
         return e == hipErrorOutOfMemory ? RSP_STATUS_ALLOC_FAILED : RSP_STATUS_EXECUTION_FAILED;
