@@ -143,6 +143,23 @@ def test_ilu0_numerical_zero_pivot():
     assert sz == -1 and zp == 1
 
 
+def test_fp32_solve_fuses_with_one_rounding():
+    """The oracle's fp32 solve fuses with fmaf (one rounding); the HIP kernels
+    mirror it (tests/test_gpu_ilu0.py::test_fp32_fma_single_rounding). For
+    a*b + c = 1 + 2^-23 + 2^-24 - 2^-60, just below a float midpoint, one
+    rounding gives 1 + 2^-23; a double fma rounded to float gives 1 + 2^-22."""
+    a = np.float32(2.0 ** -12 * (1 + 2.0 ** -18))
+    b = np.float32(2.0 ** -12 * (1 - 2.0 ** -18))
+    c = np.float32(1 + 2.0 ** -23)
+    rp = np.array([0, 1, 3], np.int32)
+    ci = np.array([0, 0, 1], np.int32)
+    v = np.array([1.0, -a, 1.0], np.float32)  # L = [[1, 0], [-a, 1]]
+    z = ob.trsv("lower_n", rp, ci, v, np.array([b, c], np.float32))
+    assert z[0] == b
+    assert z[1] == np.float32(1 + 2.0 ** -23)
+    assert np.float32(np.float64(c) + np.float64(a) * np.float64(b)) == np.float32(1 + 2.0 ** -22)
+
+
 def test_ftz_oracle_flushes_subnormals():
     rp = np.array([0, 2], np.int32)
     ci = np.array([0, 1], np.int32)
