@@ -147,12 +147,94 @@ __device__ __forceinline__ void lds_barrier() {
 
 // --------------------------------------------------------------- kernels
 
-// Fat level: one wave per row.
+// Fat level, global-memory path: one wave per row.
 template <typename T, int B>
 __global__ __launch_bounds__(64 * kIluWaves) void ilu0_level(IluArgs a, int off, int nrows) {
     const int w = blockIdx.x * kIluWaves + (threadIdx.x >> 6);
     if (w >= nrows) return;
     factor_row<T, B>(a, a.plan.rows[off + w], threadIdx.x & 63);
+}
+
+// Fat level, one wave (workgroup) per row with the row staged in LDS. Every
+// operand that does not come from the row itself is final before the level
+// starts: the u_kj of all the row's update pairs (rows of earlier levels)
+// and its divisors u_kk. So they, the row's values and its stage structure
+// are loaded up front in a few independent memory round trips; the stages
+// then run on LDS operands only (an l_ik of an earlier stage is the row's own
+// LDS value; one wave's LDS accesses are in order), and the row is written
+// back once. Same per-position fma sequence and division as factor_row, so
+// bitwise equal to it. Rows beyond kFacRow entries or kFacPairs pairs take
+// the global path (factor_row).
+template <typename T, int B>
+__global__ __launch_bounds__(64) void ilu0_level_lds(IluArgs a, int off) {
+    constexpr int R = rsp::kFacRow, Q = rsp::kFacPairs;
+    __shared__ T rv[R], dv[R], pu[Q];
+    __shared__ int up[R + 1], lo[R], le[R];
+    __shared__ unsigned short pl[Q];
+    const int lane = threadIdx.x;
+    const rsp::FacRow fr = a.frow[off + blockIdx.x];
+    T *vals = (T *)a.vals;
+    const int i = fr.i, rs = fr.rs, re = fr.re, q0 = fr.q0;
+    const int nr = re - rs, nq = fr.q1 - q0, nlo = fr.di - rs;
+    if (nr > R || nq > Q) {
+        factor_row<T, B>(a, i, lane);
+        return;
+    }
+    for (int x = lane; x < nr; x += 64) {
+        const bool lower = x < nlo;
+        const int d = lower ? a.udiv[rs + x] : -1;
+        rv[x] = vals[rs + x];
+        dv[x] = d >= 0 ? vals[d] : T(0);
+        up[x] = a.upd_ptr[rs + x] - q0;
+        if (lower) {
+            lo[x] = a.lord[rs + x] - rs;
+            le[x] = a.lend[rs + x] - rs;
+        }
+    }
+    if (lane == 0) up[nr] = nq;
+    for (int u = lane; u < nq; u += 64) {
+        pl[u] = (unsigned short)(a.upd_l[q0 + u] - rs);
+        pu[u] = vals[a.upd_u[q0 + u]];
+    }
+    auto wave_sync = [] {  // order this wave's LDS stores before its later loads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    };
+    wave_sync();
+    auto entry = [&](int x) {  // a_ij - sum l_ik u_kj over its pairs, k ascending
+        T v = rv[x];
+        const int u0 = up[x], u1 = up[x + 1];
+        for (int u = u0; u < u1; u += 4) {
+            T l[4], w[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int uu = min(u + b, u1 - 1);
+                l[b] = rv[pl[uu]];
+                w[b] = pu[uu];
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (u + b < u1) v = fma_t(-l[b], w[b], v);
+        }
+        return v;
+    };
+    for (int s = 0; s < nlo;) {  // lower positions, stage by stage
+        const int e = le[s];
+        for (int x = s + lane; x < e; x += 64) {
+            const int r = lo[x];
+            rv[r] = entry(r) / dv[r];
+        }
+        wave_sync();
+        s = e;
+    }
+    for (int x = nlo + lane; x < nr; x += 64) {  // upper positions (never operands of this row)
+        const T v = entry(x);
+        rv[x] = v;
+        if (x == nlo && fr.hasdiag && v == T(0)) atomicMin(a.zero_pivot, i);
+    }
+    wave_sync();
+    for (int x = lane; x < nr; x += 64) vals[rs + x] = rv[x];
 }
 
 // Thin run of the factor in ROUNDS (plan: build_factor_plan; rsp::RndChunk,
@@ -328,32 +410,70 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
 // flat terms: y_i = (alpha x_i - sum_k vals[tpos[k]] * y[src[k]]) (/ u_ii),
 // one fma per term in the term order (for L^T: j descending).
 
-// Fat level, terms straight from global memory: blocks [0, nb) one thread
-// per short row (the level's first nshort rows), the blocks after them one
-// wave per long row.
+// s - sum v_k y[src_k] over k = k0 .. k1-1 in order, from the solve streams
+// (term values in flat order, no position indirection). The values and y
+// indices of batch j+1 are loaded while batch j's y gather is in flight (the
+// loads are clamped, unpredicated), so a batch costs one memory round trip.
+template <typename T, int B>
+__device__ __forceinline__ T stream_chain(T s, int k0, int k1, const T *sval, const int *src, const T *y) {
+    const int n = k1 - k0;
+    if (n <= 0) return s;
+    T v[B];
+    int id[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int k = k0 + min(b, n - 1);
+        v[b] = sval[k];
+        id[b] = src[k];
+    }
+    for (int b0 = 0; b0 < n; b0 += B) {
+        T yv[B], vc[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            yv[b] = y[id[b]];
+            vc[b] = v[b];
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int k = k0 + min(b0 + B + b, n - 1);
+            v[b] = sval[k];
+            id[b] = src[k];
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (b0 + b < n) s = fma_t(-vc[b], yv[b], s);
+    }
+    return s;
+}
+
+// Fat level, terms from the solve streams (trsv_stream): blocks [0, nb) one
+// thread per short row (the level's first nshort rows), the blocks after them
+// one wave per long row. Slot off + r of the level order: task, alpha x_i
+// (and u_ii) at the same index, so the row's first loads are independent.
 template <typename T, int KIND, int B>
-__global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, T alpha, int off, int nrows,
-                                                  int nshort, int nb) {
-    const T *vals = (const T *)a.vals;
+__global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows, int nshort, int nb) {
+    const T *sval = (const T *)a.sval;
     T *y = (T *)a.y;
-    const int *tpos = a.plan.tpos, *src = a.plan.src;
-    auto vat = [&](int k) { return vals[tpos[k]]; };
-    auto yat = [&](int k) { return y[src[k]]; };
+    const int *src = a.plan.src;
+    int x;
     T s;
     rsp::RowTask t;
     if ((int)blockIdx.x < nb) {
         const int r = blockIdx.x * 256 + threadIdx.x;
         if (r >= nshort) return;
-        t = a.plan.tasks[off + r];
-        s = fma_chain<T, B>(alpha * ((const T *)a.x)[t.i], t.t0, t.t1, vat, yat);
+        x = off + r;
+        t = a.plan.tasks[x];
+        s = stream_chain<T, B>(((const T *)a.sx)[x], t.t0, t.t1, sval, src, y);
     } else {
         const int r = nshort + (blockIdx.x - nb) * 4 + (threadIdx.x >> 6);
         if (r >= nrows) return;
-        t = a.plan.tasks[off + r];
-        s = wave_chain<T>(alpha * ((const T *)a.x)[t.i], t.t0, t.t1, threadIdx.x & 63, vat, yat);
+        x = off + r;
+        t = a.plan.tasks[x];
+        s = wave_chain<T>(((const T *)a.sx)[x], t.t0, t.t1, threadIdx.x & 63,
+                          [&](int k) { return sval[k]; }, [&](int k) { return y[src[k]]; });
         if ((threadIdx.x & 63) != 0) return;
     }
-    if constexpr (KIND == 2) s = s / (t.d >= 0 ? vals[t.d] : T(0));
+    if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
     y[t.i] = s;
 }
 
@@ -722,8 +842,11 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
         for (int l = sg.lb; l < sg.le; ++l) {
             const int off = P.ptr_host[l], cnt = P.ptr_host[l + 1] - off;
             if (cnt <= 0) continue;
-            hipLaunchKernelGGL((ilu0_level<T, B>), dim3((cnt + kIluWaves - 1) / kIluWaves),
-                               dim3(64 * kIluWaves), 0, s, a, off, cnt);
+            if (a.fat_lds)
+                hipLaunchKernelGGL((ilu0_level_lds<T, B>), dim3(cnt), dim3(64), 0, s, a, off);
+            else
+                hipLaunchKernelGGL((ilu0_level<T, B>), dim3((cnt + kIluWaves - 1) / kIluWaves),
+                                   dim3(64 * kIluWaves), 0, s, a, off, cnt);
         }
     }
     return hipGetLastError();
@@ -733,11 +856,9 @@ template <typename T, int KIND, int B>
 static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
     const LevelPlan &P = a.plan;
     const T alpha = (T)a.alpha;
-    bool any_thin = false;
-    for (int g = 0; g < P.nseg; ++g) any_thin |= P.segs[g].thin != 0;
-    if (any_thin) {  // the streams the thin runs stage
+    {  // the streams every level reads (term values, alpha x_i, u_ii in level order)
         const int nk = max(P.nterms, a.n);
-        hipLaunchKernelGGL((trsv_stream<T, KIND>), dim3((nk + 255) / 256), dim3(256), 0, s, a, alpha);
+        if (nk > 0) hipLaunchKernelGGL((trsv_stream<T, KIND>), dim3((nk + 255) / 256), dim3(256), 0, s, a, alpha);
     }
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
@@ -756,7 +877,7 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             if (cnt <= 0) continue;
             const int ns = P.nshort_host[l], nb = (ns + 255) / 256;
             hipLaunchKernelGGL((trsv_level<T, KIND, B>), dim3(nb + (cnt - ns + 3) / 4), dim3(256), 0,
-                               s, a, alpha, off, cnt, ns, nb);
+                               s, a, off, cnt, ns, nb);
         }
     }
     return hipGetLastError();

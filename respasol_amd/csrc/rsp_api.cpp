@@ -60,7 +60,7 @@ struct rsp_ilu0_info {
     int structural_zero;         // -1 = none
     int factored;
     int *d_dpos, *d_hasdiag;
-    int *d_upd_ptr, *d_upd_l, *d_upd_u, *d_lord, *d_lend;
+    int *d_upd_ptr, *d_upd_l, *d_upd_u, *d_lord, *d_lend, *d_udiv;
     int *d_zero;
     long long n_updates;
     // one level set per DAG: L (factor + L solve), L^T, U
@@ -84,6 +84,7 @@ struct rsp_ilu0_info {
     void *d_sval = nullptr, *d_sx = nullptr, *d_sdg = nullptr;  // solve streams (trsv_stream)
     rsp::RndChunk *d_rchunks = nullptr;        // round-based factor chunks (thin runs)
     rsp::RndItem *d_ritems = nullptr;
+    rsp::FacRow *d_frow = nullptr;
     int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
     int fac_batch;
 };
@@ -748,7 +749,7 @@ static void ilu_free_device(rsp_ilu0_info *f) {
                     &f->LT.d_rows,  &f->LT.d_ptr,  &f->U.d_rows,  &f->U.d_ptr,
                     &f->d_zero,
                     &f->d_upd_ptr,  &f->d_upd_l,   &f->d_upd_u,   &f->d_lord,
-                    &f->d_lend};
+                    &f->d_lend,     &f->d_udiv};
     for (int **p : ptrs) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
@@ -757,7 +758,7 @@ static void ilu_free_device(rsp_ilu0_info *f) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
-    for (void **p : {(void **)&f->d_rchunks, (void **)&f->d_ritems, (void **)&f->d_rpairs,
+    for (void **p : {(void **)&f->d_frow, (void **)&f->d_rchunks, (void **)&f->d_ritems, (void **)&f->d_rpairs,
                      (void **)&f->d_rstaged, (void **)&f->d_rrounds}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
@@ -781,7 +782,7 @@ rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
     f->factored = 0;
     f->d_dpos = f->d_hasdiag = nullptr;
     f->d_zero = nullptr;
-    f->d_upd_ptr = f->d_upd_l = f->d_upd_u = f->d_lord = f->d_lend = nullptr;
+    f->d_upd_ptr = f->d_upd_l = f->d_upd_u = f->d_lord = f->d_lend = f->d_udiv = nullptr;
     f->n_updates = 0;
     *info = f;
     return RSP_STATUS_SUCCESS;
@@ -857,19 +858,7 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
                              int thin_rows, int group, const std::vector<int> &diag,
                              RowTerms row_terms, SolvePlan &sp) {
     const int nlev = (int)ptr.size() - 1;
-    // within each level: rows of <= kLongTerms terms first (a thread each),
-    // longer rows after them (a wave each)
     std::vector<int> order(rows);
-    sp.nshort.assign((size_t)std::max(nlev, 1), 0);
-    for (int l = 0; l < nlev; l++) {
-        auto b = order.begin() + ptr[(size_t)l], e = order.begin() + ptr[(size_t)l + 1];
-        auto mid = std::stable_partition(b, e, [&](int i) {
-            int cnt = 0;
-            row_terms(i, [&](int, int) { cnt++; });
-            return cnt <= rsp::kLongTerms;
-        });
-        sp.nshort[(size_t)l] = (int)(mid - b);
-    }
     // segments: runs of thin levels / fat levels. A thin level's rows have
     // their terms padded to whole groups of `group` (at least one group):
     // pads are (position -1, source kPadSrc), i.e. a zero value times the zero
@@ -897,6 +886,18 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     std::vector<char> thin_lev((size_t)std::max(nlev, 1), 0);
     for (const rsp::LevelSeg &sg : sp.segs)
         for (int l = sg.lb; l < sg.le; l++) thin_lev[(size_t)l] = (char)sg.thin;
+    // within each level: short rows first (a thread each), longer rows after
+    // them (a wave each). Short: <= kLongTerms terms in a thin run (LDS
+    // operands); <= kFatLongTerms in a fat level, where a thread pays one
+    // global round trip per batch of terms and a wave one per 64 terms.
+    const int fat_long = env_int("RSP_ILU_FAT_LONG", rsp::kFatLongTerms);
+    sp.nshort.assign((size_t)std::max(nlev, 1), 0);
+    for (int l = 0; l < nlev; l++) {
+        const int lim = thin_lev[(size_t)l] ? rsp::kLongTerms : fat_long;
+        auto b = order.begin() + ptr[(size_t)l], e = order.begin() + ptr[(size_t)l + 1];
+        auto mid = std::stable_partition(b, e, [&](int i) { return nterms(i) <= lim; });
+        sp.nshort[(size_t)l] = (int)(mid - b);
+    }
     std::vector<int> col;
     sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
     sp.tpos.clear();
@@ -1465,6 +1466,22 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     if (e == hipSuccess) e = upload(&f->d_upd_u, sym.upd_u);
     if (e == hipSuccess) e = upload(&f->d_lord, sym.lord);
     if (e == hipSuccess) e = upload(&f->d_lend, sym.lend);
+    {  // per lower position (i, k): the position of its divisor u_kk (-1: none, or upper)
+        std::vector<int> udiv((size_t)nnz_s, -1);
+        for (int i = 0; i < n; i++)
+            for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) {
+                const int k = ci[(size_t)p];
+                if (hasdiag[(size_t)k]) udiv[(size_t)p] = dpos[(size_t)k];
+            }
+        if (e == hipSuccess) e = upload(&f->d_udiv, udiv);
+        std::vector<rsp::FacRow> frow(std::max<size_t>(rows_l.size(), 1), rsp::FacRow{});
+        for (size_t x = 0; x < rows_l.size(); x++) {
+            const int i = rows_l[x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
+            frow[x] = rsp::FacRow{i, rs, dpos[(size_t)i], re, sym.upd_ptr[(size_t)rs], sym.upd_ptr[(size_t)re],
+                                  hasdiag[(size_t)i], 0};
+        }
+        if (e == hipSuccess) e = upload_vec(&f->d_frow, frow);
+    }
     if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
     if (e == hipSuccess) e = upload(&f->d_hasdiag, hasdiag);
     if (e == hipSuccess) e = upload(&f->L.d_rows, rows_l);
@@ -1578,6 +1595,9 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.upd_u = f->d_upd_u;
     a.lord = f->d_lord;
     a.lend = f->d_lend;
+    a.udiv = f->d_udiv;
+    a.frow = f->d_frow;
+    a.fat_lds = env_int("RSP_ILU_FAT_LDS", 1) != 0;
     a.rchunks = f->d_rchunks;
     a.ritems = f->d_ritems;
     a.rpairs = f->d_rpairs;

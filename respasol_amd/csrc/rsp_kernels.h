@@ -159,17 +159,20 @@ struct LevelPlan {
     const int *sid;       // thin runs: per term, its y's index in the LDS y buffer
     const StagedTerm *stg;  // thin runs: staged terms, per chunk [st0, st1)
     int nterms;           // flat terms
-    const int *nshort;    // per level: rows with <= kLongTerms terms come first (host copy: nshort_host)
+    const int *nshort;    // per level: short rows come first (host copy: nshort_host)
     const int *nshort_host;
 };
-constexpr int kLongTerms = 64;       // solve rows with more terms are done by a whole wave
+constexpr int kLongTerms = 64;       // thin-run solve rows with more terms are done by a whole wave
+constexpr int kFatLongTerms = 8;     // fat-level solve rows with more terms: a wave each (RSP_ILU_FAT_LONG)
 constexpr int kYWin = 4096;          // LDS y window of a thin solve run (entries, power of 2)
 constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin)
 constexpr int kChunkTerms = 4096;    // terms staged per thin-run chunk
 constexpr int kThinThreads = 1024;   // workgroup of a thin segment
 constexpr int kGroup = 4;            // thin-run rows: terms padded to whole groups of (at most) this many
 constexpr int kPadSrc = -(kYWin + 1); // source of a pad term: the zero slot after the y window
-constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels)
+constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels, global path)
+constexpr int kFacRow = 256;         // fat factor levels: rows staged in LDS up to this many entries
+constexpr int kFacPairs = 1024;      // ... and this many update pairs (else the global path)
 constexpr int kThinSolveRows = 1024; // solve levels this small (and <= kChunkTerms terms) run thin
 constexpr int kThinFactorRows = 1024; // factor levels this small (and within kRndLevelItems) run thin
 // LDS-staged factor chunks (ilu0_chunked): a chunk is a run of levels whose
@@ -196,6 +199,12 @@ struct alignas(16) RndItem {
     int pos, u, d, zr;
 };
 
+// A row of a fat factor level (level-order slot): its row, entry range with
+// the diagonal split, its update-pair range, whether it has a diagonal.
+struct alignas(16) FacRow {
+    int i, rs, di, re, q0, q1, hasdiag, pad;
+};
+
 struct IluArgs {
     int n;
     const int *rowptr;
@@ -216,6 +225,9 @@ struct IluArgs {
     // lord = position, lend = one past the last slot of the slot's stage.
     const int *lord;
     const int *lend;
+    const int *udiv;      // lower position (i, k): position of u_kk, -1 if row k has no diagonal
+    const FacRow *frow;   // per level-order slot of the L DAG (ilu0_level_lds)
+    int fat_lds;          // fat levels: rows staged in LDS (ilu0_level_lds; RSP_ILU_FAT_LDS=0: global path)
     LevelPlan plan;       // L DAG, factor thresholds
     // round-based thin runs (ilu0_rounds), see RndChunk / RndItem
     const RndChunk *rchunks;
