@@ -446,19 +446,70 @@ __device__ __forceinline__ T stream_chain(T s, int k0, int k1, const T *sval, co
     return s;
 }
 
+// The serial chain of one hub row (thousands of terms) by a 256-thread
+// workgroup: waves 1-3 gather the terms group by group (768 a group: value
+// and y index, then the y) into an LDS double buffer while wave 0 runs the
+// chain over the previous group on broadcast LDS operands, one fma per term
+// in order. A wave alone paid two dependent global round trips per 64 terms.
+// The result is valid in wave 0.
+template <typename T>
+__device__ __forceinline__ T block_chain(T s, int k0, int k1, const T *sval, const int *src, const T *y) {
+    constexpr int NL = 192, PER = 4, GS = NL * PER;
+    __shared__ T bv[2][GS], by[2][GS];
+    const int tid = threadIdx.x, n = k1 - k0, ng = (n + GS - 1) / GS;
+    auto gather = [&](int g) {  // loader waves: group g into buffer g & 1
+        T v[PER], yv[PER];
+        int id[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int k = min(g * GS + (tid - 64) + j * NL, n - 1);
+            v[j] = sval[k0 + k];
+            id[j] = src[k0 + k];
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) yv[j] = y[id[j]];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            bv[g & 1][(tid - 64) + j * NL] = v[j];
+            by[g & 1][(tid - 64) + j * NL] = yv[j];
+        }
+    };
+    if (tid >= 64) gather(0);
+    __syncthreads();
+    for (int g = 0; g < ng; ++g) {
+        if (tid >= 64) {
+            if (g + 1 < ng) gather(g + 1);
+        } else {
+            const T *pv = bv[g & 1], *py = by[g & 1];
+            const int cnt = min(GS, n - g * GS);
+#pragma unroll 8
+            for (int j = 0; j < cnt; ++j) s = fma_t(-pv[j], py[j], s);
+        }
+        __syncthreads();
+    }
+    return s;
+}
+
 // Fat level, terms from the solve streams (trsv_stream): blocks [0, nb) one
-// thread per short row (the level's first nshort rows), the blocks after them
-// one wave per long row. Slot off + r of the level order: task, alpha x_i
-// (and u_ii) at the same index, so the row's first loads are independent.
+// thread per short row (the level's first nshort rows), the next nwb blocks
+// one wave per long row (rows up to nwave), the blocks after them one hub row
+// each. Slot off + r of the level order: task, alpha x_i (and u_ii) at the
+// same index, so the row's first loads are independent.
 template <typename T, int KIND, int B>
-__global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows, int nshort, int nb) {
+__global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows, int nshort, int nb,
+                                                  int nwave, int nwb) {
     const T *sval = (const T *)a.sval;
     T *y = (T *)a.y;
     const int *src = a.plan.src;
     int x;
     T s;
     rsp::RowTask t;
-    if ((int)blockIdx.x < nb) {
+    if ((int)blockIdx.x >= nb + nwb) {  // hub row: the whole workgroup (uniform branch)
+        x = off + nwave + (blockIdx.x - nb - nwb);
+        t = a.plan.tasks[x];
+        s = block_chain<T>(((const T *)a.sx)[x], t.t0, t.t1, sval, src, y);
+        if (threadIdx.x != 0) return;
+    } else if ((int)blockIdx.x < nb) {
         const int r = blockIdx.x * 256 + threadIdx.x;
         if (r >= nshort) return;
         x = off + r;
@@ -466,7 +517,7 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
         s = stream_chain<T, B>(((const T *)a.sx)[x], t.t0, t.t1, sval, src, y);
     } else {
         const int r = nshort + (blockIdx.x - nb) * 4 + (threadIdx.x >> 6);
-        if (r >= nrows) return;
+        if (r >= nwave) return;
         x = off + r;
         t = a.plan.tasks[x];
         s = wave_chain<T>(((const T *)a.sx)[x], t.t0, t.t1, threadIdx.x & 63,
@@ -876,8 +927,9 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             const int off = P.ptr_host[l], cnt = P.ptr_host[l + 1] - off;
             if (cnt <= 0) continue;
             const int ns = P.nshort_host[l], nb = (ns + 255) / 256;
-            hipLaunchKernelGGL((trsv_level<T, KIND, B>), dim3(nb + (cnt - ns + 3) / 4), dim3(256), 0,
-                               s, a, off, cnt, ns, nb);
+            const int nw = P.nwave_host ? P.nwave_host[l] : cnt, nwb = (nw - ns + 3) / 4;
+            hipLaunchKernelGGL((trsv_level<T, KIND, B>), dim3(nb + nwb + (cnt - nw)), dim3(256), 0,
+                               s, a, off, cnt, ns, nb, nw, nwb);
         }
     }
     return hipGetLastError();

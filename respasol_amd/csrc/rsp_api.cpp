@@ -76,6 +76,7 @@ struct rsp_ilu0_info {
         int nterms = 0;                        // solve: flat terms
         int *d_nshort = nullptr;               // solve: short rows per level (device)
         std::vector<int> nshort;               // (host)
+        std::vector<int> nwave;                // solve: short + wave rows per level (host)
         std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
         int batch = 8;                         // solve fma-chain batch
         int group = 4;                         // thin-run term groups (2 or 4)
@@ -843,6 +844,7 @@ static int chain_batch(long long total, long long count) {
 // run, so its store is visible after the chunk's full barrier).
 struct SolvePlan {
     std::vector<int> nshort;  // per level
+    std::vector<int> nwave;   // per level: short + wave rows (the rest: hub rows)
     std::vector<rsp::RowTask> tasks;
     std::vector<int> tpos, src;
     std::vector<rsp::LevelSeg> segs;
@@ -890,13 +892,18 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     // them (a wave each). Short: <= kLongTerms terms in a thin run (LDS
     // operands); <= kFatLongTerms in a fat level, where a thread pays one
     // global round trip per batch of terms and a wave one per 64 terms.
+    // A fat level's rows of > kHubTerms terms come last, a workgroup each.
     const int fat_long = env_int("RSP_ILU_FAT_LONG", rsp::kFatLongTerms);
+    const int hub = env_int("RSP_ILU_HUB", rsp::kHubTerms);
     sp.nshort.assign((size_t)std::max(nlev, 1), 0);
+    sp.nwave.assign((size_t)std::max(nlev, 1), 0);
     for (int l = 0; l < nlev; l++) {
         const int lim = thin_lev[(size_t)l] ? rsp::kLongTerms : fat_long;
         auto b = order.begin() + ptr[(size_t)l], e = order.begin() + ptr[(size_t)l + 1];
         auto mid = std::stable_partition(b, e, [&](int i) { return nterms(i) <= lim; });
         sp.nshort[(size_t)l] = (int)(mid - b);
+        auto hb = thin_lev[(size_t)l] ? e : std::stable_partition(mid, e, [&](int i) { return nterms(i) <= hub; });
+        sp.nwave[(size_t)l] = (int)(hb - b);
     }
     std::vector<int> col;
     sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
@@ -1495,6 +1502,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         SolvePlan &sp = sps[kind];
         d.segs = sp.segs;
         d.nshort = sp.nshort;
+        d.nwave = sp.nwave;
         e = upload_vec(&d.d_tasks, sp.tasks);
         if (e == hipSuccess) e = upload_vec(&d.d_nshort, sp.nshort);
         if (e == hipSuccess) e = upload_vec(&d.d_tpos, sp.tpos);
@@ -1573,6 +1581,7 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<
     p.nterms = d.nterms;
     p.nshort = d.d_nshort;
     p.nshort_host = d.nshort.data();
+    p.nwave_host = d.nwave.empty() ? nullptr : d.nwave.data();
     return p;
 }
 

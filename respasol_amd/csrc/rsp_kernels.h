@@ -161,8 +161,10 @@ struct LevelPlan {
     int nterms;           // flat terms
     const int *nshort;    // per level: short rows come first (host copy: nshort_host)
     const int *nshort_host;
+    const int *nwave_host;  // per level: short + wave rows (fat solve levels; the rest are hub rows)
 };
 constexpr int kLongTerms = 64;       // thin-run solve rows with more terms are done by a whole wave
+constexpr int kHubTerms = 256;       // fat-level solve rows with more terms: a workgroup each (RSP_ILU_HUB)
 constexpr int kFatLongTerms = 8;     // fat-level solve rows with more terms: a wave each (RSP_ILU_FAT_LONG)
 constexpr int kYWin = 4096;          // LDS y window of a thin solve run (entries, power of 2)
 constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin)
