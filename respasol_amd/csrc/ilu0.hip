@@ -391,8 +391,13 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
     Recs R = load_recs(rc);
     Pre P = load_pre(rc, R);
     Recs Rn = load_recs(rn);
+    auto mark = [&](int c, int j, unsigned long long v) {  // diagnostics only (RSP_ILU_FTRACE)
+        if (a.trace && tid == 0 && 4 * c + j < a.trace_cap) a.trace[4 * c + j] = v;
+    };
     for (int c = c0; c < c1; ++c) {
+        mark(c, 0, clock64());
         stage(c, rc, R, P);
+        mark(c, 1, clock64());
         const rsp::RndChunk cur = rc;
         if (c + 1 < c1) {
             const rsp::RndChunk r2 = chunk(min(c + 2, cl));
@@ -403,6 +408,8 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
             rn = r2;
         }
         rounds(c, cur);
+        mark(c, 2, clock64());
+        mark(c, 3, (unsigned long long)(cur.r1 - cur.r0) | (unsigned long long)(cur.i1 - cur.i0) << 32);
     }
 }
 

@@ -1613,11 +1613,38 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.rstaged = f->d_rstaged;
     a.rrounds = f->d_rrounds;
     a.plan = level_plan(f->L, f->fac_segs, f->fac_batch);
+    // diagnostics: RSP_ILU_FTRACE=<file> appends per-chunk shader-clock stamps
+    // of the thin factor runs (host-blocking; never set in timed runs)
+    const char *trace_file = getenv("RSP_ILU_FTRACE");
+    static unsigned long long *d_trace = nullptr;
+    const int trace_cap = 1 << 22;
+    a.trace = nullptr;
+    a.trace_cap = 0;
+    if (trace_file) {
+        if (!d_trace) RSP_CHECK_HIP(hipMalloc((void **)&d_trace, trace_cap * sizeof(unsigned long long)));
+        RSP_CHECK_HIP(hipMemsetAsync(d_trace, 0, trace_cap * sizeof(unsigned long long), h->stream));
+        a.trace = d_trace;
+        a.trace_cap = trace_cap;
+    }
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::ilu0_factor_f64(a, h->stream);
     else
         e = h->ftz ? rsp_k_ftz::ilu0_factor_f32(a, h->stream) : rsp_k::ilu0_factor_f32(a, h->stream);
+    if (trace_file && e == hipSuccess) {
+        std::vector<unsigned long long> t(trace_cap);
+        RSP_CHECK_HIP(hipMemcpyAsync(t.data(), d_trace, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost,
+                                     h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+        if (FILE *fp = fopen(trace_file, "a")) {
+            fprintf(fp, "# factor n=%d\n", f->n);
+            for (int c = 0; c < trace_cap / 4; c++)
+                if (t[4 * (size_t)c])
+                    fprintf(fp, "%d %llu %llu %llu %llu %llu\n", c, t[4 * (size_t)c], t[4 * (size_t)c + 1],
+                            t[4 * (size_t)c + 2], t[4 * (size_t)c + 3] & 0xffffffffull, t[4 * (size_t)c + 3] >> 32);
+            fclose(fp);
+        }
+    }
     f->factored = 1;
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
 }

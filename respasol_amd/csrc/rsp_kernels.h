@@ -235,6 +235,8 @@ struct IluArgs {
     const RndChunk *rchunks;
     const RndItem *ritems;
     const int *rpairs, *rstaged, *rrounds;
+    unsigned long long *trace;  // diagnostics (RSP_ILU_FTRACE): 4 words per thin-run chunk, or null
+    int trace_cap;
 };
 
 struct TrsvArgs {
