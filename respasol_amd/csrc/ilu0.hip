@@ -336,8 +336,9 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
     auto process = [&](int it, int cb) {
         const int4 r = litem[it];
         T v = V[cb + it];
+        const T dv = V[r.z >= 0 ? r.z : kZero];  // the divisor, read with the pair indices
         const int u0 = r.y & 0xffff, u1 = u0 + (r.y >> 16);
-        for (int u = u0; u < u1; u += 4) {  // operands of 4 pairs loaded together (clamped)
+        auto batch = [&](int u) {  // operands of 4 pairs loaded together (clamped)
             int pr[4];
             T l[4], w[4];
 #pragma unroll
@@ -350,8 +351,12 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
 #pragma unroll
             for (int b = 0; b < 4; ++b)
                 if (u + b < u1) v = fma_t(-l[b], w[b], v);
+        };
+        if (u1 > u0) {  // the first batch straight-line (most items have <= 4 pairs)
+            batch(u0);
+            for (int u = u0 + 4; u < u1; u += 4) batch(u);
         }
-        if (r.z >= 0) v = v / V[r.z];
+        if (r.z >= 0) v = v / dv;
         V[cb + it] = v;
         vals[r.x] = v;
         if (r.w >= 0 && v == T(0)) atomicMin(a.zero_pivot, r.w);
