@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64) void ilu0_level_lds(IluArgs a, int off) {
     auto entry = [&](int x) {  // a_ij - sum l_ik u_kj over its pairs, k ascending
         T v = rv[x];
         const int u0 = up[x], u1 = up[x + 1];
-        for (int u = u0; u < u1; u += 4) {
+        auto batch = [&](int u) {
             T l[4], w[4];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -216,6 +216,10 @@ __global__ __launch_bounds__(64) void ilu0_level_lds(IluArgs a, int off) {
 #pragma unroll
             for (int b = 0; b < 4; ++b)
                 if (u + b < u1) v = fma_t(-l[b], w[b], v);
+        };
+        if (u1 > u0) {  // the first batch straight-line
+            batch(u0);
+            for (int u = u0 + 4; u < u1; u += 4) batch(u);
         }
         return v;
     };
@@ -223,7 +227,8 @@ __global__ __launch_bounds__(64) void ilu0_level_lds(IluArgs a, int off) {
         const int e = le[s];
         for (int x = s + lane; x < e; x += 64) {
             const int r = lo[x];
-            rv[r] = entry(r) / dv[r];
+            const T d = dv[r];  // read before the chain, not after it
+            rv[r] = entry(r) / d;
         }
         wave_sync();
         s = e;
