@@ -22,8 +22,12 @@
  *
  * Precision: RSP_R_64F / RSP_R_32F select fp64 or fp32 storage AND
  * accumulation (GPU/spmv.cu:131-162 with and without `#define FLOAT`).
- * Flush-to-zero (nvcc `-ftz=true`, GPU/Makefile:5) is a handle mode here
- * (rsp_set_ftz) selecting kernels compiled with fp32 denormal flushing.
+ * Flush-to-zero is an EXTENSION, not reference parity: the reference's nvcc
+ * flag is commented out (`CFLAGS = -arch=sm_70 -O3  #-ftz=true`,
+ * GPU/Makefile:5) and would not reach cuSPARSE's precompiled kernels anyway.
+ * It is a handle mode here (rsp_set_ftz) selecting kernels compiled with fp32
+ * denormal flushing, for the "fp32+FTZ" experiment the README describes
+ * (README.md:79-80). The parity configuration is fp32 without FTZ.
  */
 #ifndef RSP_H
 #define RSP_H
@@ -74,8 +78,9 @@ rsp_status_t rsp_destroy(rsp_handle_t handle);
 /* cusparseSetStream. `stream` is a hipStream_t (NULL = default stream). */
 rsp_status_t rsp_set_stream(rsp_handle_t handle, void *stream);
 rsp_status_t rsp_get_stream(rsp_handle_t handle, void **stream);
-/* nvcc -ftz=true (GPU/Makefile:5): fp32 kernels flush denormal inputs and
- * results to zero when enabled. fp64 is never flushed (as with nvcc). */
+/* Extension (the reference's `-ftz=true` at GPU/Makefile:5 is commented
+ * out): fp32 kernels flush denormal inputs and results to zero when enabled.
+ * fp64 is never flushed (as with nvcc -ftz). Default off = parity mode. */
 rsp_status_t rsp_set_ftz(rsp_handle_t handle, int enable);
 rsp_status_t rsp_get_ftz(rsp_handle_t handle, int *enable);
 /* cusparseGetErrorString analogue. Never NULL. */
@@ -140,6 +145,10 @@ rsp_status_t rsp_ilu0_buffer_size(rsp_handle_t handle, int n, int nnz, rsp_datat
  * triangle (factor + L-solve) and of its transpose (L^T-solve), and the
  * transposed strict-lower index map. `nnz` may exceed offsets[n] (the
  * reference passes A.nnz, GPU/ilu0.cu:166); offsets[n] is what is analysed.
+ * Each row's column indices must be strictly increasing (sorted, no
+ * duplicates — as csrilu02 requires); otherwise INVALID_VALUE. The reference
+ * loader sorts rows but keeps duplicate entries of a file, so a file with
+ * repeated coordinates is rejected here rather than factored as undefined.
  * Host-blocking (reads the pattern once). */
 rsp_status_t rsp_ilu0_analysis(rsp_handle_t handle, int n, int nnz, const int *d_row_offsets,
                                const int *d_col_ind, rsp_ilu0_info_t info);

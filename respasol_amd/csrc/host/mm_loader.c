@@ -105,16 +105,27 @@ static int cur_int(cursor *c, long long *out) {
     return 1;
 }
 
-/* scanf "%lg": strtod on the token (the buffer is NUL-terminated at `end`). */
+/* scanf "%lg": strtod on the token. The token (up to white space or `end`)
+ * is copied into a NUL-terminated scratch first: rsp_mm_load_buffer does not
+ * require its input to be terminated, and strtod must not read past `end`. */
 static int cur_double(cursor *c, double *out) {
     cur_skip_ws(c);
     if (c->p >= c->end) return -1;
+    const char *q = c->p;
+    while (q < c->end && !isspace((unsigned char)*q)) q++;
+    const size_t len = (size_t)(q - c->p);
+    char small[256];
+    char *tok = len < sizeof(small) ? small : (char *)malloc(len + 1);
+    if (!tok) return 0;
+    memcpy(tok, c->p, len);
+    tok[len] = '\0';
     char *stop = NULL;
-    double v = strtod(c->p, &stop);
-    if (stop == c->p) return 0;
-    if (stop > c->end) stop = (char *)c->end;
+    double v = strtod(tok, &stop);
+    const size_t used = (size_t)(stop - tok);
+    if (tok != small) free(tok);
+    if (used == 0) return 0;
     *out = v;
-    c->p = stop;
+    c->p += used;
     return 1;
 }
 

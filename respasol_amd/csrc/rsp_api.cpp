@@ -13,6 +13,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <unordered_map>
 #include <memory>
 #include <new>
 #include <chrono>
@@ -32,6 +34,10 @@ struct rsp_context {
     int ftz;
     int spmv_variant;  // RSP_SPMV_VARIANT (tuning knob, default 0)
     int num_cus;
+    // diagnostic trace buffers (RSP_ILU_FTRACE / RSP_ILU_TRACE), allocated
+    // on the handle's device on first use, freed by rsp_destroy
+    unsigned long long *d_ftrace;
+    unsigned long long *d_strace;
 };
 
 struct rsp_spmat {
@@ -50,8 +56,36 @@ struct rsp_spmat {
     int64_t nnz_c16;            // entries read through 16-bit column offsets
     int64_t local_cols;         // rsp_spmat_set_local_cols (-1: not split)
     int nint;                   // interior tiles at the front of the schedule
-    unsigned plan_gen;          // bumped by every preprocess (batch staleness check)
+    unsigned long long plan_gen;  // unique per preprocess / value rebind (plan registry key)
 };
+
+// Which matrix last planned into each SpMV workspace. cuSPARSE lets several
+// matrices share one workspace; the schedule lives in it, so ownership is
+// recorded here (buffer -> plan generation of the owning preprocess, unique
+// process-wide) and a call on a buffer owned by another plan re-plans first.
+namespace {
+std::mutex g_plan_mu;
+std::unordered_map<const void *, unsigned long long> g_plan_owner;
+std::atomic<unsigned long long> g_plan_next{1};
+
+unsigned long long plan_new_gen() { return g_plan_next.fetch_add(1); }
+void plan_claim(const void *buf, unsigned long long gen) {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    g_plan_owner[buf] = gen;
+}
+bool plan_owns(const rsp_spmat *m) {
+    if (!m->plan_buffer) return false;
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    auto it = g_plan_owner.find(m->plan_buffer);
+    return it != g_plan_owner.end() && it->second == m->plan_gen;
+}
+void plan_release(const rsp_spmat *m) {
+    if (!m->plan_buffer) return;
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    auto it = g_plan_owner.find(m->plan_buffer);
+    if (it != g_plan_owner.end() && it->second == m->plan_gen) g_plan_owner.erase(it);
+}
+}  // namespace
 
 struct rsp_ilu0_info {
     int analysed;
@@ -134,12 +168,22 @@ rsp_status_t rsp_create(rsp_handle_t *handle) {
     const char *v = getenv("RSP_SPMV_VARIANT");
     c->spmv_variant = v ? atoi(v) : 0;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    c->d_ftrace = nullptr;
+    c->d_strace = nullptr;
     *handle = c;
     return RSP_STATUS_SUCCESS;
 }
 
 rsp_status_t rsp_destroy(rsp_handle_t h) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (h->d_ftrace || h->d_strace) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(h->device);
+        if (h->d_ftrace) (void)hipFree(h->d_ftrace);
+        if (h->d_strace) (void)hipFree(h->d_strace);
+        (void)hipSetDevice(cur);
+    }
     delete h;
     return RSP_STATUS_SUCCESS;
 }
@@ -201,6 +245,7 @@ rsp_status_t rsp_create_csr(rsp_spmat_t *mat, int64_t rows, int64_t cols, int64_
 rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local) {
     if (!mat || ncols_local < 0 || ncols_local > mat->cols) return RSP_STATUS_INVALID_VALUE;
     mat->local_cols = ncols_local;
+    plan_release(mat);
     mat->plan_buffer = nullptr;  // re-plan on the next call
     return RSP_STATUS_SUCCESS;
 }
@@ -208,15 +253,22 @@ rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local) {
 rsp_status_t rsp_csr_set_values(rsp_spmat_t mat, void *d_values, rsp_datatype_t value_type) {
     if (!mat) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
-    if (d_values != mat->vals) mat->plan_gen++;  // batches hold the old pointer
+    if (d_values != mat->vals && plan_owns(mat)) {  // batches hold the old pointer: new gen
+        mat->plan_gen = plan_new_gen();
+        plan_claim(mat->plan_buffer, mat->plan_gen);
+    }
     mat->vals = d_values;
-    if (value_type != mat->type) mat->plan_buffer = nullptr;  // tile size depends on type
+    if (value_type != mat->type) {  // tile size depends on type
+        plan_release(mat);
+        mat->plan_buffer = nullptr;
+    }
     mat->type = value_type;
     return RSP_STATUS_SUCCESS;
 }
 
 rsp_status_t rsp_destroy_spmat(rsp_spmat_t mat) {
     if (!mat) return RSP_STATUS_INVALID_VALUE;
+    plan_release(mat);
     delete mat;
     return RSP_STATUS_SUCCESS;
 }
@@ -470,11 +522,13 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
                                      longrows.size() * sizeof(SpmvLongRow), hipMemcpyHostToDevice,
                                      h->stream));
     RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    if (mat->plan_buffer != d_buffer) plan_release(mat);
     mat->plan_buffer = d_buffer;
     mat->plan_type = compute_type;
     mat->nblocks = (int)blocks.size();
     mat->nint = nint;
-    mat->plan_gen++;
+    mat->plan_gen = plan_new_gen();
+    plan_claim(d_buffer, mat->plan_gen);
     mat->nlong = (int)longrows.size();
     mat->nslots = nslots;
     mat->nnz_s = m > 0 ? rp[(size_t)m] : 0;
@@ -502,7 +556,7 @@ static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alp
     if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
     if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
     if (mat->rows > 0 && (!d_y || (mat->cols > 0 && !d_x))) return RSP_STATUS_INVALID_VALUE;
-    if (mat->plan_buffer != d_buffer || mat->plan_type != compute_type || mat->plan_buffer == nullptr) {
+    if (mat->plan_buffer != d_buffer || mat->plan_type != compute_type || !plan_owns(mat)) {
         rsp_status_t st =
             rsp_spmv_preprocess(h, op, alpha, mat, d_x, beta, d_y, compute_type, d_buffer);
         if (st != RSP_STATUS_SUCCESS) return st;
@@ -572,7 +626,7 @@ struct rsp_spmv_batch {
     int part;
     std::vector<rsp_spmat_t> mats;
     std::vector<const void *> buffers;
-    std::vector<unsigned> plan_gen;  // schedules as copied (stale check)
+    std::vector<unsigned long long> plan_gen;  // schedules as copied (stale check)
     std::vector<rsp::SpmvBatchArgs> launches;  // one per kSpmvBatchMax matrices
     void *d_mem = nullptr;                      // entries, tiles, long rows of every launch
     ~rsp_spmv_batch() {
@@ -599,7 +653,9 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         if (!A || !d_buffers[j]) return RSP_STATUS_INVALID_VALUE;
         if (A->type != compute_type) return RSP_STATUS_NOT_SUPPORTED;
         if (A->rows > 0 && (!d_y[j] || (A->cols > 0 && !d_x[j]))) return RSP_STATUS_INVALID_VALUE;
-        if (A->plan_buffer != d_buffers[j] || A->plan_type != compute_type) {
+        for (int q = 0; q < j; q++)  // one workspace holds one schedule
+            if (d_buffers[q] == d_buffers[j]) return RSP_STATUS_INVALID_VALUE;
+        if (A->plan_buffer != d_buffers[j] || A->plan_type != compute_type || !plan_owns(A)) {
             rsp_status_t st = rsp_spmv_preprocess(h, RSP_OPERATION_NON_TRANSPOSE, pa, A, d_x[j],
                                                   pb, d_y[j], compute_type, d_buffers[j]);
             if (st != RSP_STATUS_SUCCESS) return st;
@@ -699,7 +755,7 @@ rsp_status_t rsp_spmv_batch_run(rsp_handle_t h, rsp_spmv_batch_t b, const void *
     if (!b || !alpha || !beta) return RSP_STATUS_INVALID_VALUE;
     for (size_t j = 0; j < b->mats.size(); j++) {  // re-planned since create: stale copy
         const rsp_spmat_t A = b->mats[j];
-        if (A->plan_buffer != b->buffers[j] || A->plan_gen != b->plan_gen[j])
+        if (A->plan_buffer != b->buffers[j] || A->plan_gen != b->plan_gen[j] || !plan_owns(A))
             return RSP_STATUS_INVALID_VALUE;
     }
     const double av = b->type == RSP_R_64F ? *(const double *)alpha : *(const float *)alpha;
@@ -1350,6 +1406,14 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     }
     for (int v : ci)
         if (v < 0 || v >= n) return RSP_STATUS_INVALID_VALUE;
+    // The diagonal search, update pairs and stages assume each row's columns
+    // strictly increasing (the reference loader sorts rows,
+    // loadMatrixMarket.cpp:237-242; csrilu02 requires sorted, duplicate-free
+    // rows). Unsorted rows or a repeated column are rejected here instead of
+    // silently factoring the wrong pattern.
+    for (int i = 0; i < n; i++)
+        for (int p = rp[(size_t)i] + 1; p < rp[(size_t)i + 1]; p++)
+            if (ci[(size_t)p] <= ci[(size_t)p - 1]) return RSP_STATUS_INVALID_VALUE;
     std::vector<int> dpos((size_t)n), hasdiag((size_t)n);
     for (int i = 0; i < n; i++) {
         const int *b = ci.data() + rp[(size_t)i], *e = ci.data() + rp[(size_t)i + 1];
@@ -1616,7 +1680,7 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     // diagnostics: RSP_ILU_FTRACE=<file> appends per-chunk shader-clock stamps
     // of the thin factor runs (host-blocking; never set in timed runs)
     const char *trace_file = getenv("RSP_ILU_FTRACE");
-    static unsigned long long *d_trace = nullptr;
+    unsigned long long *&d_trace = h->d_ftrace;
     const int trace_cap = 1 << 22;
     a.trace = nullptr;
     a.trace_cap = 0;
@@ -1682,7 +1746,7 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
     // diagnostics: RSP_ILU_TRACE=<file> appends per-chunk timestamps of the
     // prefetching thin kernel (host-blocking; never set in timed runs)
     const char *trace_file = getenv("RSP_ILU_TRACE");
-    static unsigned long long *d_trace = nullptr;
+    unsigned long long *&d_trace = h->d_strace;
     const int trace_cap = 4 << 20;
     if (trace_file) {
         if (!d_trace) RSP_CHECK_HIP(hipMalloc((void **)&d_trace, trace_cap * sizeof(unsigned long long)));

@@ -1,5 +1,7 @@
 """BASELINE config 3: level-scheduled ILU(0) factor + L / L^T solves on the
-21 moderate matrices (surrogates), fp64 and fp32+FTZ, on one MI355X, with
+21 moderate matrices (surrogates), fp64, fp32 (the parity configuration)
+and fp32+FTZ (an extension: the reference's -ftz flag is commented out,
+GPU/Makefile:5), on one MI355X, with
 the oracle's sequential CPU time beside it and a bitwise parity check.
 
     python scripts/bench_ilu0.py [--set moderate] [--reps 3] [--json out.json]
@@ -89,23 +91,26 @@ def main():
     h = Handle()
     out = []
     print(f"{'matrix':16s} {'n':>8s} {'nnz_s':>9s} {'lvL':>5s} {'lvT':>5s} | "
-          f"{'fp64 fac':>9s} {'solve':>8s} | {'fp32ftz fac':>11s} {'solve':>8s} | "
+          f"{'fp64 fac':>9s} {'solve':>8s} | {'fp32 fac':>9s} {'solve':>8s} | {'fp32ftz fac':>11s} {'solve':>8s} | "
           f"{'cpu fac':>8s} {'cpu slv':>8s} ok")
     for name in names:
         A = csr.surrogate(name)
         r64 = run_one(h, A, torch.float64, False, args.reps)
+        r32p = run_one(h, A, torch.float32, False, args.reps)
         r32 = run_one(h, A, torch.float32, True, args.reps)
-        row = {"matrix": name, "n": A.m, "nnz_s": A.nnz_stored, "fp64": r64, "fp32_ftz": r32}
+        row = {"matrix": name, "n": A.m, "nnz_s": A.nnz_stored, "fp64": r64, "fp32": r32p, "fp32_ftz": r32}
         out.append(row)
         print(f"{name:16s} {A.m:8d} {A.nnz_stored:9d} {r64['levels_L']:5d} {r64['levels_LT']:5d} | "
-              f"{r64['factor_ms']:9.3f} {r64['solve_ms']:8.3f} | {r32['factor_ms']:11.3f} "
+              f"{r64['factor_ms']:9.3f} {r64['solve_ms']:8.3f} | {r32p['factor_ms']:9.3f} {r32p['solve_ms']:8.3f} | "
+              f"{r32['factor_ms']:11.3f} "
               f"{r32['solve_ms']:8.3f} | {r64['cpu_factor_ms']:8.2f} {r64['cpu_solve_ms']:8.2f} "
-              f"{r64['bitwise_ok'] and r32['bitwise_ok']}", flush=True)
+              f"{r64['bitwise_ok'] and r32p['bitwise_ok'] and r32['bitwise_ok']}", flush=True)
     tot = lambda k, p: sum(r[p][k] for r in out)  # noqa: E731
     gb = lambda k, p: statistics.median(r[p][k] for r in out)  # noqa: E731
     print(f"median algorithmic GB/s (SURVEY 8d, reporting only; 8000 = HBM peak): fp64 factor "
           f"{gb('factor_gbps', 'fp64'):.1f} solve {gb('solve_gbps', 'fp64'):.1f}")
     print(f"TOTAL fp64 factor {tot('factor_ms', 'fp64'):.2f} ms solve {tot('solve_ms', 'fp64'):.2f} ms; "
+          f"fp32 factor {tot('factor_ms', 'fp32'):.2f} solve {tot('solve_ms', 'fp32'):.2f}; "
           f"fp32+ftz factor {tot('factor_ms', 'fp32_ftz'):.2f} solve {tot('solve_ms', 'fp32_ftz'):.2f}; "
           f"cpu(1 thread) factor {tot('cpu_factor_ms', 'fp64'):.1f} solve {tot('cpu_solve_ms', 'fp64'):.1f}")
     if args.json:

@@ -229,3 +229,26 @@ def test_fp32_fma_single_rounding(handle, monkeypatch, thin_solve):
     assert z[1] == np.float32(1 + 2.0 ** -23), z[1]
     v, _, _ = ob.ilu0(rp, ci, va_h.astype(np.float32))
     assert np.array_equal(z, ob.trsv("lower_n", rp, ci, v, np.array([b, c], np.float32)))
+
+
+def test_unsorted_or_duplicate_rows_rejected(handle):
+    """rsp_ilu0_analysis needs strictly increasing columns per row (the
+    diagonal search and the update pairs assume it; csrilu02 requires sorted,
+    duplicate-free rows): an unsorted row or a repeated column is
+    INVALID_VALUE, never a factor of the wrong pattern."""
+    from respasol_amd import RspError
+    rp = torch.tensor([0, 2, 4], dtype=torch.int32, device="cuda")
+    for cols in ([1, 0, 0, 1], [0, 0, 0, 1]):  # row 0 unsorted / duplicate column 0
+        ci = torch.tensor(cols, dtype=torch.int32, device="cuda")
+        il = Ilu0(handle, rp, ci)
+        with pytest.raises(RspError) as e:
+            il.analysis()
+        assert e.value.status == 3
+        il.close()
+    # the reference fixture with duplicate coordinates (sorted by the loader)
+    A = csr.load_matrix_market(os.path.join(GOLD, "mtx", "unsorted_dups.mtx"))
+    rp, ci, _ = upload_csr(A.rowptr, A.colidx, A.values)
+    il = Ilu0(handle, rp, ci)
+    with pytest.raises(RspError):
+        il.analysis()
+    il.close()

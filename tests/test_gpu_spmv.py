@@ -251,3 +251,45 @@ def test_kernel_variants_same_bits(monkeypatch, variant):
                 check(A, x, dt, h)
     finally:
         h.close()
+
+
+def test_shared_workspace_alternating(handle):
+    """Several matrices may share one SpMV workspace (cusparseSpMV without
+    preprocess treats it as scratch). Preprocess A into it, then B, then call
+    A, B, A: every call must re-plan for its own matrix (ownership registry,
+    rsp_api.cpp) and give the canonical-order bits."""
+    from respasol_amd import RspError
+    from respasol_amd.sparse import SpmvBatch
+    A = csr.surrogate("cfd2", 0.05)
+    B = csr.surrogate("ASIC_320ks", 0.1)  # different shape, hub rows (long-row fixup)
+    xa, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+    xb, _ = csr.dlarnv(2, [0, 0, 0, 1], B.n)
+    ma = SpMat(handle, *upload_csr(A.rowptr, A.colidx, A.values), A.n)
+    mb = SpMat(handle, *upload_csr(B.rowptr, B.colidx, B.values), B.n)
+    shared = torch.empty(max(ma.buffer.numel(), mb.buffer.numel()), dtype=torch.uint8, device="cuda")
+    own_a, own_b = ma.buffer, mb.buffer
+    ma.buffer = mb.buffer = shared
+    ma.set_local_cols(A.n)  # re-preprocess A into the shared buffer (whole-matrix plan)
+    mb.set_local_cols(B.n)  # ... then B over it
+    ref_a = ob.spmv(A.rowptr, A.colidx, A.values, xa, order="canon")
+    ref_b = ob.spmv(B.rowptr, B.colidx, B.values, xb, order="canon")
+    dxa, dxb = torch.from_numpy(xa).cuda(), torch.from_numpy(xb).cuda()
+    for mat, dx, ref in ((ma, dxa, ref_a), (mb, dxb, ref_b), (ma, dxa, ref_a), (mb, dxb, ref_b)):
+        y = mat.spmv(dx).cpu().numpy()
+        assert same_bits(y, ref), "shared workspace ran another matrix's schedule"
+    # a batch over one workspace twice is rejected; a batch whose schedule was
+    # overwritten by another matrix's preprocess since create is stale
+    ya, yb = torch.empty(A.m, dtype=torch.float64, device="cuda"), torch.empty(B.m, dtype=torch.float64, device="cuda")
+    with pytest.raises(RspError) as e:
+        SpmvBatch(handle, [ma, mb], [dxa, dxb], [ya, yb])
+    assert e.value.status == 3
+    mb.buffer = own_b  # A keeps the shared workspace
+    bt = SpmvBatch(handle, [ma, mb], [dxa, dxb], [ya, yb])
+    bt.run()
+    assert same_bits(ya.cpu().numpy(), ref_a) and same_bits(yb.cpu().numpy(), ref_b)
+    mb.buffer = shared
+    mb.spmv(dxb)  # B re-plans into A's workspace: the batch's copy of A is stale
+    with pytest.raises(RspError) as e:
+        bt.run()
+    assert e.value.status == 3
+    bt.close()

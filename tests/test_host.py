@@ -167,3 +167,16 @@ def test_gpu_drivers_usage_without_args():
     for exe in ("test_spmv", "test_ilu0", "spmv", "ilu0", "test_spmv_cpu"):
         r = subprocess.run([os.path.join(BIN, exe)], capture_output=True, text=True)
         assert r.returncode == 255 and "Usage examples" in r.stderr
+
+
+def test_buffer_loader_stays_inside_len():
+    """rsp_mm_load_buffer does not require a NUL at buf[len]: a number cut by
+    `len` must parse only the bytes inside it (here '2.5', not '2.5e7')."""
+    import ctypes as C
+    text = b"%%MatrixMarket matrix coordinate real general\n1 1 1\n1 1 2.5"
+    raw = C.create_string_buffer(text + b"e7 9 9 9", len(text) + 8)
+    s = _lib.CSRStruct()
+    st = _lib.host.rsp_mm_load_buffer(C.cast(raw, C.c_char_p), len(text), C.byref(s), 0, 0, _lib.MM_QUIET)
+    assert st == 0
+    A = csr._from_struct(s, 0)
+    assert A.values.tolist() == [2.5]
