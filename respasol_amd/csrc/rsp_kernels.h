@@ -29,7 +29,10 @@ struct alignas(16) SpmvLongRow {
 };
 
 // Tile geometry shared by the planner and the kernels.
-constexpr int kSpmvThreads = 256;
+#ifndef RSP_SPMV_THREADS
+#define RSP_SPMV_THREADS 256  // overridable for tile-geometry experiments (scripts/spmv_probe.py)
+#endif
+constexpr int kSpmvThreads = RSP_SPMV_THREADS;
 #ifndef RSP_SPMV_ITER
 #define RSP_SPMV_ITER 4  // overridable for tile-geometry experiments (scripts/spmv_probe.py)
 #endif

@@ -57,6 +57,9 @@
 #ifndef RSP_PROBE_LDS
 #define RSP_PROBE_LDS 0  // with RSP_PROBE 4: also an LDS write + barrier
 #endif
+#ifndef RSP_GATHER_POL
+#define RSP_GATHER_POL 0  // x gathers as buffer loads with a cache policy (A/B)
+#endif
 
 namespace RSP_KNS {
 
@@ -152,6 +155,13 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
     __builtin_amdgcn_s_setprio(0);  // loads issued: back to normal priority
 #endif
     T xv[IT][VW];
+#if RSP_GATHER_POL
+    // diagnostic builds: x gathers as buffer loads with a cache policy
+    // (1 sc0, 2 nt, 3 sc1, 4 none) — scripts/spmv_probe.py gp1..gp4
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7ffffff0, 0x00020000);
+    constexpr int kAux = RSP_GATHER_POL == 1 ? 1 : RSP_GATHER_POL == 2 ? 2 : RSP_GATHER_POL == 3 ? 16 : 0;
+#endif
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -161,7 +171,14 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
                 c = min(cbase + (int)ch[it][j], cmax);
             else
                 c = ci[it][j];
+#if RSP_GATHER_POL
+            if constexpr (sizeof(T) == 8)
+                xv[it][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr, c * 8, 0, kAux));
+            else
+                xv[it][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(xr, c * 4, 0, kAux));
+#else
             xv[it][j] = x[(RSP_PROBE == 1 || RSP_PROBE == 3) ? (c & 4095) : c];
+#endif
         }
     __builtin_amdgcn_sched_barrier(0);
     // every slot (it*256 + tid)*VW lies inside the tile's LDS image, so the

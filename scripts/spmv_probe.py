@@ -36,6 +36,13 @@ PROBES = {
     "rows256": "-DRSP_SPMV_MAXROWS=256",
     "rows1024": "-DRSP_SPMV_MAXROWS=1024",
     "prio2": "-DRSP_PROBE_PRIO=2",
+    "gp1": "-DRSP_GATHER_POL=1",
+    "gp2": "-DRSP_GATHER_POL=2",
+    "gp3": "-DRSP_GATHER_POL=3",
+    "gp4": "-DRSP_GATHER_POL=4",
+    "t512": "-DRSP_SPMV_THREADS=512",
+    "t512r1k": "-DRSP_SPMV_THREADS=512 -DRSP_SPMV_MAXROWS=1024",
+    "t512it2": "-DRSP_SPMV_THREADS=512 -DRSP_SPMV_ITER=2",
 }
 
 
@@ -56,7 +63,8 @@ def child(steps, workload):
     from respasol_amd import csr
     from respasol_amd.sparse import Handle, SpMat, upload_csr
     h = Handle()
-    names = csr.surrogate_names(1 if workload == "big" else 0)
+    names = (csr.surrogate_names(1 if workload == "big" else 0) if workload in ("big", "moderate")
+             else workload.split(","))
     out = {}
     for dt, elem in ((torch.float64, 8), (torch.float32, 4)):
         mats, nbytes, flops = [], 0, 0
