@@ -31,6 +31,8 @@
 // Compiled twice like spmv.hip (rsp_k / rsp_k_ftz).
 
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <limits.h>
 
 #include "rsp_kernels.h"
@@ -338,7 +340,12 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
         if (tid == 0) lrnd[nr] = ni;
         lds_barrier();
     };
-    auto process = [&](int it, int cb) {
+    // An item: its value in the chunk's LDS slot and (wide rounds, STORE) in
+    // vals. Narrow rounds skip the global store and the zero-pivot check: a
+    // run's items go to vals in one flush by all threads after the run, so a
+    // narrow round is LDS traffic and arithmetic only.
+    auto process = [&](int it, int cb, auto store_tag) {
+        constexpr bool STORE = decltype(store_tag)::value;
         const int4 r = litem[it];
         T v = V[cb + it];
         const T dv = V[r.z >= 0 ? r.z : kZero];  // the divisor, read with the pair indices
@@ -363,8 +370,18 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
         }
         if (r.z >= 0) v = v / dv;
         V[cb + it] = v;
-        vals[r.x] = v;
-        if (r.w >= 0 && v == T(0)) atomicMin(a.zero_pivot, r.w);
+        if constexpr (STORE) {
+            vals[r.x] = v;
+            if (r.w >= 0 && v == T(0)) atomicMin(a.zero_pivot, r.w);
+        }
+    };
+    auto flush = [&](int cb, int i0, int i1) {  // items [i0, i1) of a narrow run, after its barrier
+        for (int i = i0 + tid; i < i1; i += NTH) {
+            const int4 r = litem[i];
+            const T v = V[cb + i];
+            vals[r.x] = v;
+            if (r.w >= 0 && v == T(0)) atomicMin(a.zero_pivot, r.w);
+        }
     };
     auto narrow = [&](int q) { return lrnd[q + 1] - lrnd[q] <= 64; };
     auto run_end = [&](int q, int nr) {  // first round >= q that is not narrow, or nr
@@ -379,19 +396,30 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
         for (int q = 0; q < nr;) {
             if (narrow(q)) {
                 const int qe = run_end(q, nr);
-                if (tid < 64)  // (a software-pipelined form of this loop measured slower)
+                // long runs defer the global stores to one flush after the
+                // run; short ones (between wide rounds) store as they go
+                const bool defer = qe - q >= a.defer_rounds;
+                auto run = [&](auto store_tag) {
                     for (int qq = q; qq < qe; ++qq) {
                         const int b0 = lrnd[qq];
-                        if (b0 + lane < lrnd[qq + 1]) process(b0 + lane, cb);
+                        if (b0 + lane < lrnd[qq + 1]) process(b0 + lane, cb, store_tag);
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
                     }
+                };
+                if (tid < 64) {  // (a software-pipelined form of this loop measured slower)
+                    if (defer)
+                        run(std::false_type());
+                    else
+                        run(std::true_type());
+                }
                 lds_barrier();
+                if (defer) flush(cb, lrnd[q], lrnd[qe]);
                 q = qe;
                 continue;
             }
-            for (int it = lrnd[q] + tid; it < lrnd[q + 1]; it += NTH) process(it, cb);
+            for (int it = lrnd[q] + tid; it < lrnd[q + 1]; it += NTH) process(it, cb, std::true_type());
             lds_barrier();
             ++q;
         }
@@ -617,8 +645,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     static_assert(rsp::kChunkRows <= NTH, "one row of a chunk per thread");
     constexpr int kZero = rsp::kYWin, kStaged = rsp::kYWin + 1;
     __shared__ T ybuf[rsp::kYWin + 1 + rsp::kChunkTerms];
-    __shared__ TermGroup<T, G> lval[rsp::kChunkTerms / G];
-    __shared__ TermIds<G> lidx[rsp::kChunkTerms / G];
+    // + one pad group (values 0, y from the zero slot) after the chunk's groups
+    constexpr int kPadGroup = rsp::kChunkTerms / G;
+    __shared__ TermGroup<T, G> lval[rsp::kChunkTerms / G + 1];
+    __shared__ TermIds<G> lidx[rsp::kChunkTerms / G + 1];
     __shared__ ThinRow<T> lrow[rsp::kChunkRows];
     __shared__ int lrowi[rsp::kChunkRows];
     __shared__ T ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
@@ -628,6 +658,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     T *y = (T *)a.y;
     const int *ptr = a.plan.ptr_dev;
     if (tid == 0) ybuf[kZero] = T(0);
+    if (tid < G) {  // the pad group: exact no-op terms, fma(-0, 0, s) == s
+        lval[kPadGroup].v[tid] = T(0);
+        lidx[kPadGroup].v[tid] = kZero * (int)sizeof(T);
+    }
     struct Pre {  // this thread's share of a chunk: row tid, terms tid + j NTH (all streams)
         rsp::ThinRowPlan r;
         T xv, dg, v[TPT];
@@ -760,56 +794,68 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     };
     // A lane past a narrow level's last row reads that last row's record (its
     // index is clamped) and so computes the same value into the same slot: no
-    // store predicate.
-    auto narrow_run = [&](const rsp::LevelChunk &ch, int q0, int q1) {  // wave 0
+    // store predicate (duplicate same-address LDS writes cost less than the
+    // exec-mask branch of a predicate; measured). The prefetches for levels
+    // q+1 / q+2 are unconditional (clamped indices: past the run they read
+    // valid records that go unused), so a level is straight-line code; the
+    // diagnostics stamp is a separate instantiation (TR), not a branch per level.
+    auto narrow_run = [&](const rsp::LevelChunk &ch, int q0, int q1, auto trace_tag) {  // wave 0
+        constexpr bool TR = decltype(trace_tag)::value;
         const int lane = tid, x0 = ch.x0, nl = ch.l1 - ch.l0;
         auto lpt = [&](int q) { return lptr[min(q, nl)]; };
         auto ld_row = [&](int p0, int p1) { return max(p0 - x0 + min(lane, p1 - p0 - 1), 0); };
-        // level pointers p1..p3 = lptr[q+1 .. q+3] (clamped), rolling
-        int p1 = lpt(q0 + 1), p2 = lpt(q0 + 2), p3 = lpt(q0 + 3);
+        // level pointers p2, p3 = lptr[q+2], lptr[q+3] (clamped), rolling
+        const int p1 = lpt(q0 + 1);
+        int p2 = lpt(q0 + 2), p3 = lpt(q0 + 3);
         int cr = ld_row(lpt(q0), p1);
         ThinRow<T> cR = lrow[cr];
-        TermGroup<T, G> cV = lval[cR.g & 0xffff];
         TermIds<G> cI = lidx[cR.g & 0xffff];
         int nr = ld_row(p1, p2);
         ThinRow<T> nR = lrow[nr];
+        // Drain the prologue's LDS loads here: the compiler merges the wait
+        // state of the loop entry into the loop head, and with these loads
+        // pending there it waits at the head of EVERY level — which in the
+        // steady state is a wait for the previous level's y store.
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         for (int q = q0; q < q1; ++q) {
-            // loads for later levels: none of them depends on a y
+            // loads for later levels (none depends on a y): the y indices of
+            // level q+1's first group, the row records of level q+2. Term
+            // values are not carried: they load with the y, off the critical path.
             const int p4 = lpt(q + 4);
-            TermGroup<T, G> nV = cV;
-            TermIds<G> nI = cI;
-            ThinRow<T> mR = nR;
-            int mr = nr;
-            if (q + 1 < q1) {
-                nV = lval[nR.g & 0xffff];
-                nI = lidx[nR.g & 0xffff];
-            }
-            if (q + 2 < q1) {
-                mr = ld_row(p2, p3);
-                mR = lrow[mr];
-            }
+            const TermIds<G> nI = lidx[nR.g & 0xffff];
+            const int mr = ld_row(p2, p3);
+            const ThinRow<T> mR = lrow[mr];
             // level q: y loads -> fma chain -> y store (the critical path)
-            T s = group_fma(cR.x, cV, cI);
-            if (cR.g >= 2 << 16) {  // more than one group
-                const int g0 = cR.g & 0xffff, ng = cR.g >> 16;
-                for (int g = 1; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+            T s;
+            const int g0 = cR.g & 0xffff, ng = cR.g >> 16;
+            if (__ballot(ng >= 2)) {
+                // a row of the level has a second group: every lane loads one
+                // (its own, or the pad group) together with the first group's
+                // y, so its y loads overlap instead of following the first
+                // group's fma chain (one LDS round trip instead of two)
+                const int gi = ng >= 2 ? g0 + 1 : kPadGroup;
+                const TermIds<G> i2 = lidx[gi];
+                s = group_fma(cR.x, lval[g0], cI);
+                s = group_fma(s, lval[gi], i2);
+                if (__ballot(ng >= 3))
+                    for (int g = 2; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+            } else {
+                s = group_fma(cR.x, lval[g0], cI);
             }
             if constexpr (KIND == 2) s = s / ldg[cr];
             put(cR.out, s);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-            if (a.trace) {  // diagnostics: level end stamps
+            if constexpr (TR) {  // diagnostics: level end stamps
                 if (lane == 0 && ch.l0 + q < a.trace_cap / 2)
                     a.trace[a.trace_cap / 2 + ch.l0 + q] = a.trace_clk ? clock64() : wall_clock64();
             }
             cR = nR;
             cr = nr;
-            cV = nV;
             cI = nI;
             nR = mR;
             nr = mr;
-            p1 = p2;
             p2 = p3;
             p3 = p4;
         }
@@ -821,7 +867,12 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         for (int q = 0; q < nl;) {
             if (narrow(q)) {
                 const int qe = run_end(q, nl);
-                if (tid < 64) narrow_run(ch, q, qe);
+                if (tid < 64) {
+                    if (a.trace)
+                        narrow_run(ch, q, qe, std::true_type());
+                    else
+                        narrow_run(ch, q, qe, std::false_type());
+                }
                 lds_barrier();
                 q = qe;
                 continue;

@@ -1671,6 +1671,7 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.udiv = f->d_udiv;
     a.frow = f->d_frow;
     a.fat_lds = env_int("RSP_ILU_FAT_LDS", 1) != 0;
+    a.defer_rounds = env_int("RSP_ILU_DEFER", 8);  // A/B knob (thin factor runs)
     a.rchunks = f->d_rchunks;
     a.ritems = f->d_ritems;
     a.rpairs = f->d_rpairs;

@@ -240,6 +240,7 @@ struct IluArgs {
     const int *rpairs, *rstaged, *rrounds;
     unsigned long long *trace;  // diagnostics (RSP_ILU_FTRACE): 4 words per thin-run chunk, or null
     int trace_cap;
+    int defer_rounds;  // narrow runs of at least this many rounds flush their items after the run
 };
 
 struct TrsvArgs {
