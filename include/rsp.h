@@ -222,8 +222,10 @@ rsp_status_t rsp_spmv_part(rsp_handle_t handle, const void *alpha, rsp_spmat_t m
  * equal to rsp_spmv / rsp_spmv_part on each, without the per-launch ramp and
  * drain. `part` selects the schedule part of every matrix as rsp_spmv_part
  * (0 = whole product). Create records the pointers (x_j, y_j, d_buffers[j]
- * stay valid until destroy) and copies the matrices' schedules (a matrix not
- * yet preprocessed into d_buffers[j] is preprocessed); run fails with
+ * stay valid until destroy) and plans the batch's own tiling of every matrix
+ * (full tiles once the launch fills the chip; a matrix not yet preprocessed
+ * into d_buffers[j] is preprocessed first, its long-row partials stay
+ * there); run fails with
  * INVALID_VALUE if a matrix has been re-planned or given other values
  * (rsp_csr_set_values) since. Create and destroy
  * are host-blocking. */

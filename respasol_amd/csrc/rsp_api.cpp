@@ -394,6 +394,121 @@ static int build_spmv_plan(const int *rp, int m, int cap, int chunk, std::vector
     return 0;
 }
 
+// A complete SpMV schedule over host row offsets `rp` and column indices `ci`:
+// tiles (interior tiles first when local_cols >= 0), long rows, per-tile
+// column base and the 16-bit column offsets.
+struct TilePlan {
+    std::vector<SpmvBlock> blocks;
+    std::vector<SpmvLongRow> longrows;
+    int nslots = 0, nint = 0;
+    std::vector<int> cbase;
+    std::vector<uint16_t> c16;
+    int64_t nnz_c16 = 0;
+};
+
+// spread > 0: a plan of fewer tiles than `spread` (the resident workgroup
+// slots it may use) is re-packed into up to `spread` smaller tiles, so a lone
+// launch does not leave slots idle. Long rows do not depend on the packing
+// cap (they are cut at the fixed chunk), so every spread of one matrix has
+// the same long rows and partial slots.
+static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_bound,
+                           rsp_datatype_t type, int64_t spread, int64_t local_cols, bool use_c16,
+                           TilePlan &p) {
+    const int chunk = chunk_cap(type);
+    const int cap = tile_cap(type);
+    build_spmv_plan(rp, m, cap, chunk, p.blocks, p.longrows, &p.nslots);
+    const int64_t nb = (int64_t)p.blocks.size();
+    if (spread > 0 && nb > 0 && nb < spread) {
+        const SpmvBounds bb = spmv_bounds(m, std::max<int64_t>(nnz_bound, 0), chunk);
+        const int64_t nnz_s = rp[(size_t)m];
+        int c = (int)std::max<int64_t>(64, std::min<int64_t>(cap, (nnz_s + spread - 1) / spread));
+        for (int tries = 0; tries < 32 && c < cap; tries++) {
+            std::vector<SpmvBlock> b2;
+            std::vector<SpmvLongRow> l2;
+            int s2 = 0;
+            build_spmv_plan(rp, m, c, chunk, b2, l2, &s2);
+            if ((int64_t)b2.size() <= spread && b2.size() <= bb.nblocks) {
+                p.blocks.swap(b2);
+                p.longrows.swap(l2);
+                p.nslots = s2;
+                break;
+            }
+            c += std::max(8, c / 16);
+        }
+    }
+    // split schedule (rsp_spmat_set_local_cols): tiles reading own columns
+    // only first; long-row tiles always in the second part (with the fixup)
+    p.nint = 0;
+    if (local_cols >= 0) {
+        auto interior = [&](const SpmvBlock &b) {
+            if (b.r1 < 0) return false;
+            for (int k = b.k0; k < b.k1; k++)
+                if (ci[(size_t)k] >= local_cols) return false;
+            return true;
+        };
+        auto mid = std::stable_partition(p.blocks.begin(), p.blocks.end(), interior);
+        p.nint = (int)(mid - p.blocks.begin());
+    }
+    // 16-bit column offsets: a tile whose columns span < 65536 reads
+    // col = cbase + off (2 B per entry instead of 4; the int32 colidx is not
+    // read for it).
+    const int64_t nnz_s = m > 0 ? rp[(size_t)m] : 0;
+    p.cbase.assign(p.blocks.size(), -1);
+    p.c16.clear();
+    p.nnz_c16 = 0;
+    if (use_c16 && nnz_s > 0 && nnz_s <= nnz_bound) {
+        p.c16.assign((size_t)nnz_s, 0);
+        for (size_t t = 0; t < p.blocks.size(); t++) {
+            const SpmvBlock &bk = p.blocks[t];
+            if (bk.k1 <= bk.k0) continue;
+            int lo = ci[(size_t)bk.k0], hi = lo;
+            for (int k = bk.k0 + 1; k < bk.k1; k++) {
+                lo = std::min(lo, ci[(size_t)k]);
+                hi = std::max(hi, ci[(size_t)k]);
+            }
+            if (hi - lo > 65535) continue;
+            p.cbase[t] = lo;
+            p.nnz_c16 += bk.k1 - bk.k0;
+            for (int k = bk.k0; k < bk.k1; k++) p.c16[(size_t)k] = (uint16_t)(ci[(size_t)k] - lo);
+        }
+    }
+}
+
+// Row offsets and column indices of `mat` on the host, validated (base 0,
+// non-decreasing offsets, columns inside [0, cols)).
+static rsp_status_t download_pattern(rsp_handle_t h, rsp_spmat_t mat, std::vector<int> &rp,
+                                     std::vector<int> &ci) {
+    const int m = (int)mat->rows;
+    rp.assign((size_t)m + 1, 0);
+    ci.clear();
+    if (m > 0) {
+        RSP_CHECK_HIP(hipMemcpyAsync(rp.data(), mat->rowptr, ((size_t)m + 1) * sizeof(int),
+                                     hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    }
+    if (m > 0 && rp[0] != 0) return RSP_STATUS_INVALID_VALUE;  // base 0 only
+    for (int i = 0; i < m; i++)
+        if (rp[i + 1] < rp[i]) return RSP_STATUS_INVALID_VALUE;
+    // Column indices are gathered unchecked by the kernel: validate them once
+    // here (outside the timed loop) so a malformed matrix is an INVALID_VALUE
+    // status, never an out-of-bounds read of x on the GPU.
+    if (m > 0 && rp[(size_t)m] > 0) {
+        if (!mat->colidx) return RSP_STATUS_INVALID_VALUE;
+        ci.resize((size_t)rp[(size_t)m]);
+        RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), mat->colidx, ci.size() * sizeof(int),
+                                     hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+        const int ncols = (int)mat->cols;
+        for (int c : ci)
+            if ((unsigned)c >= (unsigned)ncols) return RSP_STATUS_INVALID_VALUE;
+    }
+    return RSP_STATUS_SUCCESS;
+}
+
+static int64_t spmv_resident_tiles(rsp_handle_t h, rsp_datatype_t t) {
+    return (int64_t)rsp_k::spmv_tiles_per_cu((int)elem_size(t)) * h->num_cus;
+}
+
 rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                  rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
                                  rsp_datatype_t compute_type, void *d_buffer) {
@@ -406,75 +521,27 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
     if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
     const int m = (int)mat->rows;
-    std::vector<int> rp((size_t)m + 1, 0);
-    if (m > 0) {
-        RSP_CHECK_HIP(hipMemcpyAsync(rp.data(), mat->rowptr, ((size_t)m + 1) * sizeof(int),
-                                     hipMemcpyDeviceToHost, h->stream));
-        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
-    }
-    if (m > 0 && rp[0] != 0) return RSP_STATUS_INVALID_VALUE;  // base 0 only
-    for (int i = 0; i < m; i++)
-        if (rp[i + 1] < rp[i]) return RSP_STATUS_INVALID_VALUE;
-    // Column indices are gathered unchecked by the kernel: validate them once
-    // here (preprocess is outside the timed loop) so a malformed matrix is an
-    // INVALID_VALUE status, never an out-of-bounds read of x on the GPU.
-    std::vector<int> ci;
-    if (m > 0 && rp[(size_t)m] > 0) {
-        if (!mat->colidx) return RSP_STATUS_INVALID_VALUE;
-        ci.resize((size_t)rp[(size_t)m]);
-        RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), mat->colidx, ci.size() * sizeof(int),
-                                     hipMemcpyDeviceToHost, h->stream));
-        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
-        const int ncols = (int)mat->cols;
-        for (int c : ci)
-            if ((unsigned)c >= (unsigned)ncols) return RSP_STATUS_INVALID_VALUE;
-    }
+    std::vector<int> rp, ci;
+    rsp_status_t st = download_pattern(h, mat, rp, ci);
+    if (st != RSP_STATUS_SUCCESS) return st;
     const int chunk = chunk_cap(compute_type);
-    int cap = tile_cap(compute_type);
-    std::vector<SpmvBlock> blocks;
-    std::vector<SpmvLongRow> longrows;
-    int nslots = 0;
-    build_spmv_plan(rp.data(), m, cap, chunk, blocks, longrows, &nslots);
-    if (!(h->spmv_variant & 16)) {
-        // A matrix with fewer tiles than the chip holds resident workgroups
-        // (R) leaves slots idle and runs each tile latency-bound: spread it
-        // over up to R smaller tiles (measured +2.7 % on the moderate set;
-        // plans of >= 2 waves are left alone, they lost 1 % this way).
-        // Tiling never changes the result (canonical summation order).
-        const int64_t R = (int64_t)rsp_k::spmv_tiles_per_cu((int)elem_size(compute_type)) * h->num_cus;
-        const int64_t nb = (int64_t)blocks.size();
-        if (nb > 0 && nb < R) {
-            const SpmvBounds bb = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), chunk);
-            const int64_t nnz_s = rp[(size_t)m];
-            int c = (int)std::max<int64_t>(64, std::min<int64_t>(cap, (nnz_s + R - 1) / R));
-            for (int tries = 0; tries < 32 && c < cap; tries++) {
-                std::vector<SpmvBlock> b2;
-                std::vector<SpmvLongRow> l2;
-                int s2 = 0;
-                build_spmv_plan(rp.data(), m, c, chunk, b2, l2, &s2);
-                if ((int64_t)b2.size() <= R && b2.size() <= bb.nblocks) {
-                    blocks.swap(b2);
-                    longrows.swap(l2);
-                    nslots = s2;
-                    break;
-                }
-                c += std::max(8, c / 16);
-            }
-        }
-    }
-    // split schedule (rsp_spmat_set_local_cols): tiles reading own columns
-    // only first; long-row tiles always in the second part (with the fixup)
-    int nint = 0;
-    if (mat->local_cols >= 0) {
-        auto interior = [&](const SpmvBlock &b) {
-            if (b.r1 < 0) return false;
-            for (int k = b.k0; k < b.k1; k++)
-                if (ci[(size_t)k] >= mat->local_cols) return false;
-            return true;
-        };
-        auto mid = std::stable_partition(blocks.begin(), blocks.end(), interior);
-        nint = (int)(mid - blocks.begin());
-    }
+    // A matrix with fewer tiles than the chip holds resident workgroups (R)
+    // leaves slots idle and runs each tile latency-bound: spread it over up
+    // to R smaller tiles (measured +2.7 % on the moderate set per matrix;
+    // plans of >= 2 waves are left alone, they lost 1 % this way). A batch
+    // re-plans its members itself (rsp_spmv_batch_create). Tiling never
+    // changes the result (canonical summation order). RSP_SPMV_VARIANT bit 4
+    // turns spreading off, bit 5 keeps every tile on the int32 indices.
+    TilePlan p;
+    make_tile_plan(rp.data(), ci.data(), m, mat->nnz, compute_type,
+                   (h->spmv_variant & 16) ? 0 : spmv_resident_tiles(h, compute_type),
+                   mat->local_cols, !(h->spmv_variant & 32), p);
+    const std::vector<SpmvBlock> &blocks = p.blocks;
+    const std::vector<SpmvLongRow> &longrows = p.longrows;
+    const int nslots = p.nslots, nint = p.nint;
+    const std::vector<int> &cbase = p.cbase;
+    const std::vector<uint16_t> &c16 = p.c16;
+    const int64_t nnz_c16 = p.nnz_c16;
     // the caller sized the buffer from mat->nnz; make sure the plan fits
     // (bounds in units of the chunk, which is <= the packing cap)
     SpmvBounds b = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), chunk);
@@ -482,30 +549,6 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
         return RSP_STATUS_INVALID_VALUE;
     if (!blocks.empty() && !d_buffer) return RSP_STATUS_INVALID_VALUE;
     const SpmvLayout lay = spmv_layout(b, elem_size(compute_type), mat->nnz);
-    // 16-bit column offsets: a tile whose columns span < 65536 reads
-    // col = cbase + off (2 B per entry instead of 4; the int32 colidx is not
-    // read for it). Built once here, like the schedule; RSP_SPMV_VARIANT bit
-    // 5 keeps every tile on the int32 indices.
-    const int64_t nnz_s = m > 0 ? rp[(size_t)m] : 0;
-    std::vector<int> cbase(blocks.size(), -1);
-    std::vector<uint16_t> c16;
-    int64_t nnz_c16 = 0;
-    if (!(h->spmv_variant & 32) && nnz_s > 0 && nnz_s <= mat->nnz) {
-        c16.assign((size_t)nnz_s, 0);
-        for (size_t t = 0; t < blocks.size(); t++) {
-            const SpmvBlock &bk = blocks[t];
-            if (bk.k1 <= bk.k0) continue;
-            int lo = ci[(size_t)bk.k0], hi = lo;
-            for (int k = bk.k0 + 1; k < bk.k1; k++) {
-                lo = std::min(lo, ci[(size_t)k]);
-                hi = std::max(hi, ci[(size_t)k]);
-            }
-            if (hi - lo > 65535) continue;
-            cbase[t] = lo;
-            nnz_c16 += bk.k1 - bk.k0;
-            for (int k = bk.k0; k < bk.k1; k++) c16[(size_t)k] = (uint16_t)(ci[(size_t)k] - lo);
-        }
-    }
     char *buf = (char *)d_buffer;
     if (!blocks.empty()) {
         RSP_CHECK_HIP(hipMemcpyAsync(buf, blocks.data(), blocks.size() * sizeof(SpmvBlock),
@@ -664,18 +707,60 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
     std::unique_ptr<rsp_spmv_batch> b(new rsp_spmv_batch());
     b->type = compute_type;
     b->part = part;
-    // layout: per launch [entries | tiles | long rows], each 16-B aligned
-    struct Span { int first, count, t0, t1, l0, l1; size_t off_e, off_t, off_c, off_l; };
+    // The batch carries its own schedules. Each matrix's own plan is spread
+    // over the whole chip for a lone launch (rsp_spmv_preprocess); in a
+    // batch that only shrinks the tiles, which cost the moderate set 35 %
+    // (0.145 vs 0.108 ms per step). So members are planned with
+    // full tiles, and spread only when the launch's tiles together do not
+    // fill the resident slots (each matrix over its nnz share of them).
+    // Long rows and their partial slots are the same in every spread of a
+    // matrix, so the partials stay in d_buffers[j].
+    const int64_t R = spmv_resident_tiles(h, compute_type);
+    const bool spread_ok = !(h->spmv_variant & 16), c16_ok = !(h->spmv_variant & 32);
+    std::vector<TilePlan> plans((size_t)count);
+    // layout: per launch [entries | tiles | tile column bases | long rows |
+    // 16-bit column offsets of each matrix], each 16-B aligned
+    struct Span { int first, count; size_t off_e, off_t, off_c, off_l; std::vector<size_t> off_16; };
     std::vector<Span> spans;
     size_t bytes = 0;
+    auto tile_range = [part](const TilePlan &p, int *t0, int *t1) {
+        *t0 = part == 2 ? p.nint : 0;
+        *t1 = part == 1 ? p.nint : (int)p.blocks.size();
+    };
     for (int first = 0; first < count; first += rsp::kSpmvBatchMax) {
-        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, 0, 0, 0, 0};
+        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, {}};
+        std::vector<std::vector<int>> rps((size_t)sp.count), cis((size_t)sp.count);
+        int64_t nt_full = 0, nnz_all = 0;
+        for (int q = 0; q < sp.count; q++) {
+            rsp_spmat_t A = mats[first + q];
+            rsp_status_t st = download_pattern(h, A, rps[q], cis[q]);
+            if (st != RSP_STATUS_SUCCESS) return st;
+            make_tile_plan(rps[q].data(), cis[q].data(), (int)A->rows, A->nnz, compute_type, 0,
+                           A->local_cols, c16_ok, plans[first + q]);
+            int t0, t1;
+            tile_range(plans[first + q], &t0, &t1);
+            nt_full += t1 - t0;
+            nnz_all += A->rows > 0 ? rps[q][(size_t)A->rows] : 0;
+        }
+        if (spread_ok && nt_full < R)
+            for (int q = 0; q < sp.count; q++) {
+                rsp_spmat_t A = mats[first + q];
+                const int64_t nnz_q = A->rows > 0 ? rps[q][(size_t)A->rows] : 0;
+                const int64_t share = std::max<int64_t>(1, R * nnz_q / std::max<int64_t>(1, nnz_all));
+                make_tile_plan(rps[q].data(), cis[q].data(), (int)A->rows, A->nnz, compute_type,
+                               share, A->local_cols, c16_ok, plans[first + q]);
+            }
         int nt = 0, nl = 0;
-        for (int j = first; j < first + sp.count; j++) {
-            rsp_spmat_t A = mats[j];
-            const int t0 = part == 2 ? A->nint : 0, t1 = part == 1 ? A->nint : A->nblocks;
+        for (int q = 0; q < sp.count; q++) {
+            const TilePlan &p = plans[first + q];
+            rsp_spmat_t A = mats[first + q];
+            // the long rows index partial slots of the matrix's own workspace
+            if ((int)p.longrows.size() != A->nlong || p.nslots != A->nslots)
+                return RSP_STATUS_INTERNAL_ERROR;
+            int t0, t1;
+            tile_range(p, &t0, &t1);
             nt += t1 - t0;
-            nl += part == 1 ? 0 : A->nlong;
+            nl += part == 1 ? 0 : (int)p.longrows.size();
         }
         sp.off_e = bytes;
         bytes += (size_t)sp.count * sizeof(rsp::SpmvBatchEntry);
@@ -685,10 +770,13 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         bytes += ((size_t)nt * sizeof(int) + 15) & ~(size_t)15;
         sp.off_l = bytes;
         bytes += ((size_t)nl * sizeof(SpmvLongRow) + 15) & ~(size_t)15;
+        for (int q = 0; q < sp.count; q++) {
+            sp.off_16.push_back(bytes);
+            bytes += (plans[first + q].c16.size() * sizeof(uint16_t) + 15) & ~(size_t)15;
+        }
         spans.push_back(sp);
     }
     if (bytes > 0) RSP_CHECK_HIP(hipMalloc(&b->d_mem, bytes));
-    RSP_CHECK_HIP(hipStreamSynchronize(h->stream));  // schedules written on the handle's stream
     std::vector<unsigned char> host(bytes);
     for (const Span &sp : spans) {
         rsp::SpmvBatchArgs a{};
@@ -702,9 +790,11 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         int nt = 0, nl = 0;
         for (int q = 0; q < sp.count; q++) {
             rsp_spmat_t A = mats[sp.first + q];
+            const TilePlan &p = plans[sp.first + q];
             const char *buf = (const char *)d_buffers[sp.first + q];
-            const int t0 = part == 2 ? A->nint : 0, t1 = part == 1 ? A->nint : A->nblocks;
-            const int nlq = part == 1 ? 0 : A->nlong;
+            int t0, t1;
+            tile_range(p, &t0, &t1);
+            const int nlq = part == 1 ? 0 : (int)p.longrows.size();
             rsp::SpmvBatchEntry e{};
             e.rowptr = A->rowptr;
             e.colidx = A->colidx;
@@ -712,26 +802,24 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
             e.x = d_x[sp.first + q];
             e.y = d_y[sp.first + q];
             e.partials = (void *)(buf + A->off_part);
-            e.cidx = (const unsigned short *)(buf + A->off_cidx);
+            e.cidx = (const unsigned short *)((char *)b->d_mem + sp.off_16[q]);
             e.cmax = A->cols > 0 ? (int)(A->cols - 1) : 0;
             e.nnz = A->nnz_s;
             e.vector_ok = ((((uintptr_t)A->colidx) | ((uintptr_t)A->vals)) & 15) == 0;
             memcpy(host.data() + sp.off_e + (size_t)q * sizeof(e), &e, sizeof(e));
             a.tiles_at.begin[q] = nt;
             a.longs_at.begin[q] = nl;
-            if (t1 > t0)
-                RSP_CHECK_HIP(hipMemcpy(host.data() + sp.off_t + (size_t)nt * sizeof(SpmvBlock),
-                                        buf + (size_t)t0 * sizeof(SpmvBlock),
-                                        (size_t)(t1 - t0) * sizeof(SpmvBlock),
-                                        hipMemcpyDeviceToHost));
-            if (t1 > t0)
-                RSP_CHECK_HIP(hipMemcpy(host.data() + sp.off_c + (size_t)nt * sizeof(int),
-                                        buf + A->off_cbase + (size_t)t0 * sizeof(int),
-                                        (size_t)(t1 - t0) * sizeof(int), hipMemcpyDeviceToHost));
+            if (t1 > t0) {
+                memcpy(host.data() + sp.off_t + (size_t)nt * sizeof(SpmvBlock), p.blocks.data() + t0,
+                       (size_t)(t1 - t0) * sizeof(SpmvBlock));
+                memcpy(host.data() + sp.off_c + (size_t)nt * sizeof(int), p.cbase.data() + t0,
+                       (size_t)(t1 - t0) * sizeof(int));
+            }
             if (nlq > 0)
-                RSP_CHECK_HIP(hipMemcpy(host.data() + sp.off_l + (size_t)nl * sizeof(SpmvLongRow),
-                                        buf + A->off_long, (size_t)nlq * sizeof(SpmvLongRow),
-                                        hipMemcpyDeviceToHost));
+                memcpy(host.data() + sp.off_l + (size_t)nl * sizeof(SpmvLongRow), p.longrows.data(),
+                       (size_t)nlq * sizeof(SpmvLongRow));
+            if (!p.c16.empty())
+                memcpy(host.data() + sp.off_16[q], p.c16.data(), p.c16.size() * sizeof(uint16_t));
             nt += t1 - t0;
             nl += nlq;
         }

@@ -101,10 +101,41 @@ def test_batch_parts_equal_whole(handle, dtype):
     assert e.value.status == 3
 
 
-@pytest.mark.parametrize("variant", [1, 8, 9, 32])
+@pytest.mark.parametrize("names,split", [
+    ([("ecology2", 0.02), ("G2_circuit", 0.1)], False),     # few tiles: spread by nnz share
+    ([("ecology2", 1.0), ("ASIC_320ks", 1.0)], False),      # > 2048 tiles: full tiles
+    ([("ecology2", 1.0), ("ASIC_320ks", 1.0)], True)])
+def test_batch_own_tiling_same_bits(handle, names, split):
+    """The batch plans its members itself (full tiles once the launch fills
+    the chip, a per-matrix share of the slots otherwise) while a lone
+    rsp_spmv spreads a small matrix over the whole chip: different tiles,
+    the same bits (canonical summation order), whole and split."""
+    mats, xs = [], []
+    for k, (name, scale) in enumerate(names):
+        A = csr.surrogate(name, scale)
+        rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values, torch.float64)
+        M = SpMat(handle, rp, ci, va, A.n, nnz=max(A.nnz, A.nnz_stored))
+        if split:
+            M.set_local_cols(A.n // 2)
+        x, _ = csr.dlarnv(1, [0, 0, k, 3], A.n)
+        mats.append(M)
+        xs.append(torch.from_numpy(x).cuda())
+    ref = [M.spmv(x) for M, x in zip(mats, xs)]
+    ys = [torch.full((M.m,), float("nan"), dtype=torch.float64, device="cuda") for M in mats]
+    if split:
+        SpmvBatch(handle, mats, xs, ys, part=1).run()
+        SpmvBatch(handle, mats, xs, ys, part=2).run()
+    else:
+        SpmvBatch(handle, mats, xs, ys).run()
+    torch.cuda.synchronize()
+    for k, (r, y) in enumerate(zip(ref, ys)):
+        assert same_bits(r.cpu().numpy(), y.cpu().numpy()), k
+
+
+@pytest.mark.parametrize("variant", [1, 8, 9, 16, 32])
 def test_batch_variants_same_bits(monkeypatch, variant):
-    """Default-policy loads (bit 0), no per-matrix XCD swizzle (bit 3), int32
-    column indices only (bit 5)."""
+    """Default-policy loads (bit 0), no per-matrix XCD swizzle (bit 3), no
+    spreading (bit 4), int32 column indices only (bit 5)."""
     monkeypatch.setenv("RSP_SPMV_VARIANT", str(variant))
     h = Handle()
     try:
