@@ -405,20 +405,35 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
                            partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds);
 }
 
-// y[row] = alpha * sum(partials of the row, chunk order) (+ beta*y[row]).
+// One long row per wave: y[row] = alpha * (0 + p0 + p1 + ...) (+ beta*y[row]),
+// the chunk partials added in chunk order. Lane c loads partial c, so a row
+// costs one memory round trip instead of one per chunk (the loads of a
+// serial loop each waited for the add before them); the in-order sum runs
+// on shuffles, every lane computing it.
+template <typename T>
+__device__ __forceinline__ void fixup_row(const SpmvLongRow r, const T *__restrict__ partials,
+                                          T *__restrict__ y, T alpha, T beta, int beta_nonzero) {
+    const int lane = threadIdx.x;
+    const T yv = (beta_nonzero && lane == 0) ? y[r.row] : T(0);
+    T s = T(0);
+    for (int c0 = 0; c0 < r.nchunks; c0 += 64) {
+        const T p = c0 + lane < r.nchunks ? partials[r.first + c0 + lane] : T(0);
+        const int cn = min(64, r.nchunks - c0);
+        for (int c = 0; c < cn; ++c) s += __shfl(p, c, 64);
+    }
+    if (lane == 0) {
+        T out = alpha * s;
+        if (beta_nonzero) out += beta * yv;
+        y[r.row] = out;
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void spmv_longrow_fixup(const SpmvLongRow *__restrict__ lr,
                                                           int nlong, const T *__restrict__ partials,
                                                           T *__restrict__ y, T alpha, T beta,
                                                           int beta_nonzero) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= nlong) return;
-    const SpmvLongRow r = lr[i];
-    T s = T(0);
-    for (int c = 0; c < r.nchunks; ++c) s += partials[r.first + c];
-    T out = alpha * s;
-    if (beta_nonzero) out += beta * y[r.row];
-    y[r.row] = out;
+    fixup_row<T>(lr[blockIdx.x], partials, y, alpha, beta, beta_nonzero);
 }
 
 // Batched form: several independent matrices' tiles in one grid (one
@@ -456,20 +471,13 @@ template <typename T>
 __global__ __launch_bounds__(64) void spmv_longrow_fixup_batch(
     const SpmvBatchEntry *__restrict__ entries, const SpmvLongRow *__restrict__ lr,
     SpmvBatchTable at, T alpha, T beta, int beta_nonzero) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= at.begin[kSpmvBatchMax]) return;
+    const int i = blockIdx.x;  // one wave per long row
     int j = 0;
 #pragma unroll
     for (int q = 1; q < kSpmvBatchMax; ++q)
         if (i >= at.begin[q]) j = q;
-    const SpmvLongRow r = lr[i];
-    const T *partials = (const T *)entries[j].partials;
-    T *y = (T *)entries[j].y;
-    T s = T(0);
-    for (int c = 0; c < r.nchunks; ++c) s += partials[r.first + c];
-    T out = alpha * s;
-    if (beta_nonzero) out += beta * y[r.row];
-    y[r.row] = out;
+    const SpmvBatchEntry e = entries[j];
+    fixup_row<T>(lr[i], (const T *)e.partials, (T *)e.y, alpha, beta, beta_nonzero);
 }
 
 template <typename T>
@@ -498,7 +506,7 @@ static hipError_t launch_spmv_batch(const SpmvBatchArgs &a, hipStream_t s) {
         // `count` holds INT_MAX, so pass the total explicitly
         SpmvBatchTable lt = a.longs_at;
         lt.begin[kSpmvBatchMax] = nlong;
-        hipLaunchKernelGGL((spmv_longrow_fixup_batch<T>), dim3((nlong + 63) / 64), dim3(64), 0, s,
+        hipLaunchKernelGGL((spmv_longrow_fixup_batch<T>), dim3(nlong), dim3(64), 0, s,
                            a.entries, a.longrows, lt, alpha, beta, bnz);
         return hipGetLastError();
     }
@@ -525,7 +533,7 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.nlong > 0) {
-        hipLaunchKernelGGL((spmv_longrow_fixup<T>), dim3((a.nlong + 63) / 64), dim3(64), 0, s,
+        hipLaunchKernelGGL((spmv_longrow_fixup<T>), dim3(a.nlong), dim3(64), 0, s,
                            a.longrows, a.nlong, (const T *)a.partials, (T *)a.y, alpha, beta, bnz);
         e = hipGetLastError();
     }
