@@ -317,8 +317,12 @@ def main():
     bytes64 = sum(s.bytes_local(8) for s in slices)
     achieved = bytes64 * args.steps / (kern_ms * 1e-3) / 1e9
     # the schedule reads 16-bit column offsets for tiles spanning < 65536
-    # columns: 2 B of the CSR's 4-B index per such entry are never moved
-    saved64 = 2 * sum(s.mat64.plan_info()["entries_16bit"] for s in slices)
+    # columns: 2 B of the CSR's 4-B index per such entry are never moved (the
+    # batch tiles the matrices itself: its own count)
+    if batches:
+        saved64 = 2 * sum(b.info()["entries_16bit"] for p, b in batches.items() if (p != 0) == overlap)
+    else:
+        saved64 = 2 * sum(s.mat64.plan_info()["entries_16bit"] for s in slices)
     moved_achieved = (bytes64 - saved64) * args.steps / (kern_ms * 1e-3) / 1e9
     # the same K steps as one rsp_spmv launch per matrix (kernel-only), for
     # comparison with the batched launch: what a caller doing one SpMV at a

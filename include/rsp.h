@@ -236,6 +236,10 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t handle, int count, const rsp_spm
 rsp_status_t rsp_spmv_batch_run(rsp_handle_t handle, rsp_spmv_batch_t batch, const void *alpha,
                                 const void *beta);
 rsp_status_t rsp_spmv_batch_destroy(rsp_spmv_batch_t batch);
+/* rsp_spmv_plan_info of a batch's own schedule (its part of every matrix):
+ * tiles of all its launches, and the entries they read through 16-bit
+ * column offsets. */
+rsp_status_t rsp_spmv_batch_info(rsp_spmv_batch_t batch, int64_t *tiles, int64_t *entries_16bit);
 
 /* Number of dependency levels found by the analysis (L DAG, L^T DAG). */
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *levels_upper);

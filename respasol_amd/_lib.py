@@ -110,6 +110,7 @@ RSP_PROTOS = {
     "rsp_spmv_batch_create": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, vp]),
     "rsp_spmv_batch_run": (i32, [vp, vp, vp, vp]),
     "rsp_spmv_batch_destroy": (i32, [vp]),
+    "rsp_spmv_batch_info": (i32, [vp, vp, vp]),
     "rsp_spmv_plan_info": (i32, [vp, vp, vp]),
 }
 

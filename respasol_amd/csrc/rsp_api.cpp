@@ -672,6 +672,7 @@ struct rsp_spmv_batch {
     std::vector<unsigned long long> plan_gen;  // schedules as copied (stale check)
     std::vector<rsp::SpmvBatchArgs> launches;  // one per kSpmvBatchMax matrices
     void *d_mem = nullptr;                      // entries, tiles, long rows of every launch
+    int64_t tiles = 0, entries_16bit = 0;       // rsp_spmv_batch_info
     ~rsp_spmv_batch() {
         if (d_mem) (void)hipFree(d_mem);
     }
@@ -809,6 +810,9 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
             memcpy(host.data() + sp.off_e + (size_t)q * sizeof(e), &e, sizeof(e));
             a.tiles_at.begin[q] = nt;
             a.longs_at.begin[q] = nl;
+            for (int t = t0; t < t1; t++)
+                if (p.cbase[(size_t)t] >= 0) b->entries_16bit += p.blocks[(size_t)t].k1 - p.blocks[(size_t)t].k0;
+            b->tiles += t1 - t0;
             if (t1 > t0) {
                 memcpy(host.data() + sp.off_t + (size_t)nt * sizeof(SpmvBlock), p.blocks.data() + t0,
                        (size_t)(t1 - t0) * sizeof(SpmvBlock));
@@ -860,6 +864,13 @@ rsp_status_t rsp_spmv_batch_run(rsp_handle_t h, rsp_spmv_batch_t b, const void *
             e = h->ftz ? rsp_k_ftz::spmv_batch_f32(a, h->stream) : rsp_k::spmv_batch_f32(a, h->stream);
         if (e != hipSuccess) return RSP_STATUS_EXECUTION_FAILED;
     }
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_spmv_batch_info(rsp_spmv_batch_t b, int64_t *tiles, int64_t *entries_16bit) {
+    if (!b || !tiles || !entries_16bit) return RSP_STATUS_INVALID_VALUE;
+    *tiles = b->tiles;
+    *entries_16bit = b->entries_16bit;
     return RSP_STATUS_SUCCESS;
 }
 

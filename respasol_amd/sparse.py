@@ -194,6 +194,12 @@ class SpmvBatch:
         check(rsp.rsp_spmv_batch_run(self.handle.ptr, self._b, C.byref(a), C.byref(b)),
               "rsp_spmv_batch_run")
 
+    def info(self) -> dict:
+        """{"tiles", "entries_16bit"} of the batch's own schedule (rsp_spmv_batch_info)."""
+        t, e = C.c_int64(), C.c_int64()
+        check(rsp.rsp_spmv_batch_info(self._b, C.byref(t), C.byref(e)), "rsp_spmv_batch_info")
+        return {"tiles": t.value, "entries_16bit": e.value}
+
     def close(self) -> None:
         if self._b:
             rsp.rsp_spmv_batch_destroy(self._b)

@@ -73,7 +73,8 @@ def main():
     if args.meta:
         with open(args.meta, "w") as f:
             json.dump({"calibration": calib, "set": args.set, "passes": args.passes,
-                       "batch_launches_per_pass": -(-len(mats) // 16),
+                       "batch_launches_per_pass": -(-len(mats) // 32),
+                       "batch_entries_16bit": B.info()["entries_16bit"],
                        "matrices": [{"name": n_, "grid": int(M.buffer.numel()), "alg_bytes": b,
                                      "entries_16bit": M.plan_info()["entries_16bit"]}
                                     for n_, b, M, _, _ in mats]}, f)

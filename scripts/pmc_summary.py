@@ -79,7 +79,10 @@ def main():
         hb = [fb[i] * 1024.0 * rf + wb[i] * 1024.0 * wf for i in range(nb)][1:]  # skip the cold pass
         hbm_b = sum(hb) / len(hb)
         alg_b = float(sum(alg))
-        moved_b = alg_b - 2.0 * sum(m.get("entries_16bit", 0) for m in meta["matrices"])
+        e16 = meta.get("batch_entries_16bit")  # the batch tiles the matrices itself
+        if e16 is None:
+            e16 = sum(m.get("entries_16bit", 0) for m in meta["matrices"])
+        moved_b = alg_b - 2.0 * e16
         batch = {"kernel": "rsp_k::spmv_tiles_batch<double,true,false,true>",
                  "hbm_bytes_per_launch": round(hbm_b), "algorithmic_bytes_per_launch": round(alg_b),
                  "traffic_over_algorithmic": round(hbm_b / alg_b, 4),

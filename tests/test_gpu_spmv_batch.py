@@ -123,11 +123,21 @@ def test_batch_own_tiling_same_bits(handle, names, split):
     ref = [M.spmv(x) for M, x in zip(mats, xs)]
     ys = [torch.full((M.m,), float("nan"), dtype=torch.float64, device="cuda") for M in mats]
     if split:
-        SpmvBatch(handle, mats, xs, ys, part=1).run()
-        SpmvBatch(handle, mats, xs, ys, part=2).run()
+        b1, b2 = SpmvBatch(handle, mats, xs, ys, part=1), SpmvBatch(handle, mats, xs, ys, part=2)
+        b1.run()
+        b2.run()
+        infos = [b1.info(), b2.info()]
     else:
-        SpmvBatch(handle, mats, xs, ys).run()
+        B = SpmvBatch(handle, mats, xs, ys)
+        B.run()
+        infos = [B.info()]
     torch.cuda.synchronize()
+    nnz = sum(M.nnz for M in mats)
+    tiles = sum(i["tiles"] for i in infos)
+    assert tiles > 0 and all(0 <= i["entries_16bit"] for i in infos)
+    if names[0][1] == 1.0:  # > 2048 full tiles: none spread, so never more than the lone plans
+        assert tiles <= sum(M.plan_info()["tiles"] for M in mats)
+    assert sum(i["entries_16bit"] for i in infos) <= nnz
     for k, (r, y) in enumerate(zip(ref, ys)):
         assert same_bits(r.cpu().numpy(), y.cpu().numpy()), k
 
