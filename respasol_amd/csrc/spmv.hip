@@ -52,13 +52,22 @@
 #define RSP_PROBE_PRIO 0  // s_setprio at kernel entry (A/B)
 #endif
 #ifndef RSP_NT_Y
-#define RSP_NT_Y 0  // non-temporal y stores (A/B)
+#define RSP_NT_Y -1  // y stores: 1 non-temporal, 0 plain, -1 (shipped) non-temporal for fp64 only
 #endif
 #ifndef RSP_PROBE_LDS
 #define RSP_PROBE_LDS 0  // with RSP_PROBE 4: also an LDS write + barrier
 #endif
 #ifndef RSP_GATHER_POL
 #define RSP_GATHER_POL 0  // x gathers as buffer loads with a cache policy (A/B)
+#endif
+#ifndef RSP_PROBE_NOY
+#define RSP_PROBE_NOY 0  // the short-row y stores kept behind a never-taken test (their cost)
+#endif
+#ifndef RSP_PROBE_YSMALL
+#define RSP_PROBE_YSMALL 0  // the short-row y stores aimed at an L2-resident 1024-entry window
+#endif
+#ifndef RSP_PROBE_WALK
+#define RSP_PROBE_WALK 0  // spmv_tiles: each workgroup walks this many consecutive tiles
 #endif
 
 namespace RSP_KNS {
@@ -322,7 +331,7 @@ __device__ __forceinline__ void spmv_tile(
             for (int j = 0; j < VW; ++j) acc += v[j] + T(c[j]);
         }
 #if RSP_PROBE_Y
-#if RSP_NT_Y
+#if RSP_NT_Y > 0
         if (blk.r1 > 0 && tid < nrows) __builtin_nontemporal_store(acc, y + blk.r0 + tid);
 #else
         if (blk.r1 > 0 && tid < nrows) y[blk.r0 + tid] = acc;  // + the y stream
@@ -371,11 +380,19 @@ __device__ __forceinline__ void spmv_tile(
     }
     reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, kb, [&](int rr, T sum) {
         T out = alpha * sum;
+        if (RSP_PROBE_NOY && out != T(-12345.0)) return;
         if (BETA) out += beta * y[r0 + rr];
-#if RSP_NT_Y
-        __builtin_nontemporal_store(out, y + r0 + rr);
+        // fp64: non-temporal y stores (the y lines leave L2 as a stream;
+        // -3 % per pass on the big set, where plain y write-back costs ~16 %
+        // of the time for ~4 % of the bytes); fp32: plain stores (nt +2 %)
+        constexpr bool kNtY = RSP_NT_Y > 0 || (RSP_NT_Y < 0 && sizeof(T) == 8);
+#if RSP_PROBE_YSMALL
+        y[(r0 + rr) & 1023] = out;
 #else
-        y[r0 + rr] = out;
+        if constexpr (kNtY)
+            __builtin_nontemporal_store(out, y + r0 + rr);
+        else
+            y[r0 + rr] = out;
 #endif
     });
 }
@@ -393,6 +410,20 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
+#if RSP_PROBE_WALK
+    // diagnostic: tiles [W t, W t + W) of the swizzled workgroup t in turn,
+    // an LDS-only barrier between them (the previous tile's y stores stay in
+    // flight under the next tile's stream)
+    const int nwg = (nblocks + RSP_PROBE_WALK - 1) / RSP_PROBE_WALK;
+    const int t0 = xcd_swizzle(blockIdx.x, nwg) * RSP_PROBE_WALK;
+    for (int w = 0; w < RSP_PROBE_WALK && t0 + w < nblocks; ++w) {
+        if (w) lds_barrier();
+        spmv_tile<T, NT, BETA>(blocks[t0 + w], rowptr, colidx, cidx, cbases[t0 + w], cmax, vals, x,
+                               y, partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum,
+                               rp_lds);
+    }
+    return;
+#endif
 #if RSP_PROBE_NOSWIZZLE
     const int b = blockIdx.x;
 #else
@@ -527,7 +558,8 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     // variant bit 0 restores default-policy loads for A/B runs
     auto kern = (a.variant & 1) ? (bnz ? spmv_tiles<T, false, true> : spmv_tiles<T, false, false>)
                                 : (bnz ? spmv_tiles<T, true, true> : spmv_tiles<T, true, false>);
-    hipLaunchKernelGGL(kern, dim3(a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
+    hipLaunchKernelGGL(kern, dim3(RSP_PROBE_WALK ? (a.nblocks + RSP_PROBE_WALK - 1) / (RSP_PROBE_WALK ? RSP_PROBE_WALK : 1)
+                                                : a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
                        (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks, a.cbases,
                        a.cidx, a.cmax, (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok);
     hipError_t e = hipGetLastError();

@@ -32,6 +32,7 @@ PROBES = {
     "loads_y_lds": "-DRSP_PROBE=4 -DRSP_PROBE_Y=1 -DRSP_PROBE_LDS=1",
     "loads_nty": "-DRSP_PROBE=4 -DRSP_PROBE_Y=1 -DRSP_NT_Y=1",
     "nty": "-DRSP_NT_Y=1",
+    "plainy": "-DRSP_NT_Y=0",
     "noswz": "-DRSP_PROBE_NOSWIZZLE=1",
     "rows256": "-DRSP_SPMV_MAXROWS=256",
     "rows1024": "-DRSP_SPMV_MAXROWS=1024",
@@ -43,6 +44,10 @@ PROBES = {
     "t512": "-DRSP_SPMV_THREADS=512",
     "t512r1k": "-DRSP_SPMV_THREADS=512 -DRSP_SPMV_MAXROWS=1024",
     "t512it2": "-DRSP_SPMV_THREADS=512 -DRSP_SPMV_ITER=2",
+    "noy": "-DRSP_PROBE_NOY=1",
+    "ysmall": "-DRSP_PROBE_YSMALL=1",
+    "walk2": "-DRSP_PROBE_WALK=2",
+    "walk4": "-DRSP_PROBE_WALK=4",
 }
 
 
