@@ -489,6 +489,8 @@ static rsp_status_t download_pattern(rsp_handle_t h, rsp_spmat_t mat, std::vecto
     if (m > 0 && rp[0] != 0) return RSP_STATUS_INVALID_VALUE;  // base 0 only
     for (int i = 0; i < m; i++)
         if (rp[i + 1] < rp[i]) return RSP_STATUS_INVALID_VALUE;
+    // the stored entries must lie inside the colidx / vals arrays (nnz long)
+    if (m > 0 && (int64_t)rp[(size_t)m] > mat->nnz) return RSP_STATUS_INVALID_VALUE;
     // Column indices are gathered unchecked by the kernel: validate them once
     // here (outside the timed loop) so a malformed matrix is an INVALID_VALUE
     // status, never an out-of-bounds read of x on the GPU.
@@ -1497,6 +1499,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         if (rp[(size_t)i + 1] < rp[(size_t)i]) return RSP_STATUS_INVALID_VALUE;
     const int nnz_s = rp[(size_t)n];
     if (nnz_s > 0 && !d_col_ind) return RSP_STATUS_INVALID_VALUE;
+    if (nnz_s > nnz) return RSP_STATUS_INVALID_VALUE;  // entries past the declared arrays
     std::vector<int> ci((size_t)nnz_s);
     if (nnz_s > 0) {
         RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), d_col_ind, (size_t)nnz_s * sizeof(int),

@@ -252,3 +252,11 @@ def test_unsorted_or_duplicate_rows_rejected(handle):
     with pytest.raises(RspError):
         il.analysis()
     il.close()
+    # rowptr[n] past the declared nnz: rejected before colidx is read
+    rp = torch.tensor([0, 1, 3], dtype=torch.int32, device="cuda")
+    ci = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
+    il = Ilu0(handle, rp, ci, nnz=2)
+    with pytest.raises(RspError) as e:
+        il.analysis()
+    assert e.value.status == 3
+    il.close()

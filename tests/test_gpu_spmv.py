@@ -205,6 +205,13 @@ def test_invalid_inputs_are_status_codes(handle):
     with pytest.raises(RspError) as e:
         SpMat(handle, rp, ci, va, 2)
     assert e.value.status == 3
+    # rowptr[m] past the declared nnz (the colidx / vals length): rejected
+    # before any of it is read
+    rp3 = torch.tensor([0, 3], dtype=torch.int32, device="cuda")
+    ci2 = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
+    with pytest.raises(RspError) as e:
+        SpMat(handle, rp3, ci2, va, 2)
+    assert e.value.status == 3
 
 
 def test_column_offset_tiles(handle):
