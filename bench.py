@@ -185,6 +185,9 @@ def main():
                          "interior tiles under it")
     ap.add_argument("--no-batch", action="store_true",
                     help="one rsp_spmv launch per matrix instead of one batched launch per step")
+    ap.add_argument("--nccl-normal-priority", action="store_true",
+                    help="RCCL on a normal-priority stream (default: high priority, so the "
+                         "overlapped exchange is not queued behind the interior tiles)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
@@ -197,7 +200,12 @@ def main():
     device = torch.device("cuda", dev)
     if world > 1:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            # the halo all_to_all runs beside the interior SpMV tiles, which fill
+            # every CU: a high-priority RCCL stream gets its kernel dispatched as
+            # soon as slots free instead of behind the remaining tiles
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = not args.nccl_normal_priority
+            dist.init_process_group("nccl", device_id=device, pg_options=opts)
         else:
             dist.init_process_group(args.dist_backend)
     handle = Handle()

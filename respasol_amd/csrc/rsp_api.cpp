@@ -318,6 +318,12 @@ static int chunk_cap(rsp_datatype_t t) {
     return t == RSP_R_64F ? SpmvTile<double>::kChunk : SpmvTile<float>::kChunk;
 }
 static size_t elem_size(rsp_datatype_t t) { return t == RSP_R_64F ? 8 : 4; }
+// Tile row cuts: RSP_SPMV_VARIANT bit 6 aligns them to 128-B y lines, bit 7
+// to 64 B (tuning knob; default unaligned).
+static int spmv_row_align(rsp_handle_t h, rsp_datatype_t t) {
+    const int e = (int)elem_size(t);
+    return (h->spmv_variant & 64) ? 128 / e : (h->spmv_variant & 128) ? 64 / e : 1;
+}
 
 rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                   rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
@@ -338,7 +344,7 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void
 // entries); the others are packed into tiles of <= cap entries / kSpmvMaxRows.
 static int build_spmv_plan(const int *rp, int m, int cap, int chunk, std::vector<SpmvBlock> &blocks,
                            std::vector<SpmvLongRow> &longrows, int *nslots,
-                           int maxrows = rsp::kSpmvMaxRows) {
+                           int maxrows = rsp::kSpmvMaxRows, int row_align = 1) {
     blocks.clear();
     longrows.clear();
     int slots = 0;
@@ -383,6 +389,13 @@ static int build_spmv_plan(const int *rp, int m, int cap, int chunk, std::vector
             nnz += l;
             r++;
         }
+        // row_align > 1: end a packed tile on a multiple of row_align rows,
+        // so its y stores cover whole lines, where the tile keeps >= 3/4 of
+        // its entries
+        if (row_align > 1 && r < m && r % row_align != 0) {
+            const int ra = r - r % row_align;
+            if (ra > start && (int64_t)(rp[ra] - rp[start]) * 4 >= (int64_t)(rp[r] - rp[start]) * 3) r = ra;
+        }
         SpmvBlock b;
         b.r0 = start;
         b.r1 = r;
@@ -413,10 +426,11 @@ struct TilePlan {
 // the same long rows and partial slots.
 static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_bound,
                            rsp_datatype_t type, int64_t spread, int64_t local_cols, bool use_c16,
-                           TilePlan &p) {
+                           TilePlan &p, int row_align = 1) {
     const int chunk = chunk_cap(type);
     const int cap = tile_cap(type);
-    build_spmv_plan(rp, m, cap, chunk, p.blocks, p.longrows, &p.nslots);
+    const int align = row_align;
+    build_spmv_plan(rp, m, cap, chunk, p.blocks, p.longrows, &p.nslots, rsp::kSpmvMaxRows, align);
     const int64_t nb = (int64_t)p.blocks.size();
     if (spread > 0 && nb > 0 && nb < spread) {
         const SpmvBounds bb = spmv_bounds(m, std::max<int64_t>(nnz_bound, 0), chunk);
@@ -426,7 +440,7 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
             std::vector<SpmvBlock> b2;
             std::vector<SpmvLongRow> l2;
             int s2 = 0;
-            build_spmv_plan(rp, m, c, chunk, b2, l2, &s2);
+            build_spmv_plan(rp, m, c, chunk, b2, l2, &s2, rsp::kSpmvMaxRows, align);
             if ((int64_t)b2.size() <= spread && b2.size() <= bb.nblocks) {
                 p.blocks.swap(b2);
                 p.longrows.swap(l2);
@@ -537,7 +551,7 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     TilePlan p;
     make_tile_plan(rp.data(), ci.data(), m, mat->nnz, compute_type,
                    (h->spmv_variant & 16) ? 0 : spmv_resident_tiles(h, compute_type),
-                   mat->local_cols, !(h->spmv_variant & 32), p);
+                   mat->local_cols, !(h->spmv_variant & 32), p, spmv_row_align(h, compute_type));
     const std::vector<SpmvBlock> &blocks = p.blocks;
     const std::vector<SpmvLongRow> &longrows = p.longrows;
     const int nslots = p.nslots, nint = p.nint;
@@ -739,7 +753,7 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
             rsp_status_t st = download_pattern(h, A, rps[q], cis[q]);
             if (st != RSP_STATUS_SUCCESS) return st;
             make_tile_plan(rps[q].data(), cis[q].data(), (int)A->rows, A->nnz, compute_type, 0,
-                           A->local_cols, c16_ok, plans[first + q]);
+                           A->local_cols, c16_ok, plans[first + q], spmv_row_align(h, compute_type));
             int t0, t1;
             tile_range(plans[first + q], &t0, &t1);
             nt_full += t1 - t0;
@@ -751,7 +765,8 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
                 const int64_t nnz_q = A->rows > 0 ? rps[q][(size_t)A->rows] : 0;
                 const int64_t share = std::max<int64_t>(1, R * nnz_q / std::max<int64_t>(1, nnz_all));
                 make_tile_plan(rps[q].data(), cis[q].data(), (int)A->rows, A->nnz, compute_type,
-                               share, A->local_cols, c16_ok, plans[first + q]);
+                               share, A->local_cols, c16_ok, plans[first + q],
+                               spmv_row_align(h, compute_type));
             }
         int nt = 0, nl = 0;
         for (int q = 0; q < sp.count; q++) {

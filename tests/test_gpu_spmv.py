@@ -240,7 +240,7 @@ def test_column_offset_tiles(handle):
         check(A, x, dt, handle)
 
 
-@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33])
+@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33, 64, 128, 80])
 def test_kernel_variants_same_bits(monkeypatch, variant):
     """Every kernel / plan variant (RSP_SPMV_VARIANT: default-policy instead of
     non-temporal loads; small plans not spread over the chip; int32 column
