@@ -206,7 +206,7 @@ rsp_status_t rsp_spmv_plan_info(rsp_spmat_t mat, int64_t *tiles, int64_t *entrie
  * Set before rsp_spmv_preprocess (a later call re-plans): the schedule then
  * puts the tiles that read own columns only first. rsp_spmv_part runs
  * part 1 = those interior tiles (launch it while the exchange is in flight),
- * part 2 = the remaining tiles and the long-row fixup; part 0 = everything
+ * part 2 = the remaining tiles, long rows included; part 0 = everything
  * (== rsp_spmv). Part 1 followed by part 2 gives y bit for bit equal to
  * rsp_spmv. beta must be 0 for parts 1 and 2. */
 rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local);
@@ -215,8 +215,8 @@ rsp_status_t rsp_spmv_part(rsp_handle_t handle, const void *alpha, rsp_spmat_t m
                            rsp_datatype_t compute_type, void *d_buffer, int part);
 
 /* Batched SpMV: y_j = alpha*A_j*x_j + beta*y_j for `count` independent
- * matrices of one compute type, as ONE kernel launch (plus one long-row
- * fixup launch when any A_j has rows longer than a tile) per 32 matrices.
+ * matrices of one compute type, as ONE kernel launch per 32 matrices (rows
+ * longer than a tile are finished inside it by their last-arriving chunk).
  * No cuSPARSE counterpart: the reference calls cusparseSpMV once per matrix
  * (GPU/spmv.cu:179-186); this is the same product per matrix, bit for bit
  * equal to rsp_spmv / rsp_spmv_part on each, without the per-launch ramp and

@@ -305,7 +305,7 @@ static SpmvLayout spmv_layout(const SpmvBounds &b, size_t elem, int64_t nnz) {
     SpmvLayout l;
     l.off_long = align256(b.nblocks * sizeof(SpmvBlock));
     l.off_part = l.off_long + align256(b.nlong * sizeof(SpmvLongRow));
-    l.off_cbase = l.off_part + align256(b.nslots * elem);
+    l.off_cbase = l.off_part + align256(b.nslots * 2 * elem);  // value + ticket per slot
     l.off_cidx = l.off_cbase + align256(b.nblocks * sizeof(int));
     l.bytes = l.off_cidx + align256((size_t)std::max<int64_t>(nnz, 0) * sizeof(uint16_t));
     return l;
@@ -579,6 +579,10 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     if (!longrows.empty())
         RSP_CHECK_HIP(hipMemcpyAsync(buf + off_long, longrows.data(),
                                      longrows.size() * sizeof(SpmvLongRow), hipMemcpyHostToDevice,
+                                     h->stream));
+    // partial slots: the long rows' arrival tickets start (and stay) at 0
+    if (nslots > 0)
+        RSP_CHECK_HIP(hipMemsetAsync(buf + off_part, 0, (size_t)nslots * 2 * elem_size(compute_type),
                                      h->stream));
     RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
     if (mat->plan_buffer != d_buffer) plan_release(mat);

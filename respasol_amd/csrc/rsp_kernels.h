@@ -17,8 +17,12 @@ namespace rsp {
 //   r1 == INT_MIN : the whole long row r0 (kSpmvLongRow < len <= tile cap),
 //                   reduced by the 256 threads and written to y directly;
 //   other r1 < 0  : chunk [k0, k1) of a row longer than a tile; its partial
-//                   goes to partials[-(r1 + 1)] and the fixup kernel adds the
-//                   chunks in order.
+//                   goes to slot s = -(r1 + 1) and the chunks are added in
+//                   order by the row's last-arriving chunk (or, variant bit 8,
+//                   by the separate fixup kernel).
+// Partial slot s occupies partials[2 s] (its value) and partials[2 s + 1]
+// (the first slot of a row: the row's arrival ticket, an unsigned int kept
+// at 0 between calls).
 struct alignas(16) SpmvBlock {
     int r0, r1, k0, k1;
 };
@@ -73,7 +77,8 @@ struct SpmvArgs {
     int nnz;        // rowptr[m]: tiles touching the last partial vector go scalar
     int vector_ok;  // colidx/vals 16-B aligned -> vector loads
     int variant;    // bit 0: default-policy (not non-temporal) vals/colidx loads;
-                    // bit 4 (plan time): no spreading of sub-wave plans
+                    // bit 4 (plan time): no spreading of sub-wave plans;
+                    // bit 8: long rows by the separate fixup kernel
 };
 
 // Several independent SpMVs in one launch (rsp_spmv_batch_*). The batch
@@ -106,8 +111,10 @@ struct SpmvBatchArgs {
     int count;
     SpmvBatchTable tiles_at, longs_at;
     double alpha, beta;
-    int variant;  // bit 0: default-policy loads; bit 3: no per-matrix XCD swizzle
+    int variant;  // bit 0: default-policy loads; bit 3: no per-matrix XCD swizzle;
+                  // bit 8: long rows by the separate fixup kernel
 };
+constexpr int kSpmvVariantFixup = 256;
 
 // Level schedule of one dependency DAG. Rows are grouped by level
 // (rows[ptr[l] .. ptr[l+1])); `segs` (host) cover the levels in order, each

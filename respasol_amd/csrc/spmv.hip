@@ -29,6 +29,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rsp_kernels.h"
 
 #ifndef RSP_KNS
@@ -293,13 +295,50 @@ __device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
 // One tile: stream -> gathers -> products in LDS -> canonical reduce -> y.
 // BETA: beta != 0 (y is read); the beta == 0 form issues no y loads, so its
 // y stores never wait on anything.
+// A chunk of a long row (one lane): publish the chunk's partial, take a
+// ticket; the chunk that arrives last adds the row's partials in chunk order
+// (the fixup kernel's order: 0 + p0 + p1 + ...) and writes y. Partials and
+// tickets move only through agent-scope atomics (the partial by exchange, the
+// read by fetch-add of 0), which are performed at the device's coherence
+// point, so no L1 / per-XCD L2 copy is ever read; each chunk's exchange has
+// returned before its ticket add is issued. No wait, no spin: the last
+// arriver is told by the value its own add returned. It resets the ticket.
+template <typename T>
+__device__ __forceinline__ void longrow_arrive(const SpmvBlock blk, const int *__restrict__ rowptr,
+                                               T *partials, T *__restrict__ y, T t, T alpha, T beta,
+                                               bool beta_nz) {
+    typedef typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type U;
+    constexpr int C = SpmvTile<T>::kChunk;
+    const int slot = -(blk.r1 + 1);
+    const int rs = rowptr[blk.r0], re = rowptr[blk.r0 + 1];
+    const int first = slot - (blk.k0 - rs) / C;
+    const int n = (re - rs + C - 1) / C;
+    U *pv = reinterpret_cast<U *>(partials);
+    unsigned int *ticket = reinterpret_cast<unsigned int *>(partials + 2 * first + 1);
+    const U prev = __hip_atomic_exchange(pv + 2 * slot, __builtin_bit_cast(U, t), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    (void)prev;
+    const unsigned int arrived =
+        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived != (unsigned int)(n - 1)) return;
+    T s = T(0);
+    for (int c = 0; c < n; ++c)
+        s += __builtin_bit_cast(T, __hip_atomic_fetch_add(pv + 2 * (first + c), U(0), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT));
+    T out = alpha * s;
+    if (beta_nz) out += beta * y[blk.r0];
+    y[blk.r0] = out;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T, bool NT, bool BETA>
 __device__ __forceinline__ void spmv_tile(
     const SpmvBlock blk, const int *__restrict__ rowptr, const int *__restrict__ colidx,
     const unsigned short *__restrict__ cidx, int cbase, int cmax,
     const T *__restrict__ vals, const T *__restrict__ x, T *__restrict__ y,
-    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, T *lds,
-    T *wsum, int *rp_lds) {
+    T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, T *lds,
+    T *wsum, int *rp_lds, int fuse) {
     constexpr int VW = 16 / sizeof(T);
     constexpr int RPQ = (rsp::kSpmvMaxRows + kSpmvThreads) / kSpmvThreads;
     const int tid = threadIdx.x;
@@ -366,8 +405,10 @@ __device__ __forceinline__ void spmv_tile(
                 T out = alpha * t;
                 if (BETA) out += beta * y[blk.r0];
                 y[blk.r0] = out;
+            } else if (fuse) {
+                longrow_arrive<T>(blk, rowptr, partials, y, t, alpha, beta, BETA);
             } else {
-                partials[-(blk.r1 + 1)] = t;
+                partials[2 * -(blk.r1 + 1)] = t;
             }
         }
         return;
@@ -406,7 +447,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
     const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
     const int *__restrict__ cbases, const unsigned short *__restrict__ cidx, int cmax,
-    T *__restrict__ partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok) {
+    T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
@@ -420,7 +461,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
         if (w) lds_barrier();
         spmv_tile<T, NT, BETA>(blocks[t0 + w], rowptr, colidx, cidx, cbases[t0 + w], cmax, vals, x,
                                y, partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum,
-                               rp_lds);
+                               rp_lds, fuse);
     }
     return;
 #endif
@@ -433,7 +474,8 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     __builtin_amdgcn_s_setprio(RSP_PROBE_PRIO);
 #endif
     spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, cidx, cbases[b], cmax, vals, x, y,
-                           partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds);
+                           partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds,
+                           fuse);
 }
 
 // One long row per wave: y[row] = alpha * (0 + p0 + p1 + ...) (+ beta*y[row]),
@@ -448,7 +490,7 @@ __device__ __forceinline__ void fixup_row(const SpmvLongRow r, const T *__restri
     const T yv = (beta_nonzero && lane == 0) ? y[r.row] : T(0);
     T s = T(0);
     for (int c0 = 0; c0 < r.nchunks; c0 += 64) {
-        const T p = c0 + lane < r.nchunks ? partials[r.first + c0 + lane] : T(0);
+        const T p = c0 + lane < r.nchunks ? partials[2 * (r.first + c0 + lane)] : T(0);
         const int cn = min(64, r.nchunks - c0);
         for (int c = 0; c < cn; ++c) s += __shfl(p, c, 64);
     }
@@ -477,11 +519,15 @@ __global__ __launch_bounds__(64) void spmv_longrow_fixup(const SpmvLongRow *__re
 template <typename T, bool NT, bool BETA, bool SWZ>
 __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     const SpmvBatchEntry *__restrict__ entries, const SpmvBlock *__restrict__ tiles,
-    const int *__restrict__ cbases, SpmvBatchTable at, T alpha, T beta) {
+    const int *__restrict__ cbases, SpmvBatchTable at, T alpha, T beta, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
     const int b = blockIdx.x;
+    // lo / hi selected inside the compare chain (84 SGPRs with the swizzle).
+    // Counting j first and reading lo / hi by index gets 76 SGPRs (8 rather
+    // than 7 workgroups per CU by the residency rule) but puts a dependent
+    // scalar load in front of the tile: 1 % slower on the big set.
     int j = 0, lo = 0, hi = at.begin[1];
 #pragma unroll
     for (int q = 1; q < kSpmvBatchMax; ++q)  // scalar compares, no loads
@@ -495,7 +541,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     spmv_tile<T, NT, BETA>(tiles[t], e.rowptr, e.colidx, e.cidx, cbases[t], e.cmax,
                            (const T *)e.vals, (const T *)e.x,
                            (T *)e.y, (T *)e.partials, alpha, beta, BETA, e.nnz, e.vector_ok, lds,
-                           wsum, rp_lds);
+                           wsum, rp_lds, fuse);
 }
 
 template <typename T>
@@ -516,6 +562,7 @@ static hipError_t launch_spmv_batch(const SpmvBatchArgs &a, hipStream_t s) {
     const T alpha = (T)a.alpha, beta = (T)a.beta;
     const int bnz = a.beta != 0.0;
     const int ntiles = a.tiles_at.begin[a.count];
+    const int fuse = !(a.variant & rsp::kSpmvVariantFixup);
     if (ntiles > 0) {
         const bool nt = !(a.variant & 1), swz = !(a.variant & 8);
         auto kern = bnz ? (nt ? (swz ? spmv_tiles_batch<T, true, true, true>
@@ -527,12 +574,12 @@ static hipError_t launch_spmv_batch(const SpmvBatchArgs &a, hipStream_t s) {
                               : (swz ? spmv_tiles_batch<T, false, false, true>
                                      : spmv_tiles_batch<T, false, false, false>));
         hipLaunchKernelGGL(kern, dim3(ntiles), dim3(kSpmvThreads), 0, s, a.entries, a.tiles,
-                           a.cbases, a.tiles_at, alpha, beta);
+                           a.cbases, a.tiles_at, alpha, beta, fuse);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     const int nlong = a.longs_at.begin[a.count];
-    if (nlong > 0) {
+    if (nlong > 0 && !fuse) {
         // the fixup reads begin[kSpmvBatchMax] as its bound: the table past
         // `count` holds INT_MAX, so pass the total explicitly
         SpmvBatchTable lt = a.longs_at;
@@ -553,6 +600,7 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     if (a.nblocks <= 0) return hipSuccess;
     const T alpha = (T)a.alpha, beta = (T)a.beta;
     const int bnz = a.beta != 0.0;
+    const int fuse = !(a.variant & rsp::kSpmvVariantFixup);
     // vals/colidx are read once per call: non-temporal loads keep them from
     // evicting x (measured +2% fp64 / +7.5% fp32 on the cache-cold big set);
     // variant bit 0 restores default-policy loads for A/B runs
@@ -561,10 +609,10 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(RSP_PROBE_WALK ? (a.nblocks + RSP_PROBE_WALK - 1) / (RSP_PROBE_WALK ? RSP_PROBE_WALK : 1)
                                                 : a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
                        (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks, a.cbases,
-                       a.cidx, a.cmax, (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok);
+                       a.cidx, a.cmax, (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok, fuse);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (a.nlong > 0) {
+    if (a.nlong > 0 && !fuse) {
         hipLaunchKernelGGL((spmv_longrow_fixup<T>), dim3(a.nlong), dim3(64), 0, s,
                            a.longrows, a.nlong, (const T *)a.partials, (T *)a.y, alpha, beta, bnz);
         e = hipGetLastError();

@@ -96,12 +96,52 @@ def test_surrogates(handle, name, scale, dtype):
 
 def test_long_rows_exercised(handle):
     """ASIC_320ks has hub rows far longer than one tile (fp64 2047 / fp32 4093
-    entries): they take the chunked path + fixup kernel."""
+    entries): they take the chunked path (finished by the last-arriving chunk)."""
     A = csr.surrogate("ASIC_320ks")
     assert np.diff(A.rowptr).max() > 4093
     x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
     for dt in (torch.float64, torch.float32):
         check(A, x, dt, handle)
+
+
+def test_long_row_tickets_repeat(handle):
+    """Chunked long rows are finished inside the tile kernel by the chunk that
+    arrives last (agent-scope atomics; an arrival ticket per row that the last
+    arriver resets). Many back-to-back calls, with beta = 0 and beta != 0,
+    must give the oracle's bits every time: a ticket left non-zero or a stale
+    partial would show up as a wrong or missing y[row]."""
+    rng = np.random.default_rng(11)
+    n, hub = 20000, 9000  # 5 fp64 chunks / 3 fp32 chunks per hub row
+    rows, cols = [], []
+    for i in range(n):
+        if i % 997 == 0:  # hub rows
+            c = np.sort(rng.choice(n, hub, replace=False)).astype(np.int32)
+        else:
+            c = np.unique(np.clip(i + rng.integers(-30, 31, 5), 0, n - 1)).astype(np.int32)
+        cols.append(c)
+        rows.append(len(c))
+    rp = np.zeros(n + 1, np.int32)
+    np.cumsum(rows, out=rp[1:])
+    ci = np.concatenate(cols)
+    A = csr.CsrMatrix(0, n, n, len(ci), rp, ci, rng.uniform(-1, 1, len(ci)))
+    x = rng.uniform(-1, 1, n)
+    y0 = rng.uniform(-1, 1, n)
+    for dt in (torch.float64, torch.float32):
+        v, xx, yy = A.values.astype(NP[dt]), x.astype(NP[dt]), y0.astype(NP[dt])
+        canon = ob.spmv(A.rowptr, A.colidx, v, xx, order="canon")
+        rp_d, ci_d, va_d = upload_csr(A.rowptr, A.colidx, A.values, dt)
+        mat = SpMat(handle, rp_d, ci_d, va_d, n)
+        xd = torch.from_numpy(xx).cuda()
+        for rep in range(20):
+            y = mat.spmv(xd).cpu().numpy()
+            assert same_bits(y, canon), f"{dt} call {rep}"
+        # beta != 0 on the same workspace: y = 2 A x + 0.5 y0 (hub rows included)
+        yd = torch.from_numpy(yy.copy()).cuda()
+        got = mat.spmv(xd, yd, 2.0, 0.5).cpu().numpy()
+        hubs = np.arange(0, n, 997)
+        t = (NP[dt](2.0) * canon + NP[dt](0.5) * yy).astype(NP[dt])
+        assert same_bits(got[hubs], t[hubs])
+        assert same_bits(mat.spmv(xd).cpu().numpy(), canon)
 
 
 def test_single_dense_row_and_column(handle):
@@ -240,7 +280,7 @@ def test_column_offset_tiles(handle):
         check(A, x, dt, handle)
 
 
-@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33, 64, 128, 80])
+@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33, 64, 128, 80, 256, 257])
 def test_kernel_variants_same_bits(monkeypatch, variant):
     """Every kernel / plan variant (RSP_SPMV_VARIANT: default-policy instead of
     non-temporal loads; small plans not spread over the chip; int32 column
