@@ -524,10 +524,13 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
     const int b = blockIdx.x;
-    // lo / hi selected inside the compare chain (84 SGPRs with the swizzle).
-    // Counting j first and reading lo / hi by index gets 76 SGPRs (8 rather
-    // than 7 workgroups per CU by the residency rule) but puts a dependent
-    // scalar load in front of the tile: 1 % slower on the big set.
+    // lo / hi selected inside the compare chain on the kernel arguments
+    // (preloaded into SGPRs, so no memory latency in front of the tile
+    // record load). 84 SGPRs with the swizzle = 7 rather than 8 workgroups
+    // per CU by the residency rule, which measured equal to 8 on the
+    // one-matrix kernel; both lookups that needed fewer SGPRs (begin[j] read
+    // by index after counting j: 76; a ballot over begin[lane]: 42) put a
+    // load in front of the tile and measured 1-2 % slower.
     int j = 0, lo = 0, hi = at.begin[1];
 #pragma unroll
     for (int q = 1; q < kSpmvBatchMax; ++q)  // scalar compares, no loads
