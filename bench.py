@@ -75,20 +75,20 @@ class Slice:
         self.nnz_local = int(rp[-1])
         self.x_global_slice = csr.dlarnv(1, [0, 0, 0, 1], m)[0][r0:r1]
         self.mode = exchange if world > 1 else "none"
-        if self.mode == "halo":
+        self.ci_global = ci
+        self.handle, self.device, self.overlap = handle, device, overlap
+        if self.mode == "halo":  # matrices uploaded by bind_halo, in the exchange's column layout
             self.halo = HaloSlice(ci, self.bounds, rank)
-            ci_dev, self.n_x = self.halo.colidx_ext, self.halo.n_ext
-        elif self.mode == "allgather":
-            ci_dev, chunk = remap_columns(ci, self.bounds)
-            self.n_x = world * chunk
+            self.n_x = self.halo.n_ext  # x entries the slice reads (algorithmic bytes)
+            self.host = (rp, None, va)
         else:
-            ci_dev, self.n_x = ci, m
-        self.host = (rp, ci_dev, va)
-        self.mat64 = SpMat(handle, *upload_csr(rp, ci_dev, va, torch.float64, device), self.n_x)
-        self.mat32 = SpMat(handle, *upload_csr(rp, ci_dev, va, torch.float32, device), self.n_x)
-        if self.mode == "halo" and overlap:  # interior tiles (own columns only) run under the exchange
-            self.mat64.set_local_cols(self.m_local)
-            self.mat32.set_local_cols(self.m_local)
+            if self.mode == "allgather":
+                ci_dev, chunk = remap_columns(ci, self.bounds)
+                self.n_x = world * chunk
+            else:
+                ci_dev, self.n_x = ci, m
+            self.host = (rp, ci_dev, va)
+            self._upload(ci_dev, self.n_x)
         self.y64 = torch.empty(max(self.m_local, 1), dtype=torch.float64, device=device)
         self.y32 = torch.empty(max(self.m_local, 1), dtype=torch.float32, device=device)
         if self.mode != "halo":  # replicated x (padded layout for the all-gather)
@@ -99,8 +99,19 @@ class Slice:
             self.part64.exchange()
             self.part32.exchange()
 
+    def _upload(self, ci_dev, ncols):
+        rp, _, va = self.host
+        self.mat64 = SpMat(self.handle, *upload_csr(rp, ci_dev, va, torch.float64, self.device), ncols)
+        self.mat32 = SpMat(self.handle, *upload_csr(rp, ci_dev, va, torch.float32, self.device), ncols)
+        if self.mode == "halo" and self.overlap:  # interior tiles (own columns only) run under the exchange
+            self.mat64.set_local_cols(self.m_local)
+            self.mat32.set_local_cols(self.m_local)
+
     def bind_halo(self, i, ex64, ex32):
         self.i, self.ex64, self.ex32 = i, ex64, ex32
+        ci_dev = ex64.colidx(i)  # same layout in both arenas
+        self.host = (self.host[0], ci_dev, self.host[2])
+        self._upload(ci_dev, ex64.n_x(i))
         ex64.x_local(i).copy_(torch.from_numpy(self.x_global_slice))
         ex32.x_local(i).copy_(torch.from_numpy(self.x_global_slice.astype(np.float32)))
 
@@ -180,6 +191,9 @@ def main():
                     help="N>1 x exchange: halo-only all_to_all (default) or full all-gather")
     ap.add_argument("--no-bucket", action="store_true",
                     help="halo mode: one exchange per matrix instead of one per step")
+    ap.add_argument("--halo-unpack", action="store_true",
+                    help="halo mode: receive into a buffer and unpack it into each slice's x "
+                         "(one more launch per step) instead of receiving in place")
     ap.add_argument("--no-overlap", action="store_true",
                     help="halo mode: finish the exchange before any SpMV instead of running the "
                          "interior tiles under it")
@@ -218,8 +232,11 @@ def main():
     if world > 1 and args.exchange == "halo":
         groups = [[i] for i in range(len(slices))] if args.no_bucket else [list(range(len(slices)))]
         for g in groups:
-            ex64 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float64, device, handle)
-            ex32 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float32, device, handle)
+            direct = not args.halo_unpack
+            ex64 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float64, device, handle,
+                                direct=direct)
+            ex32 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float32, device, handle,
+                                direct=direct)
             for j, i in enumerate(g):
                 slices[i].bind_halo(j, ex64, ex32)
             ex64.exchange()
@@ -396,10 +413,9 @@ def main():
     bound = ob.spmv_bound(rp, ci_dev, va, xf, 2.0 ** -53)
     # the exchanged x must hold exactly the global x entries the slice references
     ok_x = True
-    if big.mode == "halo":
+    if big.mode == "halo":  # every entry the slice reads is the global x entry of its column
         xg = csr.dlarnv(1, [0, 0, 0, 1], big.n)[0]
-        cols = np.concatenate([c for c in big.halo.recv_cols])
-        ok_x = np.array_equal(xf[big.m_local:], xg[cols]) and np.array_equal(xf[: big.m_local], xg[big.r0:big.r1])
+        ok_x = np.array_equal(xf[ci_dev], xg[big.ci_global])
     # the step's y (overlapped split at N > 1) equals one whole SpMV bit for bit
     ok_step = np.array_equal(y_step, got) if big.m_local else True
     check_ok = bool(np.all(np.abs(got - ref) <= bound)) and ok_x and ok_step
@@ -433,7 +449,8 @@ def main():
                 "launch": "one rsp_spmv per matrix" if args.no_batch else
                           (f"rsp_spmv_batch ({per_step} launch(es) of <= 32 matrices per step part): "
                            + ("interior, then boundary" if overlap else "whole step")),
-                "collective": (("halo all_to_all_single" + ("" if args.no_bucket else
+                "collective": (("halo all_to_all_single" + ("" if args.halo_unpack else ", received in place")
+                                 + ("" if args.no_bucket else
                                  " (one per step, bucketed over the matrices)")
                                  + (", interior tiles overlapped" if overlap else "")
                                  if args.exchange == "halo" else "all_gather_into_tensor")

@@ -170,16 +170,33 @@ class HaloExchange:
     """Bucketed halo exchange for the slices of several matrices on one rank.
 
     Setup is collective (every rank constructs it with its slices in the same
-    order). `arena` holds every slice's x_ext back to back; `x_ext(i)` is slice
-    i's view, `x_local(i)` its owned part. `exchange()` refreshes every halo
-    with one all_to_all_single."""
+    order). `exchange()` refreshes every halo with one all_to_all_single.
+
+    Layouts of the arena that holds every slice's x:
+    * packed (direct=False): slice i's x_ext = [own rows | halo] back to back,
+      columns as HaloSlice.colidx_ext; the all-to-all lands in a receive
+      buffer and an unpack kernel (rsp_scatter) copies it into the halos.
+    * direct (direct=True): [own rows of slice 0 | ... of slice S-1 | receive
+      region]; the all-to-all writes straight into the receive region (ordered
+      by source rank, then slice, then column) and slice i's columns are
+      remapped once (`colidx(i)`) to index the arena from its own part's
+      start, so its halo entries point into the receive region. No unpack
+      launch per step; own columns stay [0, m_local), so the interior/boundary
+      tile split (rsp_spmat_set_local_cols) is unchanged.
+    `x_ext(i)` is the vector slice i's SpMV reads (`n_x(i)` entries),
+    `x_local(i)` its owned part."""
 
     def __init__(self, slices: list[HaloSlice], rank: int, world: int, dtype: torch.dtype,
-                 device, handle=None, group=None):
+                 device, handle=None, group=None, direct: bool = False):
         self.slices, self.rank, self.P, self.group = slices, rank, world, group
         self.dtype, self.device, self.handle = dtype, torch.device(device), handle
-        self.offsets = np.concatenate([[0], np.cumsum([s.n_ext for s in slices])]).astype(np.int64)
-        self.arena = torch.zeros(max(int(self.offsets[-1]), 1), dtype=dtype, device=self.device)
+        self.direct = direct
+        sizes = [s.m_local for s in slices] if direct else [s.n_ext for s in slices]
+        self.offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        n_recv_all = int(sum(int(s.recv_counts.sum()) for s in slices))
+        self.recv_off = int(self.offsets[-1])
+        total = self.recv_off + (n_recv_all if direct else 0)
+        self.arena = torch.zeros(max(total, 1), dtype=dtype, device=self.device)
         # 1) who wants what: counts then the requested global columns
         idx_dev = self.device if (self.device.type == "cuda" and
                                   dist.get_backend(group) != "gloo") else torch.device("cpu")
@@ -210,21 +227,59 @@ class HaloExchange:
                 pack.append(self.offsets[i] + (cols - s.r0))
         self.send_split = out_split
         self.recv_split = in_split
-        # 3) unpack index: data from source p arrives ordered (slice i, column)
-        unpack = []
+        # 3) data from source p arrives ordered (slice i, column): where block
+        # (p, i) starts in the receive stream
+        self.recv_start = np.zeros((world, len(slices)), np.int64)
+        pos = 0
         for p in range(world):
             for i, s in enumerate(slices):
-                c = int(s.recv_counts[p])
-                start = self.offsets[i] + s.m_local + s.halo_offsets()[p]
-                unpack.append(np.arange(start, start + c, dtype=np.int64))
+                self.recv_start[p, i] = pos
+                pos += int(s.recv_counts[p])
+        self.n_recv = pos
         cat = lambda a: np.concatenate(a) if a else np.zeros(0, np.int64)  # noqa: E731
         self.pack_idx = torch.from_numpy(cat(pack)).to(self.device)
-        self.unpack_idx = torch.from_numpy(cat(unpack)).to(self.device)
         self.sendbuf = torch.empty(max(self.pack_idx.numel(), 1), dtype=dtype, device=self.device)
-        self.recvbuf = torch.empty(max(self.unpack_idx.numel(), 1), dtype=dtype, device=self.device)
+        if direct:  # the all-to-all writes the arena's receive region itself
+            self.unpack_idx = torch.zeros(0, dtype=torch.int64, device=self.device)
+            self.recvbuf = self.arena[self.recv_off:self.recv_off + max(self.n_recv, 1)]
+        else:  # unpack index: receive stream -> each slice's halo
+            unpack = []
+            for p in range(world):
+                for i, s in enumerate(slices):
+                    c = int(s.recv_counts[p])
+                    start = self.offsets[i] + s.m_local + s.halo_offsets()[p]
+                    unpack.append(np.arange(start, start + c, dtype=np.int64))
+            self.unpack_idx = torch.from_numpy(cat(unpack)).to(self.device)
+            self.recvbuf = torch.empty(max(self.unpack_idx.numel(), 1), dtype=dtype, device=self.device)
         self._work = None
 
+    def colidx(self, i: int) -> np.ndarray:
+        """Column indices of slice i into x_ext(i) (int32)."""
+        s = self.slices[i]
+        if not self.direct:
+            return s.colidx_ext
+        ext = s.colidx_ext.astype(np.int64)
+        h = ext - s.m_local
+        halo = h >= 0
+        offs = s.halo_offsets()
+        owner = np.searchsorted(offs, h[halo], side="right") - 1
+        # several owners may hold no columns (equal offsets): side="right"
+        # picks the last of them, the one whose block is non-empty
+        base = self.recv_off - int(self.offsets[i])
+        ext[halo] = base + self.recv_start[owner, i] + (h[halo] - offs[owner])
+        if ext.size and int(ext.max()) > np.iinfo(np.int32).max:
+            raise ValueError("arena does not fit int32 indices")
+        return ext.astype(np.int32)
+
+    def n_x(self, i: int) -> int:
+        """Length of x_ext(i) (the column count of slice i's matrix)."""
+        if self.direct:
+            return max(int(self.arena.numel() - self.offsets[i]), self.slices[i].m_local)
+        return self.slices[i].n_ext
+
     def x_ext(self, i: int) -> torch.Tensor:
+        if self.direct:
+            return self.arena[int(self.offsets[i]):]
         return self.arena[int(self.offsets[i]):int(self.offsets[i + 1])]
 
     def x_local(self, i: int) -> torch.Tensor:
@@ -232,7 +287,8 @@ class HaloExchange:
 
     @property
     def bytes_per_exchange(self) -> int:
-        return int(self.pack_idx.numel() + self.unpack_idx.numel()) * self.arena.element_size()
+        """Halo bytes this rank sends plus receives per exchange."""
+        return int(self.pack_idx.numel() + self.n_recv) * self.arena.element_size()
 
     def exchange(self) -> None:
         self.start()
@@ -244,7 +300,7 @@ class HaloExchange:
         self._work = None
         if self.P <= 1:
             return
-        n_send, n_recv = self.pack_idx.numel(), self.unpack_idx.numel()
+        n_send, n_recv = self.pack_idx.numel(), self.n_recv
         if self.device.type == "cuda":
             from .sparse import gather
             if n_send:
@@ -260,6 +316,7 @@ class HaloExchange:
             self.sendbuf[:n_send] = self.arena[self.pack_idx]
             dist.all_to_all_single(self.recvbuf[:n_recv], self.sendbuf[:n_send],
                                    list(self.recv_split), list(self.send_split), group=self.group)
+        assert sum(self.recv_split) == n_recv
 
     def finish(self) -> None:
         """Wait for the all-to-all (on the current stream) and unpack the halos."""
@@ -268,6 +325,8 @@ class HaloExchange:
         if self._work is not None:
             self._work.wait()
             self._work = None
+        if self.direct:  # received in place
+            return
         n_recv = self.unpack_idx.numel()
         if self.device.type == "cuda":
             from .sparse import scatter

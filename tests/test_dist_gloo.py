@@ -74,7 +74,7 @@ def test_row_partitioned_spmv_gloo(world, name):
         assert np.array_equal(y, ref), rank
 
 
-def _halo_worker(rank, world, port, names, scale, bucket, q):
+def _halo_worker(rank, world, port, names, scale, bucket, q, direct=False):
     from respasol_amd.dist import HaloExchange, HaloSlice
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -90,36 +90,45 @@ def _halo_worker(rank, world, port, names, scale, bucket, q):
             rp, ci, va = csr.surrogate_rows_csr(name, r0, r1, scale)
             hs = HaloSlice(ci, bounds, rank)
             slices.append(hs)
-            hosts.append((rp, va, csr.dlarnv(2, [0, 0, 0, 1], m)[0], r0, r1))
+            hosts.append((rp, va, csr.dlarnv(2, [0, 0, 0, 1], m)[0], r0, r1, ci))
         groups = [list(range(len(names)))] if bucket else [[i] for i in range(len(names))]
         out = {}
         for g in groups:
-            ex = HaloExchange([slices[i] for i in g], rank, world, torch.float64, "cpu")
+            ex = HaloExchange([slices[i] for i in g], rank, world, torch.float64, "cpu", direct=direct)
             for j, i in enumerate(g):
-                rp, va, x, r0, r1 = hosts[i]
+                rp, va, x, r0, r1, ci = hosts[i]
                 ex.x_local(j).copy_(torch.from_numpy(x[r0:r1]))
             ex.exchange()
             for j, i in enumerate(g):
-                rp, va, x, r0, r1 = hosts[i]
+                rp, va, x, r0, r1, ci = hosts[i]
                 xe = ex.x_ext(j).numpy()
-                ok_x = np.array_equal(xe[slices[i].m_local:], x[np.concatenate(slices[i].recv_cols)])
-                out[names[i]] = (r0, r1, ob.spmv(rp, slices[i].colidx_ext, va, xe), ok_x,
-                                 slices[i].H)
+                cols = ex.colidx(j)
+                assert cols.dtype == np.int32 and (cols.size == 0 or cols.max() < ex.n_x(j))
+                assert len(xe) == ex.n_x(j)
+                # every entry the slice reads is the global x entry of its column
+                ok_x = np.array_equal(xe[cols], x[ci])
+                if not direct:
+                    ok_x = ok_x and np.array_equal(xe[slices[i].m_local:],
+                                                   x[np.concatenate(slices[i].recv_cols)])
+                out[names[i]] = (r0, r1, ob.spmv(rp, cols, va, xe), ok_x, slices[i].H)
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,bucket", [(2, True), (3, True), (2, False)])
-def test_halo_exchange_gloo(world, bucket):
+@pytest.mark.parametrize("world,bucket,direct", [(2, True, False), (3, True, False), (2, False, False),
+                                                 (2, True, True), (4, True, True), (3, False, True)])
+def test_halo_exchange_gloo(world, bucket, direct):
     """Halo-only exchange (all_to_all with per-peer splits), bucketed over
-    several matrices: every rank's y slice equals the single-process y
-    bitwise, and each rank received exactly the x entries it references."""
+    several matrices, in both arena layouts (halo unpacked into each slice's
+    x, or received in place with the columns remapped): every rank's y slice
+    equals the single-process y bitwise, and every x entry a slice reads is
+    the global x entry of its column."""
     names, scale = ["Serena", "G2_circuit", "cage13", "ML_Laplace"], 0.01
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, names, scale, bucket, q))
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, names, scale, bucket, q, direct))
              for r in range(world)]
     for p in procs:
         p.start()
