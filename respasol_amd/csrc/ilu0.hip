@@ -157,6 +157,59 @@ __global__ __launch_bounds__(64 * kIluWaves) void ilu0_level(IluArgs a, int off,
     factor_row<T, B>(a, a.plan.rows[off + w], threadIdx.x & 63);
 }
 
+// The stages of one fat-level row on LDS operands (ilu0_level_lds and
+// ilu0_level_slot): lower positions stage by stage, l_ij = v / u_jj, then the
+// upper positions; rv holds the row's values on entry and its factor on exit.
+template <typename T>
+__device__ __forceinline__ void row_lds_factor(T *rv, const T *dv, const T *pu, const int *up,
+                                               const int *lo, const int *le, const unsigned short *pl,
+                                               int nlo, int nr, int lane, int hasdiag, int i,
+                                               int *zero_pivot) {
+    auto wave_sync = [] {  // order this wave's LDS stores before its later loads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    };
+    wave_sync();
+    auto entry = [&](int x) {  // a_ij - sum l_ik u_kj over its pairs, k ascending
+        T v = rv[x];
+        const int u0 = up[x], u1 = up[x + 1];
+        auto batch = [&](int u) {
+            T l[4], w[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int uu = min(u + b, u1 - 1);
+                l[b] = rv[pl[uu]];
+                w[b] = pu[uu];
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (u + b < u1) v = fma_t(-l[b], w[b], v);
+        };
+        if (u1 > u0) {  // the first batch straight-line
+            batch(u0);
+            for (int u = u0 + 4; u < u1; u += 4) batch(u);
+        }
+        return v;
+    };
+    for (int s = 0; s < nlo;) {  // lower positions, stage by stage
+        const int e = le[s];
+        for (int x = s + lane; x < e; x += 64) {
+            const int r = lo[x];
+            const T d = dv[r];  // read before the chain, not after it
+            rv[r] = entry(r) / d;
+        }
+        wave_sync();
+        s = e;
+    }
+    for (int x = nlo + lane; x < nr; x += 64) {  // upper positions (never operands of this row)
+        const T v = entry(x);
+        rv[x] = v;
+        if (x == nlo && hasdiag && v == T(0)) atomicMin(zero_pivot, i);
+    }
+    wave_sync();
+}
+
 // Fat level, one wave (workgroup) per row with the row staged in LDS. Every
 // operand that does not come from the row itself is final before the level
 // starts: the u_kj of all the row's update pairs (rows of earlier levels)
@@ -198,49 +251,77 @@ __global__ __launch_bounds__(64) void ilu0_level_lds(IluArgs a, int off) {
         pl[u] = (unsigned short)(a.upd_l[q0 + u] - rs);
         pu[u] = vals[a.upd_u[q0 + u]];
     }
-    auto wave_sync = [] {  // order this wave's LDS stores before its later loads
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    };
-    wave_sync();
-    auto entry = [&](int x) {  // a_ij - sum l_ik u_kj over its pairs, k ascending
-        T v = rv[x];
-        const int u0 = up[x], u1 = up[x + 1];
-        auto batch = [&](int u) {
-            T l[4], w[4];
+    row_lds_factor<T>(rv, dv, pu, up, lo, le, pl, nlo, nr, lane, fr.hasdiag, i, a.zero_pivot);
+    for (int x = lane; x < nr; x += 64) vals[rs + x] = rv[x];
+}
+
+// Fat level in the slot layout (rsp::FacSlotLevel): the row's structure is
+// one fixed-stride slot, so its header, divisor positions, packed stage
+// structure and update pairs are one memory round trip, issued together
+// (KR / KQ = the level's entries / pairs per lane, compile-time, loads
+// clamped and unpredicated); the values they point at (the row's a_ij, its
+// divisors u_kk, the u_kj of its pairs) are the second. ilu0_level_lds reads
+// a record first and then loops over its arrays, a dependent round trip per
+// 64 pairs. Same LDS stages (row_lds_factor), so the same bits.
+template <typename T, int KR, int KQ>
+__global__ __launch_bounds__(64) void ilu0_level_slot(IluArgs a, const int *__restrict__ lvl, int stride,
+                                                      int rm, int qm) {
+    constexpr int R = rsp::kFacRow, Q = rsp::kFacPairs;
+    static_assert(KR * 64 <= R && KQ * 64 <= Q, "slot kernel budgets");
+    __shared__ T rv[R], dv[R], pu[Q];
+    __shared__ int up[R + 1], lo[R], le[R];
+    __shared__ unsigned short pl[Q];
+    const int lane = threadIdx.x;
+    const int *slot = lvl + (size_t)blockIdx.x * stride;
+    const int pa = rsp::fac_pairs_at(rm);
+    int dpos_[KR], bw[KR];
+    int2 pr[KQ];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int uu = min(u + b, u1 - 1);
-                l[b] = rv[pl[uu]];
-                w[b] = pu[uu];
-            }
+    for (int k = 0; k < KR; ++k) {  // clamped to the level's region sizes (rm, qm >= 1 here)
+        const int x = min(lane + 64 * k, rm - 1);
+        dpos_[k] = slot[8 + x];
+        bw[k] = slot[8 + rm + x];
+    }
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if (u + b < u1) v = fma_t(-l[b], w[b], v);
-        };
-        if (u1 > u0) {  // the first batch straight-line
-            batch(u0);
-            for (int u = u0 + 4; u < u1; u += 4) batch(u);
-        }
-        return v;
-    };
-    for (int s = 0; s < nlo;) {  // lower positions, stage by stage
-        const int e = le[s];
-        for (int x = s + lane; x < e; x += 64) {
-            const int r = lo[x];
-            const T d = dv[r];  // read before the chain, not after it
-            rv[r] = entry(r) / d;
-        }
-        wave_sync();
-        s = e;
+    for (int k = 0; k < KQ; ++k)
+        pr[k] = *reinterpret_cast<const int2 *>(slot + pa + 2 * min(lane + 64 * k, qm - 1));
+    const int i = slot[0], rs = slot[1], nlo = slot[2], nr = slot[3], nq = slot[4];
+    const int hasdiag = slot[5], global = slot[6];
+    if (global) {
+        factor_row<T, 4>(a, i, lane);
+        return;
     }
-    for (int x = nlo + lane; x < nr; x += 64) {  // upper positions (never operands of this row)
-        const T v = entry(x);
-        rv[x] = v;
-        if (x == nlo && fr.hasdiag && v == T(0)) atomicMin(a.zero_pivot, i);
+    T *vals = (T *)a.vals;
+    T av[KR], dd[KR], uv[KQ];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const int x = min(lane + 64 * k, nr - 1);
+        av[k] = vals[rs + x];
+        dd[k] = vals[max(dpos_[k], 0)];
     }
-    wave_sync();
+#pragma unroll
+    for (int k = 0; k < KQ; ++k) uv[k] = vals[pr[k].x];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+        const int x = lane + 64 * k;
+        if (x < nr) {
+            rv[x] = av[k];
+            dv[x] = dpos_[k] >= 0 ? dd[k] : T(0);
+            up[x] = bw[k] & 0x7ff;
+            lo[x] = (bw[k] >> 11) & 0x1ff;
+            le[x] = (bw[k] >> 20) & 0x1ff;
+        }
+    }
+    if (lane == 0) up[nr] = nq;
+#pragma unroll
+    for (int k = 0; k < KQ; ++k) {
+        const int u = lane + 64 * k;
+        if (u < nq) {
+            pl[u] = (unsigned short)pr[k].y;
+            pu[u] = uv[k];
+        }
+    }
+    row_lds_factor<T>(rv, dv, pu, up, lo, le, pl, nlo, nr, lane, hasdiag, i, a.zero_pivot);
     for (int x = lane; x < nr; x += 64) vals[rs + x] = rv[x];
 }
 
@@ -961,7 +1042,17 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
         for (int l = sg.lb; l < sg.le; ++l) {
             const int off = P.ptr_host[l], cnt = P.ptr_host[l + 1] - off;
             if (cnt <= 0) continue;
-            if (a.fat_lds)
+            const rsp::FacSlotLevel *sl = a.fat_slots && a.fslev ? &a.fslev[l] : nullptr;
+            if (sl && sl->stride > 0 && sl->rm > 0 && sl->qm > 0) {
+                const int *lvl = a.fslots + sl->off;
+                auto kern = sl->rm <= 64 ? (sl->qm <= 128 ? ilu0_level_slot<T, 1, 2>
+                                                          : sl->qm <= 512 ? ilu0_level_slot<T, 1, 8>
+                                                                          : ilu0_level_slot<T, 1, 16>)
+                                         : (sl->qm <= 128 ? ilu0_level_slot<T, 4, 2>
+                                                          : sl->qm <= 512 ? ilu0_level_slot<T, 4, 8>
+                                                                          : ilu0_level_slot<T, 4, 16>);
+                hipLaunchKernelGGL(kern, dim3(cnt), dim3(64), 0, s, a, lvl, sl->stride, sl->rm, sl->qm);
+            } else if (a.fat_lds)
                 hipLaunchKernelGGL((ilu0_level_lds<T, B>), dim3(cnt), dim3(64), 0, s, a, off);
             else
                 hipLaunchKernelGGL((ilu0_level<T, B>), dim3((cnt + kIluWaves - 1) / kIluWaves),

@@ -120,6 +120,8 @@ struct rsp_ilu0_info {
     rsp::RndChunk *d_rchunks = nullptr;        // round-based factor chunks (thin runs)
     rsp::RndItem *d_ritems = nullptr;
     rsp::FacRow *d_frow = nullptr;
+    int *d_fslots = nullptr;                   // fat factor levels, slot layout (ilu0_level_slot)
+    std::vector<rsp::FacSlotLevel> fslev;      // per L level (stride 0: FacRow path)
     int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
     int fac_batch;
 };
@@ -935,8 +937,9 @@ static void ilu_free_device(rsp_ilu0_info *f) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
-    for (void **p : {(void **)&f->d_frow, (void **)&f->d_rchunks, (void **)&f->d_ritems, (void **)&f->d_rpairs,
-                     (void **)&f->d_rstaged, (void **)&f->d_rrounds}) {
+    f->fslev.clear();
+    for (void **p : {(void **)&f->d_frow, (void **)&f->d_fslots, (void **)&f->d_rchunks, (void **)&f->d_ritems,
+                     (void **)&f->d_rpairs, (void **)&f->d_rstaged, (void **)&f->d_rrounds}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -1673,6 +1676,74 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
                                   hasdiag[(size_t)i], 0};
         }
         if (e == hipSuccess) e = upload_vec(&f->d_frow, frow);
+        // fat factor levels in the slot layout (rsp::FacSlotLevel): each row's
+        // structure at a fixed stride, so ilu0_level_slot reads it in one
+        // round trip. Levels past RSP_ILU_SLOT_CAP_MB of slots keep FacRow.
+        const std::vector<int> &lp = f->L.ptr;
+        const int nlev = (int)lp.size() - 1;
+        f->fslev.assign((size_t)std::max(nlev, 0), rsp::FacSlotLevel{0, 0, 0, 0, 0});
+        const long long cap = (long long)env_int("RSP_ILU_SLOT_CAP_MB", 2048) * (1LL << 20) / 4;
+        long long total = 0;
+        std::vector<int> slot_levels;
+        for (const rsp::LevelSeg &sg : fplan.segs) {
+            if (sg.thin) continue;
+            for (int l = sg.lb; l < sg.le; l++) {
+                int rm = 0, qm = 0;
+                for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
+                    const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
+                    const int nq = sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs];
+                    if (re - rs <= rsp::kFacRow && nq <= rsp::kFacPairs) {
+                        rm = std::max(rm, re - rs);
+                        qm = std::max(qm, nq);
+                    }
+                }
+                if (rm == 0 || qm == 0) continue;
+                const int stride = (rsp::fac_pairs_at(rm) + 2 * qm + 3) & ~3;
+                const long long cnt = lp[(size_t)l + 1] - lp[(size_t)l];
+                if (total + cnt * stride > cap) continue;
+                f->fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, rm, qm, 0};
+                total += cnt * stride;
+                slot_levels.push_back(l);
+            }
+        }
+        if (total > 0) {
+            std::vector<int> slots((size_t)total, 0);
+            std::vector<int> xs, xl;  // level-order slots of the slot-layout levels, their level
+            for (int l : slot_levels)
+                for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
+                    xs.push_back(x);
+                    xl.push_back(l);
+                }
+            parallel_rows((int)xs.size(), [&](int t0, int t1) {
+                for (int t = t0; t < t1; t++) {
+                    const int x = xs[(size_t)t], l = xl[(size_t)t];
+                    const rsp::FacSlotLevel &sl = f->fslev[(size_t)l];
+                    const int pa = rsp::fac_pairs_at(sl.rm);
+                    int *q = slots.data() + sl.off + (long long)(x - lp[(size_t)l]) * sl.stride;
+                    const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
+                    const int nr = re - rs, nlo = dpos[(size_t)i] - rs;
+                    const int q0 = sym.upd_ptr[(size_t)rs], nq = sym.upd_ptr[(size_t)re] - q0;
+                    const int global = nr > rsp::kFacRow || nq > rsp::kFacPairs;
+                    q[0] = i, q[1] = rs, q[2] = nlo, q[3] = nr, q[4] = nq, q[5] = hasdiag[(size_t)i];
+                    q[6] = global;
+                    for (int y = 0; y < sl.rm; y++) q[8 + y] = -1;
+                    if (global) continue;
+                    for (int y = 0; y < nr; y++) {
+                        const size_t pp = (size_t)rs + y;
+                        const bool lower = y < nlo;
+                        q[8 + y] = lower ? udiv[pp] : -1;
+                        q[8 + sl.rm + y] = (sym.upd_ptr[pp] - q0) |
+                                           ((lower ? sym.lord[pp] - rs : 0) << 11) |
+                                           ((lower ? sym.lend[pp] - rs : 0) << 20);
+                    }
+                    for (int u = 0; u < nq; u++) {
+                        q[pa + 2 * u] = sym.upd_u[(size_t)q0 + u];
+                        q[pa + 2 * u + 1] = sym.upd_l[(size_t)q0 + u] - rs;
+                    }
+                }
+            });
+            if (e == hipSuccess) e = upload(&f->d_fslots, slots);
+        }
     }
     if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
     if (e == hipSuccess) e = upload(&f->d_hasdiag, hasdiag);
@@ -1791,6 +1862,9 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.lend = f->d_lend;
     a.udiv = f->d_udiv;
     a.frow = f->d_frow;
+    a.fslots = f->d_fslots;
+    a.fslev = f->fslev.empty() ? nullptr : f->fslev.data();
+    a.fat_slots = f->d_fslots && env_int("RSP_ILU_FAT_SLOT", 1) != 0;
     a.fat_lds = env_int("RSP_ILU_FAT_LDS", 1) != 0;
     a.defer_rounds = env_int("RSP_ILU_DEFER", 8);  // A/B knob (thin factor runs)
     a.rchunks = f->d_rchunks;

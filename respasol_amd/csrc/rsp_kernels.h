@@ -217,6 +217,22 @@ struct alignas(16) FacRow {
     int i, rs, di, re, q0, q1, hasdiag, pad;
 };
 
+// Fat factor levels, slot layout (ilu0_level_slot): the rows of fat level l
+// are fixed-stride slots (stride ints) at fslots + off, row b of the level at
+// slot b, so a workgroup finds its row's whole structure without first
+// reading a record. Slot: header {i, rs, nlo, nr, nq, hasdiag, global, 0};
+// [8, 8 + rm): divisor position of each lower entry (udiv, -1 = none);
+// [8 + rm, 8 + 2 rm): up | lo << 11 | le << 20 per entry (upd_ptr, lord,
+// lend relative to the row); from kPairsAt(rm): (upd_u, upd_l - rs) per
+// update pair. rm / qm = the level's largest LDS-path row / pair count;
+// global = 1: the row exceeds kFacRow / kFacPairs (global path). stride 0:
+// the level uses the FacRow path.
+struct FacSlotLevel {
+    long long off;
+    int stride, rm, qm, pad;
+};
+__host__ __device__ constexpr int fac_pairs_at(int rm) { return (8 + 2 * rm + 1) & ~1; }
+
 struct IluArgs {
     int n;
     const int *rowptr;
@@ -239,6 +255,9 @@ struct IluArgs {
     const int *lend;
     const int *udiv;      // lower position (i, k): position of u_kk, -1 if row k has no diagonal
     const FacRow *frow;   // per level-order slot of the L DAG (ilu0_level_lds)
+    const int *fslots;    // fat factor levels in the slot layout (ilu0_level_slot), device
+    const FacSlotLevel *fslev;  // per level (host), or null
+    int fat_slots;        // RSP_ILU_FAT_SLOT (default 1): use the slot layout where built
     int fat_lds;          // fat levels: rows staged in LDS (ilu0_level_lds; RSP_ILU_FAT_LDS=0: global path)
     LevelPlan plan;       // L DAG, factor thresholds
     // round-based thin runs (ilu0_rounds), see RndChunk / RndItem
