@@ -287,6 +287,7 @@ __global__ __launch_bounds__(64) void ilu0_level_slot(IluArgs a, const int *__re
         pr[k] = *reinterpret_cast<const int2 *>(slot + pa + 2 * min(lane + 64 * k, qm - 1));
     const int i = slot[0], rs = slot[1], nlo = slot[2], nr = slot[3], nq = slot[4];
     const int hasdiag = slot[5], global = slot[6];
+    if (nr == 0) return;  // (an empty row has no lower entries: it is never in a slot level)
     if (global) {
         factor_row<T, 4>(a, i, lane);
         return;
@@ -1118,6 +1119,46 @@ hipError_t trsv_lower_n_f32(const TrsvArgs &a, hipStream_t s) { return solve_dis
 hipError_t trsv_lower_t_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 1>(a, s); }
 hipError_t trsv_upper_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 2>(a, s); }
 #ifndef RSP_FTZ_BUILD
+// Slot rows of the fat factor levels (analysis, once per pattern). Padding
+// is written too: divisor positions -1 and pairs (0, 0), so every value
+// index the factor kernel loads from a slot is a valid position.
+__global__ __launch_bounds__(64) void ilu0_slot_build(IluArgs a, const int4 *__restrict__ desc,
+                                                      const long long *__restrict__ offs,
+                                                      int *__restrict__ slots) {
+    const int lane = threadIdx.x;
+    const int4 d = desc[blockIdx.x];
+    int *q = slots + offs[blockIdx.x];
+    const int x = d.x, rm = d.y, qm = d.z;
+    const int i = a.plan.rows[x], rs = a.rowptr[i], re = a.rowptr[i + 1];
+    const int nr = re - rs, nlo = a.dpos[i] - rs;
+    const int q0 = a.upd_ptr[rs], nq = a.upd_ptr[re] - q0;
+    const bool global = nr > rsp::kFacRow || nq > rsp::kFacPairs;
+    if (lane < 8) {
+        const int h[8] = {i, rs, nlo, nr, nq, a.hasdiag[i], global ? 1 : 0, 0};
+        q[lane] = h[lane];
+    }
+    for (int y = lane; y < rm; y += 64) {
+        const bool in = !global && y < nr, lower = in && y < nlo;
+        q[8 + y] = lower ? a.udiv[rs + y] : -1;
+        q[8 + rm + y] = in ? ((a.upd_ptr[rs + y] - q0) | ((lower ? a.lord[rs + y] - rs : 0) << 11) |
+                              ((lower ? a.lend[rs + y] - rs : 0) << 20))
+                           : 0;
+    }
+    const int pa = rsp::fac_pairs_at(rm);
+    for (int u = lane; u < qm; u += 64) {
+        const bool in = !global && u < nq;
+        q[pa + 2 * u] = in ? a.upd_u[q0 + u] : 0;
+        q[pa + 2 * u + 1] = in ? a.upd_l[q0 + u] - rs : 0;
+    }
+}
+
+hipError_t ilu0_build_slots(const IluArgs &a, const int4 *desc, const long long *offs, int nrows, int *slots,
+                            hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ilu0_slot_build, dim3(nrows), dim3(64), 0, s, a, desc, offs, slots);
+    return hipGetLastError();
+}
+
 hipError_t ilu0_factor_f64(const IluArgs &a, hipStream_t s) { return factor_dispatch<double>(a, s); }
 hipError_t trsv_lower_n_f64(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<double, 0>(a, s); }
 hipError_t trsv_lower_t_f64(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<double, 1>(a, s); }

@@ -1600,6 +1600,8 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
     const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
     IluSymbolic sym;
+    std::vector<int4> slot_desc;        // fat factor slot rows: {x, rm, qm, 0}
+    std::vector<long long> slot_offs;   // ... and their offsets in f->d_fslots
     phase("group");
     if (!ilu_symbolic(n, rp, ci, dpos, hasdiag, sym)) return RSP_STATUS_ALLOC_FAILED;
     phase("symbolic");
@@ -1685,6 +1687,8 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         const long long cap = (long long)env_int("RSP_ILU_SLOT_CAP_MB", 2048) * (1LL << 20) / 4;
         long long total = 0;
         std::vector<int> slot_levels;
+        slot_desc.clear();
+        slot_offs.clear();
         for (const rsp::LevelSeg &sg : fplan.segs) {
             if (sg.thin) continue;
             for (int l = sg.lb; l < sg.le; l++) {
@@ -1706,43 +1710,15 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
                 slot_levels.push_back(l);
             }
         }
-        if (total > 0) {
-            std::vector<int> slots((size_t)total, 0);
-            std::vector<int> xs, xl;  // level-order slots of the slot-layout levels, their level
-            for (int l : slot_levels)
+        if (total > 0) {  // written on the device from the symbolic arrays (ilu0_build_slots)
+            for (int l : slot_levels) {
+                const rsp::FacSlotLevel &sl = f->fslev[(size_t)l];
                 for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
-                    xs.push_back(x);
-                    xl.push_back(l);
+                    slot_desc.push_back(int4{x, sl.rm, sl.qm, 0});
+                    slot_offs.push_back(sl.off + (long long)(x - lp[(size_t)l]) * sl.stride);
                 }
-            parallel_rows((int)xs.size(), [&](int t0, int t1) {
-                for (int t = t0; t < t1; t++) {
-                    const int x = xs[(size_t)t], l = xl[(size_t)t];
-                    const rsp::FacSlotLevel &sl = f->fslev[(size_t)l];
-                    const int pa = rsp::fac_pairs_at(sl.rm);
-                    int *q = slots.data() + sl.off + (long long)(x - lp[(size_t)l]) * sl.stride;
-                    const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
-                    const int nr = re - rs, nlo = dpos[(size_t)i] - rs;
-                    const int q0 = sym.upd_ptr[(size_t)rs], nq = sym.upd_ptr[(size_t)re] - q0;
-                    const int global = nr > rsp::kFacRow || nq > rsp::kFacPairs;
-                    q[0] = i, q[1] = rs, q[2] = nlo, q[3] = nr, q[4] = nq, q[5] = hasdiag[(size_t)i];
-                    q[6] = global;
-                    for (int y = 0; y < sl.rm; y++) q[8 + y] = -1;
-                    if (global) continue;
-                    for (int y = 0; y < nr; y++) {
-                        const size_t pp = (size_t)rs + y;
-                        const bool lower = y < nlo;
-                        q[8 + y] = lower ? udiv[pp] : -1;
-                        q[8 + sl.rm + y] = (sym.upd_ptr[pp] - q0) |
-                                           ((lower ? sym.lord[pp] - rs : 0) << 11) |
-                                           ((lower ? sym.lend[pp] - rs : 0) << 20);
-                    }
-                    for (int u = 0; u < nq; u++) {
-                        q[pa + 2 * u] = sym.upd_u[(size_t)q0 + u];
-                        q[pa + 2 * u + 1] = sym.upd_l[(size_t)q0 + u] - rs;
-                    }
-                }
-            });
-            if (e == hipSuccess) e = upload(&f->d_fslots, slots);
+            }
+            if (e == hipSuccess) e = hipMalloc((void **)&f->d_fslots, (size_t)total * sizeof(int));
         }
     }
     if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
@@ -1777,6 +1753,30 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     }
     if (e == hipSuccess) e = hipMalloc((void **)&f->d_zero, sizeof(int));
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
+    if (e == hipSuccess && !slot_desc.empty()) {  // fat factor slots, written on the device
+        int4 *d_desc = nullptr;
+        long long *d_offs = nullptr;
+        e = upload_vec(&d_desc, slot_desc);
+        if (e == hipSuccess) e = upload_vec(&d_offs, slot_offs);
+        if (e == hipSuccess) {
+            rsp::IluArgs a{};
+            a.n = n;
+            a.rowptr = d_row_offsets;
+            a.dpos = f->d_dpos;
+            a.hasdiag = f->d_hasdiag;
+            a.upd_ptr = f->d_upd_ptr;
+            a.upd_l = f->d_upd_l;
+            a.upd_u = f->d_upd_u;
+            a.lord = f->d_lord;
+            a.lend = f->d_lend;
+            a.udiv = f->d_udiv;
+            a.plan.rows = f->L.d_rows;
+            e = rsp_k::ilu0_build_slots(a, d_desc, d_offs, (int)slot_desc.size(), f->d_fslots, h->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        }
+        if (d_desc) (void)hipFree(d_desc);
+        if (d_offs) (void)hipFree(d_offs);
+    }
     phase("uploads");
     if (e != hipSuccess) {
         ilu_free_device(f);

@@ -315,4 +315,9 @@ hipError_t ilu0_factor_f64(const rsp::IluArgs &a, hipStream_t s);
 hipError_t trsv_lower_n_f64(const rsp::TrsvArgs &a, hipStream_t s);
 hipError_t trsv_lower_t_f64(const rsp::TrsvArgs &a, hipStream_t s);
 hipError_t trsv_upper_f64(const rsp::TrsvArgs &a, hipStream_t s);
+// Writes the slots of the fat factor levels (rsp::FacSlotLevel layout) from
+// the symbolic arrays already on the device: one workgroup per slot row,
+// desc[t] = {level-order slot x, rm, qm, 0}, offs[t] = its slot's offset.
+hipError_t ilu0_build_slots(const rsp::IluArgs &a, const int4 *desc, const long long *offs, int nrows,
+                            int *slots, hipStream_t s);
 }  // namespace rsp_k
