@@ -624,7 +624,7 @@ __device__ __forceinline__ T block_chain(T s, int k0, int k1, const T *sval, con
 // same index, so the row's first loads are independent.
 template <typename T, int KIND, int B>
 __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows, int nshort, int nb,
-                                                  int nwave, int nwb) {
+                                                  int nwave, int nwb, int sbase) {
     const T *sval = (const T *)a.sval;
     T *y = (T *)a.y;
     const int *src = a.plan.src;
@@ -641,7 +641,29 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
         if (r >= nshort) return;
         x = off + r;
         t = a.plan.tasks[x];
-        s = stream_chain<T, B>(((const T *)a.sx)[x], t.t0, t.t1, sval, src, y);
+        if (sbase >= 0) {
+            // padded short rows: the row's kFatLongTerms flat terms start at
+            // sbase + 8 r, so the values and y indices load with the task
+            // instead of after it; pads (beyond t1) are never used
+            constexpr int F = rsp::kFatLongTerms;
+            const int t0 = sbase + r * F;
+            T v[F], yv[F];
+            int id[F];
+#pragma unroll
+            for (int b = 0; b < F; ++b) {
+                v[b] = sval[t0 + b];
+                id[b] = src[t0 + b];
+            }
+            s = ((const T *)a.sx)[x];
+            const int n = t.t1 - t0;
+#pragma unroll
+            for (int b = 0; b < F; ++b) yv[b] = y[b < n ? id[b] : 0];
+#pragma unroll
+            for (int b = 0; b < F; ++b)
+                if (b < n) s = fma_t(-v[b], yv[b], s);
+        } else {
+            s = stream_chain<T, B>(((const T *)a.sx)[x], t.t0, t.t1, sval, src, y);
+        }
     } else {
         const int r = nshort + (blockIdx.x - nb) * 4 + (threadIdx.x >> 6);
         if (r >= nwave) return;
@@ -1088,8 +1110,9 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             if (cnt <= 0) continue;
             const int ns = P.nshort_host[l], nb = (ns + 255) / 256;
             const int nw = P.nwave_host ? P.nwave_host[l] : cnt, nwb = (nw - ns + 3) / 4;
+            const int sb = P.sbase_host ? P.sbase_host[l] : -1;
             hipLaunchKernelGGL((trsv_level<T, KIND, B>), dim3(nb + nwb + (cnt - nw)), dim3(256), 0,
-                               s, a, off, cnt, ns, nb, nw, nwb);
+                               s, a, off, cnt, ns, nb, nw, nwb, sb);
         }
     }
     return hipGetLastError();

@@ -111,6 +111,7 @@ struct rsp_ilu0_info {
         int *d_nshort = nullptr;               // solve: short rows per level (device)
         std::vector<int> nshort;               // (host)
         std::vector<int> nwave;                // solve: short + wave rows per level (host)
+        std::vector<int> sbase;                // solve: padded short rows' first term per level (host)
         std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
         int batch = 8;                         // solve fma-chain batch
         int group = 4;                         // thin-run term groups (2 or 4)
@@ -1022,6 +1023,7 @@ static int chain_batch(long long total, long long count) {
 // the chunk start — the producer is then in an earlier chunk or before the
 // run, so its store is visible after the chunk's full barrier).
 struct SolvePlan {
+    std::vector<int> sbase;   // per level: first flat term of its padded short rows, -1 = none
     std::vector<int> nshort;  // per level
     std::vector<int> nwave;   // per level: short + wave rows (the rest: hub rows)
     std::vector<rsp::RowTask> tasks;
@@ -1087,7 +1089,14 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     std::vector<int> col;
     sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
     sp.tpos.clear();
-    for (int l = 0; l < nlev; l++)
+    // fat levels: each short row owns kFatLongTerms flat terms (its terms,
+    // then pads), so trsv_level finds a row's terms at sbase + r * 8 without
+    // reading its task first; t1 stays at the row's last real term
+    const bool pad_fat = fat_long == rsp::kFatLongTerms && env_int("RSP_ILU_FAT_PAD", 1) != 0;
+    sp.sbase.assign((size_t)std::max(nlev, 1), -1);
+    for (int l = 0; l < nlev; l++) {
+        const bool padl = pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0;
+        if (padl) sp.sbase[(size_t)l] = (int)sp.tpos.size();
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
             const int i = order[(size_t)x];
             rsp::RowTask &t = sp.tasks[(size_t)x];
@@ -1103,8 +1112,14 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
                     col.push_back(-1);
                 }
             t.t1 = (int)sp.tpos.size();
+            if (padl && x - ptr[(size_t)l] < sp.nshort[(size_t)l])
+                while ((int)sp.tpos.size() - t.t0 < rsp::kFatLongTerms) {
+                    sp.tpos.push_back(-1);
+                    col.push_back(-1);
+                }
             t.d = diag.empty() ? -1 : diag[(size_t)i];
         }
+    }
     std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
     for (int l = 0; l < nlev; l++)
         if (ptr[(size_t)l + 1] > ptr[(size_t)l])
@@ -1735,6 +1750,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         d.segs = sp.segs;
         d.nshort = sp.nshort;
         d.nwave = sp.nwave;
+        d.sbase = sp.sbase;
         e = upload_vec(&d.d_tasks, sp.tasks);
         if (e == hipSuccess) e = upload_vec(&d.d_nshort, sp.nshort);
         if (e == hipSuccess) e = upload_vec(&d.d_tpos, sp.tpos);
@@ -1828,6 +1844,7 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<
     p.batch = batch;
     p.group = d.group;
     p.tasks = d.d_tasks;
+    p.sbase_host = d.sbase.empty() ? nullptr : d.sbase.data();
     p.tpos = d.d_tpos;
     p.src = d.d_src;
     p.chunks = d.d_chunks;

@@ -172,6 +172,8 @@ struct LevelPlan {
     const int *nshort;    // per level: short rows come first (host copy: nshort_host)
     const int *nshort_host;
     const int *nwave_host;  // per level: short + wave rows (fat solve levels; the rest are hub rows)
+    const int *sbase_host;  // per level: fat levels whose short rows sit kFatLongTerms flat terms
+                            // apart (pads after each row's terms) start at this term; -1 = unpadded
 };
 constexpr int kLongTerms = 64;       // thin-run solve rows with more terms are done by a whole wave
 constexpr int kHubTerms = 256;       // fat-level solve rows with more terms: a workgroup each (RSP_ILU_HUB)

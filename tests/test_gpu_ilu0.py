@@ -181,16 +181,19 @@ def test_schedule_variants(handle, monkeypatch, thin_solve, thin_factor, name, s
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
-@pytest.mark.parametrize("slot,lds", [(0, 1), (0, 0), (1, 1)])
+@pytest.mark.parametrize("slot,lds,pad", [(0, 1, 0), (0, 0, 1), (1, 1, 1)])
 @pytest.mark.parametrize("name,scale", [("FEM_3D_thermal2", 0.1), ("Goodwin_095", 0.1), ("crashbasis", 0.1),
                                         ("ASIC_320ks", 0.1)])
-def test_fat_factor_paths(handle, monkeypatch, slot, lds, name, scale):
-    """Fat factor levels with every thin level forced fat, through each row
-    kernel: the slot layout (one round trip for a row's structure), the
-    FacRow + LDS kernel, and the global-memory path — the same bits."""
+def test_fat_level_paths(handle, monkeypatch, slot, lds, pad, name, scale):
+    """Every level forced fat, through each row kernel: factor rows in the
+    slot layout (one round trip for a row's structure), the FacRow + LDS
+    kernel and the global-memory path; solve short rows with padded flat terms
+    (values loaded with the task) or unpadded — the same bits."""
     monkeypatch.setenv("RSP_ILU_FAT_SLOT", str(slot))
     monkeypatch.setenv("RSP_ILU_FAT_LDS", str(lds))
+    monkeypatch.setenv("RSP_ILU_FAT_PAD", str(pad))
     monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
+    monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
     A = csr.surrogate(name, scale)
     x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
     compare(A, torch.float64, handle, x=x)
