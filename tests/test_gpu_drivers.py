@@ -147,3 +147,96 @@ def test_halo_partitioned_spmv_single_gpu(P):
         assert np.array_equal(y2.cpu().numpy()[: r1 - r0], ys[-1])
     assert np.array_equal(np.concatenate(ys), y_full)
     h.close()
+
+
+class _AllRanks:
+    """Stands in for torch.distributed in HaloExchange's setup: answers the two
+    setup all-to-alls of rank r from every rank's HaloSlices (one process)."""
+
+    def __init__(self, all_slices, r):
+        self.all, self.r, self.calls = all_slices, r, 0
+
+    def get_backend(self, group=None):
+        return "nccl"
+
+    def all_to_all_single(self, out, inp, out_splits, in_splits, group=None, async_op=False):
+        P = len(self.all)
+        if self.calls == 0:
+            v = [self.all[p][i].recv_counts[self.r] for p in range(P) for i in range(len(self.all[p]))]
+            out.copy_(torch.tensor(v, dtype=out.dtype))
+        else:
+            cols = [self.all[p][i].recv_cols[self.r] for p in range(P) for i in range(len(self.all[p]))]
+            out.copy_(torch.from_numpy(np.concatenate(cols).astype(np.int64)))
+        self.calls += 1
+
+
+@pytest.mark.parametrize("P", [3, 8])
+def test_halo_direct_layout_single_gpu(P):
+    """Halo received in place (HaloExchange(direct=True): arena = own parts of
+    every slice + one receive region, columns remapped) for several matrices
+    bucketed into one exchange, every rank emulated on one GPU: the receive
+    region is filled as the all-to-all would (source rank, slice, column), the
+    interior tiles run with it poisoned, the boundary tiles after it is
+    restored — one-matrix calls and the batched parts — and every rank's y
+    equals the single-GPU y bit for bit."""
+    from respasol_amd import dist as rdist
+    from respasol_amd.sparse import SpmvBatch
+    names, scale = ["Serena", "G2_circuit", "cage13"], 0.02
+    h = Handle()
+    mats = {n: csr.surrogate(n, scale) for n in names}
+    xs = {n: csr.dlarnv(1, [0, 0, 0, 1], mats[n].n)[0] for n in names}
+    y_full = {n: SpMat(h, *upload_csr(mats[n].rowptr, mats[n].colidx, mats[n].values), mats[n].n).spmv(
+        torch.from_numpy(xs[n]).cuda()).cpu().numpy() for n in names}
+    bounds = {n: csr.partition_rows(mats[n].rowptr, P) for n in names}
+    hosts = {(n, p): csr.surrogate_rows_csr(n, int(bounds[n][p]), int(bounds[n][p + 1]), scale)
+             for n in names for p in range(P)}
+    all_slices = [[rdist.HaloSlice(hosts[(n, p)][1], bounds[n], p) for n in names] for p in range(P)]
+    ys = {n: [] for n in names}
+    for r in range(P):
+        real = rdist.dist
+        rdist.dist = _AllRanks(all_slices, r)
+        try:
+            ex = rdist.HaloExchange(all_slices[r], r, P, torch.float64, "cuda", h, direct=True)
+        finally:
+            rdist.dist = real
+        recv = np.concatenate([xs[n][all_slices[r][i].recv_cols[p]] for p in range(P)
+                               for i, n in enumerate(names)] + [np.zeros(0)])
+        for i, n in enumerate(names):
+            r0, r1 = int(bounds[n][r]), int(bounds[n][r + 1])
+            ex.x_local(i).copy_(torch.from_numpy(xs[n][r0:r1]))
+        region = ex.arena[ex.recv_off:ex.recv_off + ex.n_recv]
+        Ms, outs = [], []
+        for i, n in enumerate(names):
+            rp, ci, va = hosts[(n, r)]
+            M = SpMat(h, *upload_csr(rp, ex.colidx(i), va), ex.n_x(i))
+            M.set_local_cols(all_slices[r][i].m_local)
+            Ms.append(M)
+            outs.append(torch.full((max(all_slices[r][i].m_local, 1),), float("nan"), dtype=torch.float64,
+                                   device="cuda"))
+        b1 = SpmvBatch(h, Ms, [ex.x_ext(i) for i in range(len(names))], outs, 1)
+        b2 = SpmvBatch(h, Ms, [ex.x_ext(i) for i in range(len(names))], outs, 2)
+        for batched in (False, True):
+            for o in outs:
+                o.fill_(float("nan"))
+            region.fill_(float("nan"))  # the exchange has not landed yet
+            if batched:
+                b1.run()
+            else:
+                for i, M in enumerate(Ms):
+                    M.spmv_part(ex.x_ext(i), outs[i], 1)
+            region.copy_(torch.from_numpy(recv))
+            if batched:
+                b2.run()
+            else:
+                for i, M in enumerate(Ms):
+                    M.spmv_part(ex.x_ext(i), outs[i], 2)
+            for i, n in enumerate(names):
+                m_loc = all_slices[r][i].m_local
+                got = outs[i].cpu().numpy()[:m_loc]
+                if batched:
+                    assert np.array_equal(got, ys[n][-1]), (n, r)
+                else:
+                    ys[n].append(got)
+    for n in names:
+        assert np.array_equal(np.concatenate(ys[n]), y_full[n]), n
+    h.close()
