@@ -344,7 +344,7 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void
 
 // Greedy row-block schedule over host row offsets (see spmv.hip header).
 // Rows longer than kSpmvLongRow get tiles of their own (one per `chunk`
-// entries); the others are packed into tiles of <= cap entries / kSpmvMaxRows.
+// entries); the others are packed into tiles of <= cap entries / maxrows rows.
 static int build_spmv_plan(const int *rp, int m, int cap, int chunk, std::vector<SpmvBlock> &blocks,
                            std::vector<SpmvLongRow> &longrows, int *nslots,
                            int maxrows = rsp::kSpmvMaxRows, int row_align = 1) {
@@ -433,7 +433,8 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
     const int chunk = chunk_cap(type);
     const int cap = tile_cap(type);
     const int align = row_align;
-    build_spmv_plan(rp, m, cap, chunk, p.blocks, p.longrows, &p.nslots, rsp::kSpmvMaxRows, align);
+    const int maxrows = type == RSP_R_64F ? SpmvTile<double>::kMaxRows : SpmvTile<float>::kMaxRows;
+    build_spmv_plan(rp, m, cap, chunk, p.blocks, p.longrows, &p.nslots, maxrows, align);
     const int64_t nb = (int64_t)p.blocks.size();
     if (spread > 0 && nb > 0 && nb < spread) {
         const SpmvBounds bb = spmv_bounds(m, std::max<int64_t>(nnz_bound, 0), chunk);
@@ -443,7 +444,7 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
             std::vector<SpmvBlock> b2;
             std::vector<SpmvLongRow> l2;
             int s2 = 0;
-            build_spmv_plan(rp, m, c, chunk, b2, l2, &s2, rsp::kSpmvMaxRows, align);
+            build_spmv_plan(rp, m, c, chunk, b2, l2, &s2, maxrows, align);
             if ((int64_t)b2.size() <= spread && b2.size() <= bb.nblocks) {
                 p.blocks.swap(b2);
                 p.longrows.swap(l2);

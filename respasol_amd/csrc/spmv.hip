@@ -4,7 +4,7 @@
 //
 // Schedule ("row-block" tiles, built on the host by rsp_spmv_preprocess):
 // consecutive rows are packed into tiles of at most SpmvTile<T>::kMaxNnz
-// entries (<= kSpmvMaxRows rows); one 256-thread workgroup per tile.
+// entries (<= SpmvTile<T>::kMaxRows rows); one 256-thread workgroup per tile.
 //   1. stream: each thread issues all of its 16-byte colidx/vals loads for
 //      the tile back to back (predicated, no per-element branches, so every
 //      load is in flight before the first wait), then all its x[col] gathers,
@@ -217,7 +217,7 @@ __device__ __forceinline__ void stream_products_scalar(const int *__restrict__ c
 // Rows [0, nrows) of a tile, L lanes per row, canonical 8-way order; the
 // row sum goes to sink(row, sum) (lane 0 of the row's group).
 template <typename T, int L, int NTH, typename Sink>
-__device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int nrows, int kb,
+__device__ __forceinline__ void reduce_rows(const T *lds, const unsigned short *rp_lds, int nrows, int kb,
                                             Sink sink) {
     constexpr int NA = 8 / L;                  // partials held per lane
     constexpr int NG = NTH / L;                // row groups per pass
@@ -254,7 +254,7 @@ __device__ __forceinline__ void reduce_rows(const T *lds, const int *rp_lds, int
 // lanes per row: power of two <= 8 such that each lane still sums >= 4
 // products of an average row and the groups fit the workgroup
 template <typename T, int NTH = kSpmvThreads, typename Sink>
-__device__ __forceinline__ void reduce_tile_rows(const T *lds, const int *rp_lds, int nrows,
+__device__ __forceinline__ void reduce_tile_rows(const T *lds, const unsigned short *rp_lds, int nrows,
                                                  int nnzt, int kb, Sink sink) {
     int L = 1;
     while (L < 8 && 2 * L * nrows <= NTH && 8 * L * nrows <= nnzt) L <<= 1;
@@ -338,9 +338,9 @@ __device__ __forceinline__ void spmv_tile(
     const unsigned short *__restrict__ cidx, int cbase, int cmax,
     const T *__restrict__ vals, const T *__restrict__ x, T *__restrict__ y,
     T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, T *lds,
-    T *wsum, int *rp_lds, int fuse) {
+    T *wsum, unsigned short *rp_lds, int fuse) {
     constexpr int VW = 16 / sizeof(T);
-    constexpr int RPQ = (rsp::kSpmvMaxRows + kSpmvThreads) / kSpmvThreads;
+    constexpr int RPQ = (SpmvTile<T>::kMaxRows + kSpmvThreads) / kSpmvThreads;
     const int tid = threadIdx.x;
     const int k0 = blk.k0, k1 = blk.k1;
     // the tile's row offsets, loaded ahead of the stream and parked in LDS
@@ -394,7 +394,7 @@ __device__ __forceinline__ void spmv_tile(
 #pragma unroll
     for (int q = 0; q < RPQ; ++q) {
         const int i = tid + q * kSpmvThreads;
-        if (i <= nrows) rp_lds[i] = rpv[q];
+        if (i <= nrows) rp_lds[i] = (unsigned short)(rpv[q] - kb);  // < kSlots + kVec
     }
     lds_barrier();
 
@@ -419,7 +419,7 @@ __device__ __forceinline__ void spmv_tile(
         if (tid < nrows) y[r0 + tid] = lds[tid];
         return;
     }
-    reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, kb, [&](int rr, T sum) {
+    reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, 0, [&](int rr, T sum) {
         T out = alpha * sum;
         if (RSP_PROBE_NOY && out != T(-12345.0)) return;
         if (BETA) out += beta * y[r0 + rr];
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
-    __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
+    __shared__ unsigned short rp_lds[SpmvTile<T>::kMaxRows + 2];  // row offsets - kb
 #if RSP_PROBE_WALK
     // diagnostic: tiles [W t, W t + W) of the swizzled workgroup t in turn,
     // an LDS-only barrier between them (the previous tile's y stores stay in
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     const int *__restrict__ cbases, SpmvBatchTable at, T alpha, T beta, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
-    __shared__ int rp_lds[rsp::kSpmvMaxRows + 1];
+    __shared__ unsigned short rp_lds[SpmvTile<T>::kMaxRows + 2];  // row offsets - kb
     const int b = blockIdx.x;
     // lo / hi selected inside the compare chain on the kernel arguments
     // (preloaded into SGPRs, so no memory latency in front of the tile
