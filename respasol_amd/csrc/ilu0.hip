@@ -103,6 +103,53 @@ __device__ __forceinline__ T wave_chain(T s, int k0, int k1, int lane, FV vat, F
     return s;
 }
 
+// The same chain for one fat-level row by a wave, on LDS broadcast operands:
+// each group of 64 terms is gathered by the lanes (values, then y; the next
+// group's loads are issued before this group's chain), parked in the wave's
+// LDS rows, and every lane runs the in-order fma chain reading them (reads
+// independent of the sum, so they issue ahead of it) — instead of four
+// readlanes per term. One fma per term in order: the same bits.
+template <typename T>
+__device__ __forceinline__ T wave_chain_lds(T s, int k0, int k1, int lane, T *wv, T *wy, const T *sval,
+                                           const int *src, const T *y) {
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    };
+    int k = min(k0 + lane, k1 - 1);
+    T v = sval[k];
+    int id = src[k];
+    T yv = y[id];
+    for (int base = k0; base < k1; base += 64) {
+        wv[lane] = v;
+        wy[lane] = yv;
+        wave_sync();
+        const int cnt = min(64, k1 - base);
+        const bool more = base + 64 < k1;
+        if (more) {  // the next group's values and y indices in flight under this chain
+            k = min(base + 64 + lane, k1 - 1);
+            v = sval[k];
+            id = src[k];
+        }
+        int j = 0;
+        for (; j + 4 <= cnt; j += 4) {
+            T p[4], q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                p[u] = wv[j + u];
+                q[u] = wy[j + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s = fma_t(-p[u], q[u], s);
+        }
+        for (; j < cnt; ++j) s = fma_t(-wv[j], wy[j], s);
+        wave_sync();  // this group's reads before the next group's stores
+        if (more) yv = y[id];
+    }
+    return s;
+}
+
 // One position of the factor, pull form: v = a_p - sum_k l_ik u_kj over the
 // position's update list (k ascending, one fma each — the same sequence of
 // roundings as the IKJ loop).
@@ -669,8 +716,15 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
         if (r >= nwave) return;
         x = off + r;
         t = a.plan.tasks[x];
-        s = wave_chain<T>(((const T *)a.sx)[x], t.t0, t.t1, threadIdx.x & 63,
-                          [&](int k) { return sval[k]; }, [&](int k) { return y[src[k]]; });
+        if (a.wave_lds) {
+            __shared__ T cwv[4][64], cwy[4][64];
+            const int w = threadIdx.x >> 6;
+            s = wave_chain_lds<T>(((const T *)a.sx)[x], t.t0, t.t1, threadIdx.x & 63, cwv[w], cwy[w], sval,
+                                  src, y);
+        } else {
+            s = wave_chain<T>(((const T *)a.sx)[x], t.t0, t.t1, threadIdx.x & 63,
+                              [&](int k) { return sval[k]; }, [&](int k) { return y[src[k]]; });
+        }
         if ((threadIdx.x & 63) != 0) return;
     }
     if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];

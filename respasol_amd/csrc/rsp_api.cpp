@@ -1946,6 +1946,7 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.trace = nullptr;
     a.trace_cap = 0;
     a.trace_clk = 0;
+    a.wave_lds = env_int("RSP_ILU_WAVE_LDS", 1);
     return a;
 }
 

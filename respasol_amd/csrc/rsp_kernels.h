@@ -291,6 +291,7 @@ struct TrsvArgs {
     unsigned long long *trace;  // diagnostics (RSP_ILU_TRACE): 8 timestamps per chunk, or null
     int trace_cap;
     int trace_clk;              // level stamps in shader clock cycles (s_memtime) instead
+    int wave_lds;               // fat-level wave rows: chain on LDS broadcast operands (RSP_ILU_WAVE_LDS)
 };
 
 }  // namespace rsp

@@ -181,14 +181,16 @@ def test_schedule_variants(handle, monkeypatch, thin_solve, thin_factor, name, s
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
-@pytest.mark.parametrize("slot,lds,pad", [(0, 1, 0), (0, 0, 1), (1, 1, 1)])
+@pytest.mark.parametrize("slot,lds,pad,wlds", [(0, 1, 0, 0), (0, 0, 1, 1), (1, 1, 1, 1), (1, 1, 1, 0)])
 @pytest.mark.parametrize("name,scale", [("FEM_3D_thermal2", 0.1), ("Goodwin_095", 0.1), ("crashbasis", 0.1),
                                         ("ASIC_320ks", 0.1)])
-def test_fat_level_paths(handle, monkeypatch, slot, lds, pad, name, scale):
+def test_fat_level_paths(handle, monkeypatch, slot, lds, pad, wlds, name, scale):
     """Every level forced fat, through each row kernel: factor rows in the
     slot layout (one round trip for a row's structure), the FacRow + LDS
     kernel and the global-memory path; solve short rows with padded flat terms
-    (values loaded with the task) or unpadded — the same bits."""
+    (values loaded with the task) or unpadded; wave rows chained on LDS
+    broadcast operands or on readlanes — the same bits."""
+    monkeypatch.setenv("RSP_ILU_WAVE_LDS", str(wlds))
     monkeypatch.setenv("RSP_ILU_FAT_SLOT", str(slot))
     monkeypatch.setenv("RSP_ILU_FAT_LDS", str(lds))
     monkeypatch.setenv("RSP_ILU_FAT_PAD", str(pad))
