@@ -1045,8 +1045,36 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             }
             for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
                 const ThinRow<T> t = lrow[off + r];
+#if RSP_THIN_LONG_READLANE
                 const int k0 = G * (t.g & 0xffff);
                 T s = wave_chain<T>(t.x, k0, k0 + G * (t.g >> 16), tid & 63, vat, yat);
+#else
+                // every lane runs the row's chain on broadcast LDS operands,
+                // group g+1's values, indices and y read under group g's fmas
+                // (the same terms in the same order as wave_chain: same bits)
+                const int g0 = t.g & 0xffff, ng = t.g >> 16;
+                T s = t.x;
+                TermGroup<T, G> vc = lval[g0];
+                T yc[G];
+                {
+                    const TermIds<G> ic = lidx[g0];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) yc[j] = yb(ic.v[j]);
+                }
+                for (int g = 0; g < ng; ++g) {
+                    const int gn = g0 + min(g + 1, ng - 1);
+                    const TermGroup<T, G> vn = lval[gn];
+                    const TermIds<G> in = lidx[gn];
+                    T yn[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) yn[j] = yb(in.v[j]);
+#pragma unroll
+                    for (int j = 0; j < G; ++j) s = fma_t(-vc.v[j], yc[j], s);
+                    vc = vn;
+#pragma unroll
+                    for (int j = 0; j < G; ++j) yc[j] = yn[j];
+                }
+#endif
                 if constexpr (KIND == 2) s = s / ldg[off + r];
                 if ((tid & 63) == 0) put(t.out, s);
             }
