@@ -933,6 +933,34 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         for (int j = 0; j < G; ++j) s = fma_t(-g.v[j], yv[j], s);
         return s;
     };
+    // groups [g, ge) of a row after s, in order; group g+1's values, indices
+    // and y are read under group g's fmas (the same fmas in the same order)
+    auto groups_fma = [&](T s, int g, int ge) {
+        TermGroup<T, G> vc = lval[g];
+        T yc[G];
+        {
+            const TermIds<G> ic = lidx[g];
+#pragma unroll
+            for (int j = 0; j < G; ++j) yc[j] = yb(ic.v[j]);
+        }
+        for (; g < ge; ++g) {
+            const int gn = min(g + 1, ge - 1);
+            const TermGroup<T, G> vn = lval[gn];
+            const TermIds<G> in = lidx[gn];
+            T yn[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) yn[j] = yb(in.v[j]);
+#pragma unroll
+            for (int j = 0; j < G; ++j) s = fma_t(-vc.v[j], yc[j], s);
+            vc = vn;
+#pragma unroll
+            for (int j = 0; j < G; ++j) yc[j] = yn[j];
+        }
+        return s;
+    };
+    // (groups_fma for every short row, and for the narrow rows' third group
+    // on, measured 1.6 % slower on config 3: short chains gain nothing from
+    // the lookahead and pay its loads; long rows gain 10 %)
     auto row_value = [&](const ThinRow<T> &r) {  // one short row, groups in order
         T s = r.x;
         const int g0 = r.g & 0xffff, ng = r.g >> 16;
@@ -1053,27 +1081,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 // group g+1's values, indices and y read under group g's fmas
                 // (the same terms in the same order as wave_chain: same bits)
                 const int g0 = t.g & 0xffff, ng = t.g >> 16;
-                T s = t.x;
-                TermGroup<T, G> vc = lval[g0];
-                T yc[G];
-                {
-                    const TermIds<G> ic = lidx[g0];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) yc[j] = yb(ic.v[j]);
-                }
-                for (int g = 0; g < ng; ++g) {
-                    const int gn = g0 + min(g + 1, ng - 1);
-                    const TermGroup<T, G> vn = lval[gn];
-                    const TermIds<G> in = lidx[gn];
-                    T yn[G];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) yn[j] = yb(in.v[j]);
-#pragma unroll
-                    for (int j = 0; j < G; ++j) s = fma_t(-vc.v[j], yc[j], s);
-                    vc = vn;
-#pragma unroll
-                    for (int j = 0; j < G; ++j) yc[j] = yn[j];
-                }
+                T s = ng > 0 ? groups_fma(t.x, g0, g0 + ng) : t.x;
 #endif
                 if constexpr (KIND == 2) s = s / ldg[off + r];
                 if ((tid & 63) == 0) put(t.out, s);
