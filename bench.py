@@ -178,6 +178,143 @@ def pmc_traffic(workload, batched):
     return best
 
 
+class Workload:
+    """One bench step over a set of matrices on this rank: the slices, the
+    RCCL halo exchange (N > 1), the batched launches and the step itself."""
+
+    def __init__(self, names, rank, world, handle, device, args):
+        self.world, self.device = world, device
+        self.overlap = overlap = world > 1 and args.exchange == "halo" and not args.no_overlap
+        self.slices = slices = [Slice(n, rank, world, handle, device, args.exchange, overlap) for n in names]
+        self.exchanges64, self.exchanges32 = [], []
+        if world > 1 and args.exchange == "halo":
+            groups = [[i] for i in range(len(slices))] if args.no_bucket else [list(range(len(slices)))]
+            for g in groups:
+                direct = not args.halo_unpack
+                ex64 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float64, device, handle,
+                                    direct=direct)
+                ex32 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float32, device, handle,
+                                    direct=direct)
+                for j, i in enumerate(g):
+                    slices[i].bind_halo(j, ex64, ex32)
+                ex64.exchange()
+                ex32.exchange()
+                self.exchanges64.append((g, ex64))
+                self.exchanges32.append((g, ex32))
+        torch.cuda.synchronize()
+        self.stream = torch.cuda.current_stream()
+        # part -> one batched launch over every matrix (rsp_spmv_batch): a
+        # step's SpMVs cost one kernel ramp and drain instead of one per
+        # matrix (--no-batch: one rsp_spmv per matrix)
+        self.batches = {}
+        if not args.no_batch:
+            for part in ((0, 1, 2) if overlap else (0,)):
+                self.batches[part] = SpmvBatch(handle, [s.mat64 for s in slices], [s.x64() for s in slices],
+                                               [s.y64 for s in slices], part)
+
+    def spmv_all(self, part):
+        for s in self.slices:
+            if part:
+                s.mat64.spmv_part(s.x64(), s.y64, part)
+            else:
+                s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
+
+    def run(self, part):
+        b = self.batches.get(part)
+        if b is not None:
+            b.run()
+        else:
+            self.spmv_all(part)
+
+    def step(self, exchange=True, events=None):
+        stream = self.stream
+        if events is not None:  # instrumented pass: kernels only, one event pair per matrix
+            # one whole step first keeps the stream busy while the host queues
+            # the pairs, so the first pair does not time the host submission
+            # gap after the previous synchronise
+            self.run(0)
+            for i, s in enumerate(self.slices):
+                events[i][0].record(stream)
+                s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
+                events[i][1].record(stream)
+            return
+        if exchange and self.overlap:
+            # halo overlap: start every exchange, interior tiles of every matrix
+            # (own columns only), join the exchanges, then the boundary tiles
+            for _, ex in self.exchanges64:
+                ex.start()
+            self.run(1)
+            for _, ex in self.exchanges64:
+                ex.finish()
+            self.run(2)
+            return
+        if exchange and self.world > 1:  # every matrix's x is independent: exchange all, then compute
+            for s in self.slices:
+                if s.mode == "allgather":
+                    s.part64.exchange()
+            for _, ex in self.exchanges64:
+                ex.exchange()
+        self.run(0)
+
+    def ramp(self, ramp_ms, device):
+        """The GPU's clocks ramp up over the first tens of ms of load: 5
+        warm-up steps (3 ms) leave 20 timed ones 5-8 % below steady state
+        (measured 882-902 vs 933-957 GFLOP/s on one box). So setup runs the
+        step until ramp_ms of GPU time have passed (untimed, reported in the
+        JSON); returns the step count (equal on every rank)."""
+        steps = 0
+        if ramp_ms > 0:
+            t_r = time.perf_counter()
+            while True:
+                for _ in range(5):
+                    self.step()
+                steps += 5
+                torch.cuda.synchronize()
+                more = torch.tensor([1.0 if (time.perf_counter() - t_r) * 1e3 < ramp_ms else 0.0],
+                                    device=device)
+                if self.world > 1:  # every rank runs the same number of steps (collectives inside)
+                    dist.all_reduce(more, op=dist.ReduceOp.MAX)
+                if more.item() == 0.0:
+                    break
+        return steps
+
+    def timed(self, steps, warmup):
+        """W warm-up steps, then exactly K steps between barrier + synchronize,
+        one HIP event pair on the kernels' stream around the loop (an event
+        pair per launch would insert ~10 us of marker gap between kernels).
+        Returns (max-over-ranks wall seconds, start event, end event)."""
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize()
+        e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e_start.record(self.stream)
+        for _ in range(steps):
+            self.step()
+        e_end.record(self.stream)
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if self.world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, e_start, e_end
+
+    def totals(self):
+        """(FLOPs, algorithmic fp64 bytes) of one step summed over ranks."""
+        tot = torch.tensor([float(sum(2.0 * s.nnz_local for s in self.slices)),
+                            float(sum(s.bytes_local(8) for s in self.slices))],
+                           dtype=torch.float64, device=self.device)
+        if self.world > 1:
+            dist.all_reduce(tot)
+        return float(tot[0]), float(tot[1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,6 +341,8 @@ def main():
     ap.add_argument("--nccl-normal-priority", action="store_true",
                     help="RCCL on a normal-priority stream (default: high priority, so the "
                          "overlapped exchange is not queued behind the interior tiles)")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip the Serena-only step (BASELINE config 5) reported beside the big set")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
@@ -228,122 +367,16 @@ def main():
     names = workload_names(args.workload)
 
     t_setup = time.perf_counter()
-    overlap = world > 1 and args.exchange == "halo" and not args.no_overlap
-    slices = [Slice(n, rank, world, handle, device, args.exchange, overlap) for n in names]
-    exchanges64, exchanges32 = [], []
-    if world > 1 and args.exchange == "halo":
-        groups = [[i] for i in range(len(slices))] if args.no_bucket else [list(range(len(slices)))]
-        for g in groups:
-            direct = not args.halo_unpack
-            ex64 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float64, device, handle,
-                                direct=direct)
-            ex32 = HaloExchange([slices[i].halo for i in g], rank, world, torch.float32, device, handle,
-                                direct=direct)
-            for j, i in enumerate(g):
-                slices[i].bind_halo(j, ex64, ex32)
-            ex64.exchange()
-            ex32.exchange()
-            exchanges64.append((g, ex64))
-            exchanges32.append((g, ex32))
-    torch.cuda.synchronize()
+    W = Workload(names, rank, world, handle, device, args)
+    slices, batches, overlap, exchanges64 = W.slices, W.batches, W.overlap, W.exchanges64
+    step, spmv_all, stream = W.step, W.spmv_all, W.stream
     log(f"setup {time.perf_counter() - t_setup:.1f}s: {len(slices)} matrices, "
         f"{sum(s.nnz_global for s in slices) / 1e6:.1f} M stored nnz, world={world}")
 
-    stream = torch.cuda.current_stream()
-
-    def spmv_all(part):
-        for s in slices:
-            if part:
-                s.mat64.spmv_part(s.x64(), s.y64, part)
-            else:
-                s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
-
-    # part -> one batched launch over every matrix (rsp_spmv_batch): a step's
-    # 15 SpMVs cost one kernel ramp and drain instead of 15 (--no-batch: one
-    # rsp_spmv per matrix)
-    batches = {}
-    if not args.no_batch:
-        for part in ((0, 1, 2) if overlap else (0,)):
-            batches[part] = SpmvBatch(handle, [s.mat64 for s in slices], [s.x64() for s in slices],
-                                      [s.y64 for s in slices], part)
-
-    def run(part):
-        b = batches.get(part)
-        if b is not None:
-            b.run()
-        else:
-            spmv_all(part)
-
-    def step(exchange=True, events=None):
-        if events is not None:  # instrumented pass: kernels only, one event pair per matrix
-            for i, s in enumerate(slices):
-                events[i][0].record(stream)
-                s.mat64.spmv(s.x64(), s.y64[: s.m_local] if s.m_local else s.y64)
-                events[i][1].record(stream)
-            return
-        if exchange and overlap:
-            # halo overlap: start every exchange, interior tiles of every matrix
-            # (own columns only), join the exchanges, then the boundary tiles
-            for _, ex in exchanges64:
-                ex.start()
-            run(1)
-            for _, ex in exchanges64:
-                ex.finish()
-            run(2)
-            return
-        if exchange and world > 1:  # every matrix's x is independent: exchange all, then compute
-            for s in slices:
-                if s.mode == "allgather":
-                    s.part64.exchange()
-            for _, ex in exchanges64:
-                ex.exchange()
-        run(0)
-
-    # The GPU's clocks ramp up over the first tens of ms of load: 5 warm-up
-    # steps (3 ms) leave the 20 timed ones 5-8 % below steady state (measured
-    # 882-902 vs 933-957 GFLOP/s on one box). Setup therefore runs the step
-    # until --ramp-ms of GPU time have passed (untimed, reported in the JSON),
-    # then the W warm-up steps, then exactly K timed steps.
-    ramp_steps = 0
-    if args.ramp_ms > 0:
-        t_r = time.perf_counter()
-        while True:
-            for _ in range(5):
-                step()
-            ramp_steps += 5
-            torch.cuda.synchronize()
-            more = torch.tensor([1.0 if (time.perf_counter() - t_r) * 1e3 < args.ramp_ms else 0.0],
-                                device=device)
-            if world > 1:  # every rank runs the same number of steps (collectives inside)
-                dist.all_reduce(more, op=dist.ReduceOp.MAX)
-            if more.item() == 0.0:
-                break
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # timed region: exactly K steps, barrier + synchronize on both sides, one
-    # HIP event pair on the kernels' stream around the whole loop (an event
-    # pair per launch would insert ~10 us of marker gap between kernels)
-    e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e_start.record(stream)
-    for _ in range(args.steps):
-        step()
-    e_end.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    ramp_steps = W.ramp(args.ramp_ms, device)
+    elapsed, e_start, e_end = W.timed(args.steps, args.warmup)
     big = max(slices, key=lambda s: s.nnz_global)
     y_step_t = big.y64.clone()  # checked against a whole SpMV below
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     # dominant kernel, this rank: algorithmic bytes / average launch duration.
     # N = 1: the timed region is nothing but back-to-back launches of it; N > 1:
@@ -441,6 +474,24 @@ def main():
     ok_step = np.array_equal(y_step, got) if big.m_local else True
     check_ok = bool(np.all(np.abs(got - ref) <= bound)) and ok_x and ok_step
 
+    # config 5 (BASELINE.json): row-partitioned fp64 SpMV on the largest
+    # matrix alone (Serena), measured like the headline step at the same N —
+    # the hard case for scaling (about 11 us of compute per GPU at N = 8)
+    config5 = None
+    if args.workload == "big" and not args.no_config5:
+        W5 = Workload(["Serena"], rank, world, handle, device, args)
+        W5.ramp(20.0, device)
+        el5, _, _ = W5.timed(args.steps, args.warmup)
+        f5, b5 = W5.totals()
+        config5 = {"workload": "Serena only, CSR SpMV fp64"
+                               + (f", row-partitioned x{world} + RCCL {args.exchange} exchange of x"
+                                  if world > 1 else ", 1 GPU"),
+                   "value": round(f5 * args.steps / el5 / 1e9, 2), "unit": "GFLOP/s",
+                   "ms_per_step": round(el5 / args.steps * 1e3, 4),
+                   "hbm_gbps": round(b5 * args.steps / el5 / 1e9, 1),
+                   "nnz_stored": int(W5.slices[0].nnz_global), "steps": args.steps}
+        del W5
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(slices, args.cpu_seconds)
@@ -504,6 +555,7 @@ def main():
                 "moved_frac": round(moved_achieved / HBM_PEAK_GBS, 4),
             },
             "cpu_baseline": cpu,
+            "config5_serena": config5,
             "fp32": fp32,
             "per_matrix_calls": per_matrix_calls,
             "per_matrix_us_rank0": per_matrix,

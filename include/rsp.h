@@ -104,26 +104,34 @@ rsp_status_t rsp_destroy_spmat(rsp_spmat_t mat); /* cusparseDestroySpMat (GPU/sp
 
 /* ------------------------------------------------------------------ SpMV */
 
-/* cusparseSpMV_bufferSize (GPU/spmv.cu:143-145,159-161). Upper bound on the
- * workspace rsp_spmv needs; computed from rows/nnz only (no device access). */
+/* cusparseSpMV_bufferSize (GPU/spmv.cu:143-145,159-161). Host-blocking: builds
+ * the row-block schedule of `mat` for `compute_type` (reads the row offsets and
+ * column indices once, validates them — INVALID_VALUE for a malformed
+ * pattern — and keeps a 16-bit copy of the column indices, relative to each
+ * tile's first column, for tiles spanning < 65536 columns) in device memory
+ * owned by `mat` (freed by rsp_destroy_spmat), so that the reference's call
+ * sequence create_csr -> bufferSize -> malloc -> SpMV x50 (GPU/spmv.cu:143-195)
+ * plans nothing inside a timed call. *buffer_size is 0: rsp_spmv needs no
+ * caller workspace (any pointer, NULL included, is accepted), and several
+ * matrices may share one. The schedule is reused while it is valid; as with
+ * cuSPARSE, the sparsity pattern must not change afterwards without a new
+ * rsp_spmv_preprocess (values may: they are read on every call). */
 rsp_status_t rsp_spmv_buffer_size(rsp_handle_t handle, rsp_operation_t op, const void *alpha,
                                   rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
                                   size_t *buffer_size);
-/* cusparseSpMV_preprocess analogue: builds the row-block schedule of `mat`
- * into `d_buffer` (host-blocking: reads the row offsets and column indices
- * once, validates the indices, and stores a 16-bit copy of them, relative to
- * each tile's first column, for tiles spanning < 65536 columns — the
- * workspace holds 2 B per entry for it). rsp_spmv on a buffer that was not
- * preprocessed for `mat` preprocesses it first. As with cuSPARSE's
- * preprocess, the sparsity pattern must not change afterwards without a new
- * preprocess (values may: they are read from the matrix on every call). */
+/* cusparseSpMV_preprocess analogue (cuSPARSE 12; the reference has no such
+ * call): rebuilds the schedule of `mat` (host-blocking, as bufferSize). Only
+ * needed after the pattern changed; rsp_spmv plans lazily if neither call was
+ * made. `d_buffer` is unused. */
 rsp_status_t rsp_spmv_preprocess(rsp_handle_t handle, rsp_operation_t op, const void *alpha,
                                  rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
                                  rsp_datatype_t compute_type, void *d_buffer);
 /* cusparseSpMV (GPU/spmv.cu:179-186): y = alpha * A * x + beta * y.
  * op must be NON_TRANSPOSE (the only form the reference uses). If *beta == 0,
  * y is write-only. compute_type must equal the matrix value type. Deterministic:
- * the same inputs give bitwise identical y on every call. */
+ * the same inputs give bitwise identical y on every call. `d_buffer` is
+ * accepted for signature parity and unused. Calls on one matrix must be
+ * stream-ordered (its long-row tickets live in its schedule). */
 rsp_status_t rsp_spmv(rsp_handle_t handle, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
                       const void *d_x, const void *beta, void *d_y, rsp_datatype_t compute_type,
                       void *d_buffer);
@@ -194,16 +202,17 @@ rsp_status_t rsp_gather(rsp_handle_t handle, rsp_datatype_t value_type, int64_t 
 rsp_status_t rsp_scatter(rsp_handle_t handle, rsp_datatype_t value_type, int64_t n,
                          const int64_t *d_idx, const void *d_src, void *d_dst);
 
-/* Schedule facts of the last rsp_spmv_preprocess of `mat` (no cuSPARSE
+/* Schedule facts of the current schedule of `mat` (no cuSPARSE
  * counterpart; for byte accounting): its tile count, and how many stored
  * entries it reads through 16-bit column offsets (2 B each instead of the
  * 4-B colidx: tiles whose columns span < 65536; the rest read colidx).
- * NOT_INITIALIZED before the first preprocess. */
+ * NOT_INITIALIZED before the first bufferSize / preprocess / SpMV. */
 rsp_status_t rsp_spmv_plan_info(rsp_spmat_t mat, int64_t *tiles, int64_t *entries_16bit);
 
 /* Overlap of the halo exchange with the SpMV. Columns [0, ncols_local) of
  * `mat` are the rank's own x entries, the others arrive with the exchange.
- * Set before rsp_spmv_preprocess (a later call re-plans): the schedule then
+ * Invalidates the schedule (the next bufferSize / preprocess / SpMV re-plans
+ * it, and batches holding the old one become stale): the schedule then
  * puts the tiles that read own columns only first. rsp_spmv_part runs
  * part 1 = those interior tiles (launch it while the exchange is in flight),
  * part 2 = the remaining tiles, long rows included; part 0 = everything
@@ -221,14 +230,14 @@ rsp_status_t rsp_spmv_part(rsp_handle_t handle, const void *alpha, rsp_spmat_t m
  * (GPU/spmv.cu:179-186); this is the same product per matrix, bit for bit
  * equal to rsp_spmv / rsp_spmv_part on each, without the per-launch ramp and
  * drain. `part` selects the schedule part of every matrix as rsp_spmv_part
- * (0 = whole product). Create records the pointers (x_j, y_j, d_buffers[j]
- * stay valid until destroy) and plans the batch's own tiling of every matrix
- * (full tiles once the launch fills the chip; a matrix not yet preprocessed
- * into d_buffers[j] is preprocessed first, its long-row partials stay
- * there); run fails with
- * INVALID_VALUE if a matrix has been re-planned or given other values
- * (rsp_csr_set_values) since. Create and destroy
- * are host-blocking. */
+ * (0 = whole product). Create records the pointers (x_j, y_j stay valid
+ * until destroy) and plans the batch's own tiling of every matrix (full tiles
+ * once the launch fills the chip; a matrix without a schedule is planned
+ * first, its long-row partials stay in its schedule, so a matrix may appear
+ * once per batch: INVALID_VALUE otherwise). d_buffers is unused (may be
+ * NULL). Run fails with INVALID_VALUE if a matrix has been re-planned or
+ * given other values (rsp_csr_set_values) since. Create and destroy are
+ * host-blocking. */
 rsp_status_t rsp_spmv_batch_create(rsp_handle_t handle, int count, const rsp_spmat_t *mats,
                                    const void *const *d_x, void *const *d_y,
                                    void *const *d_buffers, rsp_datatype_t compute_type,

@@ -132,6 +132,14 @@ int rsp_surrogate_csr(const char *name, double scale, int flags, CSR *matrix);
  * nnz-balanced contiguous row ranges: bounds[p] =
  * lower_bound(rowptr, rowptr[0] + p*nnz/P), bounds[0] = 0, bounds[P] = m. */
 int rsp_partition_rows(const int *rowptr, int m, int parts, int *bounds);
+/* Padded all-gather layout of a row-partitioned x: slice p's entries sit at
+ * x_pad[p*chunk ..) with chunk = max_p (bounds[p+1] - bounds[p]) (returned;
+ * -1 on bad arguments), so one equal-count ncclAllGather reassembles x. */
+int rsp_padded_chunk(const int *bounds, int parts);
+/* colidx_out[k] = p*chunk + (c - bounds[p]) for c = colidx_in[k] in slice p
+ * (in place allowed). -1 if a column lies outside [0, bounds[parts]). */
+int rsp_remap_cols_padded(int64_t nnz, const int *colidx_in, const int *bounds, int parts, int chunk,
+                          int *colidx_out);
 
 /* Host CSR SpMV used by the drivers' verification step (the role MKL's
  * sequential mkl_sparse_?_mv plays in GPU/spmv.cu:221-260). Row-parallel. */

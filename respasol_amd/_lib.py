@@ -134,6 +134,8 @@ HOST_PROTOS = {
     "rsp_surrogate_fill": (i32, [C.c_char_p, C.c_double, i32, i32, i32, ip, ip, C.POINTER(C.c_double)]),
     "rsp_surrogate_csr": (i32, [C.c_char_p, C.c_double, i32, C.POINTER(CSRStruct)]),
     "rsp_partition_rows": (i32, [ip, i32, i32, ip]),
+    "rsp_padded_chunk": (i32, [ip, i32]),
+    "rsp_remap_cols_padded": (i32, [i64, ip, ip, i32, i32, ip]),
     "rsp_host_spmv_f64": (None, [i32, ip, ip, vp, vp, vp]),
     "rsp_host_spmv_f32": (None, [i32, ip, ip, vp, vp, vp]),
 }

@@ -49,3 +49,48 @@ void rsp_host_spmv_f32(int m, const int *rowptr, const int *colidx, const float 
         y[i] = s;
     }
 }
+
+/* Padded all-gather layout of a row-partitioned x: slice p's
+ * entries x[bounds[p] .. bounds[p+1]) sit at x_pad[p*chunk ..), chunk = the
+ * largest slice, so one equal-count all-gather (ncclAllGather, sendcount =
+ * chunk) reassembles x on every rank. */
+int rsp_padded_chunk(const int *bounds, int parts) {
+    if (!bounds || parts < 1) return -1;
+    int chunk = 0;
+    for (int p = 0; p < parts; p++) {
+        const int len = bounds[p + 1] - bounds[p];
+        if (len < 0) return -1;
+        if (len > chunk) chunk = len;
+    }
+    return chunk;
+}
+
+/* colidx_out[k] = padded position of global column colidx_in[k]: the slice
+ * p owning it (bounds[p] <= c < bounds[p+1], by binary search) gives
+ * p*chunk + (c - bounds[p]). In place allowed. */
+int rsp_remap_cols_padded(int64_t nnz, const int *colidx_in, const int *bounds, int parts, int chunk,
+                          int *colidx_out) {
+    if (nnz < 0 || (nnz > 0 && (!colidx_in || !colidx_out)) || !bounds || parts < 1 || chunk < 0)
+        return -1;
+    if ((int64_t)parts * chunk > 2147483647LL) return -1;
+    const int n = bounds[parts];
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t k = 0; k < nnz; k++) {
+        const int c = colidx_in[k];
+        if (c < 0 || c >= n) {
+            bad = 1;
+            continue;
+        }
+        int lo = 0, hi = parts - 1;  /* last p with bounds[p] <= c */
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (bounds[mid] <= c)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        colidx_out[k] = lo * chunk + (c - bounds[lo]);
+    }
+    return bad ? -1 : 0;
+}

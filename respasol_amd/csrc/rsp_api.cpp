@@ -40,6 +40,13 @@ struct rsp_context {
     unsigned long long *d_strace;
 };
 
+// The SpMV schedule lives in device memory owned by the matrix descriptor
+// (d_plan), not in the caller's workspace: it is built once, at
+// rsp_spmv_buffer_size time (where the reference calls
+// cusparseSpMV_bufferSize, GPU/spmv.cu:159-164, outside its timed loop), so
+// the reference's exact call sequence create_csr -> bufferSize -> malloc ->
+// 50x SpMV pays no planning inside a timed call, and any number of matrices
+// may share one workspace without re-planning.
 struct rsp_spmat {
     int64_t rows, cols, nnz;
     int *rowptr;
@@ -47,44 +54,24 @@ struct rsp_spmat {
     void *vals;
     rsp_datatype_t type;
     // schedule state
-    const void *plan_buffer;  // buffer the schedule was written into
+    int planned;                // d_plan holds a schedule for plan_type / local_cols
+    int plan_device;            // device d_plan was allocated on
+    void *d_plan;               // [tiles | long rows | partials | col bases | 16-bit offsets]
+    size_t plan_cap;            // bytes allocated at d_plan
     rsp_datatype_t plan_type;
     int nblocks, nlong, nslots;
-    int nnz_s;                  // rowptr[rows] seen by the preprocess
-    size_t off_long, off_part;  // byte offsets inside the buffer
+    int nnz_s;                  // rowptr[rows] seen by the planner
+    size_t off_long, off_part;  // byte offsets inside d_plan
     size_t off_cbase, off_cidx;
     int64_t nnz_c16;            // entries read through 16-bit column offsets
     int64_t local_cols;         // rsp_spmat_set_local_cols (-1: not split)
     int nint;                   // interior tiles at the front of the schedule
-    unsigned long long plan_gen;  // unique per preprocess / value rebind (plan registry key)
+    unsigned long long plan_gen;  // unique per plan / value rebind (batch staleness key)
 };
 
-// Which matrix last planned into each SpMV workspace. cuSPARSE lets several
-// matrices share one workspace; the schedule lives in it, so ownership is
-// recorded here (buffer -> plan generation of the owning preprocess, unique
-// process-wide) and a call on a buffer owned by another plan re-plans first.
 namespace {
-std::mutex g_plan_mu;
-std::unordered_map<const void *, unsigned long long> g_plan_owner;
 std::atomic<unsigned long long> g_plan_next{1};
-
 unsigned long long plan_new_gen() { return g_plan_next.fetch_add(1); }
-void plan_claim(const void *buf, unsigned long long gen) {
-    std::lock_guard<std::mutex> lk(g_plan_mu);
-    g_plan_owner[buf] = gen;
-}
-bool plan_owns(const rsp_spmat *m) {
-    if (!m->plan_buffer) return false;
-    std::lock_guard<std::mutex> lk(g_plan_mu);
-    auto it = g_plan_owner.find(m->plan_buffer);
-    return it != g_plan_owner.end() && it->second == m->plan_gen;
-}
-void plan_release(const rsp_spmat *m) {
-    if (!m->plan_buffer) return;
-    std::lock_guard<std::mutex> lk(g_plan_mu);
-    auto it = g_plan_owner.find(m->plan_buffer);
-    if (it != g_plan_owner.end() && it->second == m->plan_gen) g_plan_owner.erase(it);
-}
 }  // namespace
 
 struct rsp_ilu0_info {
@@ -239,7 +226,8 @@ rsp_status_t rsp_create_csr(rsp_spmat_t *mat, int64_t rows, int64_t cols, int64_
     a->colidx = (int *)d_col_ind;
     a->vals = d_values;
     a->type = value_type;
-    a->plan_buffer = nullptr;
+    a->planned = 0;
+    a->d_plan = nullptr;
     a->local_cols = -1;
     *mat = a;
     return RSP_STATUS_SUCCESS;
@@ -248,30 +236,29 @@ rsp_status_t rsp_create_csr(rsp_spmat_t *mat, int64_t rows, int64_t cols, int64_
 rsp_status_t rsp_spmat_set_local_cols(rsp_spmat_t mat, int64_t ncols_local) {
     if (!mat || ncols_local < 0 || ncols_local > mat->cols) return RSP_STATUS_INVALID_VALUE;
     mat->local_cols = ncols_local;
-    plan_release(mat);
-    mat->plan_buffer = nullptr;  // re-plan on the next call
+    mat->planned = 0;  // re-plan on the next call
     return RSP_STATUS_SUCCESS;
 }
 
 rsp_status_t rsp_csr_set_values(rsp_spmat_t mat, void *d_values, rsp_datatype_t value_type) {
     if (!mat) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
-    if (d_values != mat->vals && plan_owns(mat)) {  // batches hold the old pointer: new gen
-        mat->plan_gen = plan_new_gen();
-        plan_claim(mat->plan_buffer, mat->plan_gen);
-    }
+    if (d_values != mat->vals) mat->plan_gen = plan_new_gen();  // batches hold the old pointer
     mat->vals = d_values;
-    if (value_type != mat->type) {  // tile size depends on type
-        plan_release(mat);
-        mat->plan_buffer = nullptr;
-    }
+    if (value_type != mat->type) mat->planned = 0;  // tile size depends on type
     mat->type = value_type;
     return RSP_STATUS_SUCCESS;
 }
 
 rsp_status_t rsp_destroy_spmat(rsp_spmat_t mat) {
     if (!mat) return RSP_STATUS_INVALID_VALUE;
-    plan_release(mat);
+    if (mat->d_plan) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(mat->plan_device);
+        (void)hipFree(mat->d_plan);
+        (void)hipSetDevice(cur);
+    }
     delete mat;
     return RSP_STATUS_SUCCESS;
 }
@@ -328,6 +315,8 @@ static int spmv_row_align(rsp_handle_t h, rsp_datatype_t t) {
     return (h->spmv_variant & 64) ? 128 / e : (h->spmv_variant & 128) ? 64 / e : 1;
 }
 
+static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t compute_type);
+
 rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                   rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
                                   size_t *buffer_size) {
@@ -337,8 +326,14 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void
     if (!mat || !buffer_size) return RSP_STATUS_INVALID_VALUE;
     if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
     if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
-    SpmvBounds b = spmv_bounds(mat->rows, mat->nnz, chunk_cap(compute_type));
-    *buffer_size = spmv_layout(b, elem_size(compute_type), mat->nnz).bytes;
+    // the schedule is built here, into the matrix's own device memory (the
+    // reference calls bufferSize once, before its timed loop); the caller's
+    // workspace is not needed
+    if (!mat->planned || mat->plan_type != compute_type) {
+        rsp_status_t st = spmv_plan(h, mat, compute_type);
+        if (st != RSP_STATUS_SUCCESS) return st;
+    }
+    *buffer_size = 0;
     return RSP_STATUS_SUCCESS;
 }
 
@@ -529,17 +524,9 @@ static int64_t spmv_resident_tiles(rsp_handle_t h, rsp_datatype_t t) {
     return (int64_t)rsp_k::spmv_tiles_per_cu((int)elem_size(t)) * h->num_cus;
 }
 
-rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void *alpha,
-                                 rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
-                                 rsp_datatype_t compute_type, void *d_buffer) {
-    (void)alpha;
-    (void)beta;
-    (void)d_x;
-    (void)d_y;
-    if (!h) return RSP_STATUS_NOT_INITIALIZED;
-    if (!mat) return RSP_STATUS_INVALID_VALUE;
-    if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
-    if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
+// Build the schedule of `mat` for `compute_type` into the matrix's own device
+// memory (host-blocking; see struct rsp_spmat).
+static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t compute_type) {
     const int m = (int)mat->rows;
     std::vector<int> rp, ci;
     rsp_status_t st = download_pattern(h, mat, rp, ci);
@@ -562,14 +549,27 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     const std::vector<int> &cbase = p.cbase;
     const std::vector<uint16_t> &c16 = p.c16;
     const int64_t nnz_c16 = p.nnz_c16;
-    // the caller sized the buffer from mat->nnz; make sure the plan fits
-    // (bounds in units of the chunk, which is <= the packing cap)
-    SpmvBounds b = spmv_bounds(mat->rows, std::max<int64_t>(mat->nnz, 0), chunk);
-    if (blocks.size() > b.nblocks || longrows.size() > b.nlong || (size_t)nslots > b.nslots)
-        return RSP_STATUS_INVALID_VALUE;
-    if (!blocks.empty() && !d_buffer) return RSP_STATUS_INVALID_VALUE;
-    const SpmvLayout lay = spmv_layout(b, elem_size(compute_type), mat->nnz);
-    char *buf = (char *)d_buffer;
+    (void)chunk;
+    // exact layout of this schedule in the matrix's device memory (grown,
+    // never shrunk, on a re-plan)
+    SpmvBounds b{blocks.size(), longrows.size(), (size_t)nslots};
+    const SpmvLayout lay = spmv_layout(b, elem_size(compute_type), (int64_t)c16.size());
+    mat->planned = 0;
+    if (lay.bytes > mat->plan_cap || !mat->d_plan) {
+        if (mat->d_plan) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(mat->plan_device);
+            (void)hipFree(mat->d_plan);
+            (void)hipSetDevice(cur);
+            mat->d_plan = nullptr;
+            mat->plan_cap = 0;
+        }
+        RSP_CHECK_HIP(hipMalloc(&mat->d_plan, std::max<size_t>(lay.bytes, 256)));
+        mat->plan_cap = std::max<size_t>(lay.bytes, 256);
+        RSP_CHECK_HIP(hipGetDevice(&mat->plan_device));
+    }
+    char *buf = (char *)mat->d_plan;
     if (!blocks.empty()) {
         RSP_CHECK_HIP(hipMemcpyAsync(buf, blocks.data(), blocks.size() * sizeof(SpmvBlock),
                                      hipMemcpyHostToDevice, h->stream));
@@ -589,13 +589,11 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
         RSP_CHECK_HIP(hipMemsetAsync(buf + off_part, 0, (size_t)nslots * 2 * elem_size(compute_type),
                                      h->stream));
     RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
-    if (mat->plan_buffer != d_buffer) plan_release(mat);
-    mat->plan_buffer = d_buffer;
+    mat->planned = 1;
     mat->plan_type = compute_type;
     mat->nblocks = (int)blocks.size();
     mat->nint = nint;
     mat->plan_gen = plan_new_gen();
-    plan_claim(d_buffer, mat->plan_gen);
     mat->nlong = (int)longrows.size();
     mat->nslots = nslots;
     mat->nnz_s = m > 0 ? rp[(size_t)m] : 0;
@@ -607,9 +605,24 @@ rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void 
     return RSP_STATUS_SUCCESS;
 }
 
+rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                 rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
+                                 rsp_datatype_t compute_type, void *d_buffer) {
+    (void)alpha;
+    (void)beta;
+    (void)d_x;
+    (void)d_y;
+    (void)d_buffer;
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!mat) return RSP_STATUS_INVALID_VALUE;
+    if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
+    if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
+    return spmv_plan(h, mat, compute_type);  // explicit request: always re-plan
+}
+
 rsp_status_t rsp_spmv_plan_info(rsp_spmat_t mat, int64_t *tiles, int64_t *entries_16bit) {
     if (!mat || !tiles || !entries_16bit) return RSP_STATUS_INVALID_VALUE;
-    if (!mat->plan_buffer) return RSP_STATUS_NOT_INITIALIZED;
+    if (!mat->planned) return RSP_STATUS_NOT_INITIALIZED;
     *tiles = mat->nblocks;
     *entries_16bit = mat->nnz_c16;
     return RSP_STATUS_SUCCESS;
@@ -623,11 +636,12 @@ static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alp
     if (op != RSP_OPERATION_NON_TRANSPOSE) return RSP_STATUS_NOT_SUPPORTED;
     if (compute_type != mat->type) return RSP_STATUS_NOT_SUPPORTED;
     if (mat->rows > 0 && (!d_y || (mat->cols > 0 && !d_x))) return RSP_STATUS_INVALID_VALUE;
-    if (mat->plan_buffer != d_buffer || mat->plan_type != compute_type || !plan_owns(mat)) {
-        rsp_status_t st =
-            rsp_spmv_preprocess(h, op, alpha, mat, d_x, beta, d_y, compute_type, d_buffer);
+    (void)d_buffer;  // the schedule lives in the matrix (struct rsp_spmat)
+    if (!mat->planned || mat->plan_type != compute_type) {  // lazily, if bufferSize was skipped
+        rsp_status_t st = spmv_plan(h, mat, compute_type);
         if (st != RSP_STATUS_SUCCESS) return st;
     }
+    char *plan = (char *)mat->d_plan;
     rsp::SpmvArgs a;
     a.m = (int)mat->rows;
     a.rowptr = mat->rowptr;
@@ -635,14 +649,14 @@ static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alp
     a.vals = mat->vals;
     a.x = d_x;
     a.y = d_y;
-    a.blocks = (const SpmvBlock *)d_buffer;
+    a.blocks = (const SpmvBlock *)plan;
     a.nblocks = mat->nblocks;
-    a.cbases = (const int *)((char *)d_buffer + mat->off_cbase);
-    a.cidx = (const unsigned short *)((char *)d_buffer + mat->off_cidx);
+    a.cbases = (const int *)(plan + mat->off_cbase);
+    a.cidx = (const unsigned short *)(plan + mat->off_cidx);
     a.cmax = mat->cols > 0 ? (int)(mat->cols - 1) : 0;
-    a.longrows = (const SpmvLongRow *)((char *)d_buffer + mat->off_long);
+    a.longrows = (const SpmvLongRow *)(plan + mat->off_long);
     a.nlong = mat->nlong;
-    a.partials = (char *)d_buffer + mat->off_part;
+    a.partials = plan + mat->off_part;
     if (compute_type == RSP_R_64F) {
         a.alpha = *(const double *)alpha;
         a.beta = *(const double *)beta;
@@ -692,7 +706,6 @@ struct rsp_spmv_batch {
     rsp_datatype_t type;
     int part;
     std::vector<rsp_spmat_t> mats;
-    std::vector<const void *> buffers;
     std::vector<unsigned long long> plan_gen;  // schedules as copied (stale check)
     std::vector<rsp::SpmvBatchArgs> launches;  // one per kSpmvBatchMax matrices
     void *d_mem = nullptr;                      // entries, tiles, long rows of every launch
@@ -707,25 +720,21 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
                                    void *const *d_buffers, rsp_datatype_t compute_type,
                                    int part, rsp_spmv_batch_t *batch) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
-    if (!batch || count < 0 || (count > 0 && (!mats || !d_x || !d_y || !d_buffers)))
+    (void)d_buffers;  // workspaces are not needed: schedules live in the matrices
+    if (!batch || count < 0 || (count > 0 && (!mats || !d_x || !d_y)))
         return RSP_STATUS_INVALID_VALUE;
     if (part < 0 || part > 2) return RSP_STATUS_INVALID_VALUE;
     if (compute_type != RSP_R_64F && compute_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     *batch = nullptr;
-    const double one = 1.0, zero = 0.0;
-    const float onef = 1.0f, zerof = 0.0f;
-    const void *pa = compute_type == RSP_R_64F ? (const void *)&one : (const void *)&onef;
-    const void *pb = compute_type == RSP_R_64F ? (const void *)&zero : (const void *)&zerof;
     for (int j = 0; j < count; j++) {
         rsp_spmat_t A = mats[j];
-        if (!A || !d_buffers[j]) return RSP_STATUS_INVALID_VALUE;
+        if (!A) return RSP_STATUS_INVALID_VALUE;
         if (A->type != compute_type) return RSP_STATUS_NOT_SUPPORTED;
         if (A->rows > 0 && (!d_y[j] || (A->cols > 0 && !d_x[j]))) return RSP_STATUS_INVALID_VALUE;
-        for (int q = 0; q < j; q++)  // one workspace holds one schedule
-            if (d_buffers[q] == d_buffers[j]) return RSP_STATUS_INVALID_VALUE;
-        if (A->plan_buffer != d_buffers[j] || A->plan_type != compute_type || !plan_owns(A)) {
-            rsp_status_t st = rsp_spmv_preprocess(h, RSP_OPERATION_NON_TRANSPOSE, pa, A, d_x[j],
-                                                  pb, d_y[j], compute_type, d_buffers[j]);
+        for (int q = 0; q < j; q++)  // a matrix's long-row tickets serve one launch slot
+            if (mats[q] == A) return RSP_STATUS_INVALID_VALUE;
+        if (!A->planned || A->plan_type != compute_type) {
+            rsp_status_t st = spmv_plan(h, A, compute_type);
             if (st != RSP_STATUS_SUCCESS) return st;
         }
     }
@@ -817,7 +826,7 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         for (int q = 0; q < sp.count; q++) {
             rsp_spmat_t A = mats[sp.first + q];
             const TilePlan &p = plans[sp.first + q];
-            const char *buf = (const char *)d_buffers[sp.first + q];
+            const char *buf = (const char *)A->d_plan;  // its long-row partials and tickets
             int t0, t1;
             tile_range(p, &t0, &t1);
             const int nlq = part == 1 ? 0 : (int)p.longrows.size();
@@ -859,7 +868,6 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
     if (bytes > 0) RSP_CHECK_HIP(hipMemcpy(b->d_mem, host.data(), bytes, hipMemcpyHostToDevice));
     for (int j = 0; j < count; j++) {
         b->mats.push_back(mats[j]);
-        b->buffers.push_back(d_buffers[j]);
         b->plan_gen.push_back(mats[j]->plan_gen);
     }
     *batch = b.release();
@@ -872,8 +880,7 @@ rsp_status_t rsp_spmv_batch_run(rsp_handle_t h, rsp_spmv_batch_t b, const void *
     if (!b || !alpha || !beta) return RSP_STATUS_INVALID_VALUE;
     for (size_t j = 0; j < b->mats.size(); j++) {  // re-planned since create: stale copy
         const rsp_spmat_t A = b->mats[j];
-        if (A->plan_buffer != b->buffers[j] || A->plan_gen != b->plan_gen[j] || !plan_owns(A))
-            return RSP_STATUS_INVALID_VALUE;
+        if (!A->planned || A->plan_gen != b->plan_gen[j]) return RSP_STATUS_INVALID_VALUE;
     }
     const double av = b->type == RSP_R_64F ? *(const double *)alpha : *(const float *)alpha;
     const double bv = b->type == RSP_R_64F ? *(const double *)beta : *(const float *)beta;
@@ -1700,7 +1707,17 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         const std::vector<int> &lp = f->L.ptr;
         const int nlev = (int)lp.size() - 1;
         f->fslev.assign((size_t)std::max(nlev, 0), rsp::FacSlotLevel{0, 0, 0, 0, 0});
-        const long long cap = (long long)env_int("RSP_ILU_SLOT_CAP_MB", 2048) * (1LL << 20) / 4;
+        // Slot budget (ints): RSP_ILU_SLOT_CAP_MB if set, else the smaller of
+        // 2 GB and 1/8 of the device memory free now. A level whose padded
+        // slots would take more than twice its rows' own structure (one large
+        // row among many small ones) keeps the FacRow path.
+        long long cap_mb = env_int("RSP_ILU_SLOT_CAP_MB", -1);
+        if (cap_mb < 0) {
+            size_t fr = 0, tot = 0;
+            cap_mb = 2048;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap_mb = std::min<long long>(cap_mb, (long long)(fr >> 23));
+        }
+        const long long cap = cap_mb * (1LL << 20) / 4;
         long long total = 0;
         std::vector<int> slot_levels;
         slot_desc.clear();
@@ -1709,6 +1726,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
             if (sg.thin) continue;
             for (int l = sg.lb; l < sg.le; l++) {
                 int rm = 0, qm = 0;
+                long long own = 0;
                 for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
                     const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
                     const int nq = sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs];
@@ -1716,10 +1734,12 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
                         rm = std::max(rm, re - rs);
                         qm = std::max(qm, nq);
                     }
+                    own += (rsp::fac_pairs_at(std::min(re - rs, rsp::kFacRow)) + 2 * std::min(nq, rsp::kFacPairs) + 3) & ~3;
                 }
                 if (rm == 0 || qm == 0) continue;
                 const int stride = (rsp::fac_pairs_at(rm) + 2 * qm + 3) & ~3;
                 const long long cnt = lp[(size_t)l + 1] - lp[(size_t)l];
+                if (cnt * stride > 2 * own) continue;  // padding would dominate
                 if (total + cnt * stride > cap) continue;
                 f->fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, rm, qm, 0};
                 total += cnt * stride;
@@ -1734,7 +1754,15 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
                     slot_offs.push_back(sl.off + (long long)(x - lp[(size_t)l]) * sl.stride);
                 }
             }
-            if (e == hipSuccess) e = hipMalloc((void **)&f->d_fslots, (size_t)total * sizeof(int));
+            // the slot layout is an optimisation: without its memory the
+            // FacRow path factors every fat level (same bits)
+            if (e == hipSuccess && hipMalloc((void **)&f->d_fslots, (size_t)total * sizeof(int)) != hipSuccess) {
+                (void)hipGetLastError();
+                f->d_fslots = nullptr;
+                f->fslev.assign(f->fslev.size(), rsp::FacSlotLevel{0, 0, 0, 0, 0});
+                slot_desc.clear();
+                slot_offs.clear();
+            }
         }
     }
     if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
@@ -1773,9 +1801,9 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     if (e == hipSuccess && !slot_desc.empty()) {  // fat factor slots, written on the device
         int4 *d_desc = nullptr;
         long long *d_offs = nullptr;
-        e = upload_vec(&d_desc, slot_desc);
-        if (e == hipSuccess) e = upload_vec(&d_offs, slot_offs);
-        if (e == hipSuccess) {
+        hipError_t es = upload_vec(&d_desc, slot_desc);
+        if (es == hipSuccess) es = upload_vec(&d_offs, slot_offs);
+        if (es == hipSuccess) {
             rsp::IluArgs a{};
             a.n = n;
             a.rowptr = d_row_offsets;
@@ -1788,11 +1816,17 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
             a.lend = f->d_lend;
             a.udiv = f->d_udiv;
             a.plan.rows = f->L.d_rows;
-            e = rsp_k::ilu0_build_slots(a, d_desc, d_offs, (int)slot_desc.size(), f->d_fslots, h->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+            es = rsp_k::ilu0_build_slots(a, d_desc, d_offs, (int)slot_desc.size(), f->d_fslots, h->stream);
+            if (es == hipSuccess) es = hipStreamSynchronize(h->stream);
         }
         if (d_desc) (void)hipFree(d_desc);
         if (d_offs) (void)hipFree(d_offs);
+        if (es != hipSuccess) {  // no slots: fall back to the FacRow path, not a failed analysis
+            (void)hipGetLastError();
+            (void)hipFree(f->d_fslots);
+            f->d_fslots = nullptr;
+            f->fslev.assign(f->fslev.size(), rsp::FacSlotLevel{0, 0, 0, 0, 0});
+        }
     }
     phase("uploads");
     if (e != hipSuccess) {

@@ -2,7 +2,8 @@
 // fp32 (fp32 storage AND accumulation, as cusparseSpMV with CUDA_R_32F,
 // GPU/spmv.cu:131-145,179-181). Replaces cusparseSpMV (GPU/spmv.cu:148-186).
 //
-// Schedule ("row-block" tiles, built on the host by rsp_spmv_preprocess):
+// Schedule ("row-block" tiles, built once per matrix by rsp_spmv_buffer_size /
+// rsp_spmv_preprocess into the matrix's own device memory):
 // consecutive rows are packed into tiles of at most SpmvTile<T>::kMaxNnz
 // entries (<= SpmvTile<T>::kMaxRows rows); one 256-thread workgroup per tile.
 //   1. stream: each thread issues all of its 16-byte colidx/vals loads for
@@ -15,10 +16,12 @@
 //      y = ((p0+p4)+(p2+p6)) + ((p1+p5)+(p3+p7)) — which every L realises
 //      exactly (local tree stages for offsets >= L, shuffles below). So y is
 //      bitwise independent of how rows are packed into tiles or split over
-//      GPUs, and equal to the oracle's oracle_spmv_w8_* bit for bit.
+//      GPUs, and equal to the oracle's oracle_spmv_canon_* bit for bit.
 // Rows longer than a tile are cut into tile-sized chunks (relative to the row
-// start); each chunk is reduced by all 256 threads in a fixed tree and a tiny
-// fixup kernel adds the chunk partials in order. Everything is deterministic.
+// start); each chunk is reduced by all 256 threads in a fixed tree, and the
+// chunk that arrives last adds the chunk partials in order (longrow_arrive;
+// RSP_SPMV_VARIANT bit 8 uses a separate fixup launch instead). Everything is
+// deterministic.
 //
 // Roofline: HBM-bound, no MFMA (no dense contraction). Algorithmic bytes per
 // call: (sizeof(T)+4)*nnz_s + 4*(m+1) + sizeof(T)*(n + m) (+ sizeof(T)*m if
@@ -298,11 +301,12 @@ __device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
 // A chunk of a long row (one lane): publish the chunk's partial, take a
 // ticket; the chunk that arrives last adds the row's partials in chunk order
 // (the fixup kernel's order: 0 + p0 + p1 + ...) and writes y. Partials and
-// tickets move only through agent-scope atomics (the partial by exchange, the
-// read by fetch-add of 0), which are performed at the device's coherence
-// point, so no L1 / per-XCD L2 copy is ever read; each chunk's exchange has
-// returned before its ticket add is issued. No wait, no spin: the last
-// arriver is told by the value its own add returned. It resets the ticket.
+// tickets are agent-scope atomics; the ticket add is a release and the last
+// arriver issues an acquire fence before reading the partials, so the
+// ordering holds under the HIP memory model for chunks on any XCD (gfx950:
+// an L2 write-back before the add, an L2 invalidate in the last arriver).
+// No wait, no spin: the last arriver is told by the value its own add
+// returned. It resets the ticket.
 template <typename T>
 __device__ __forceinline__ void longrow_arrive(const SpmvBlock blk, const int *__restrict__ rowptr,
                                                T *partials, T *__restrict__ y, T t, T alpha, T beta,
@@ -315,17 +319,18 @@ __device__ __forceinline__ void longrow_arrive(const SpmvBlock blk, const int *_
     const int n = (re - rs + C - 1) / C;
     U *pv = reinterpret_cast<U *>(partials);
     unsigned int *ticket = reinterpret_cast<unsigned int *>(partials + 2 * first + 1);
-    const U prev = __hip_atomic_exchange(pv + 2 * slot, __builtin_bit_cast(U, t), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    (void)prev;
+    __hip_atomic_store(pv + 2 * slot, __builtin_bit_cast(U, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release: this chunk's partial is visible device-wide before its ticket
+    // moves; the last arriver's acquire fence then orders its partial reads
+    // after every other chunk's release (the standard last-block pattern)
     const unsigned int arrived =
-        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (arrived != (unsigned int)(n - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     T s = T(0);
     for (int c = 0; c < n; ++c)
-        s += __builtin_bit_cast(T, __hip_atomic_fetch_add(pv + 2 * (first + c), U(0), __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT));
+        s += __builtin_bit_cast(T, __hip_atomic_load(pv + 2 * (first + c), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT));
     T out = alpha * s;
     if (beta_nz) out += beta * y[blk.r0];
     y[blk.r0] = out;

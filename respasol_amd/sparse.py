@@ -4,8 +4,9 @@ plumbing only; every operation runs the HIP kernels of librsp.so.
 
 Mapping to the reference's cuSPARSE usage:
   Handle                 cusparseCreate / cusparseDestroy   (GPU/spmv.cu:128,282)
-  SpMat                  cusparseCreateCsr + SpMV_bufferSize + the caller's
-                         workspace cudaMalloc                (GPU/spmv.cu:148-164)
+  SpMat                  cusparseCreateCsr + SpMV_bufferSize (builds the
+                         schedule) + the caller's workspace cudaMalloc
+                                                             (GPU/spmv.cu:148-164)
   SpMat.spmv             cusparseSpMV                        (GPU/spmv.cu:184-186)
   SpmvBatch              cusparseSpMV over several matrices as one launch (no
                          cuSPARSE counterpart; bits equal to SpMat.spmv each)
@@ -106,10 +107,9 @@ class SpMat:
         check(rsp.rsp_spmv_buffer_size(handle.ptr, _lib.OP_N, C.byref(one), self._mat,
                                        C.byref(zero), _DT[self.dtype], C.byref(size)),
               "rsp_spmv_buffer_size")
+        # the reference's sequence (GPU/spmv.cu:159-164): bufferSize (which
+        # builds the schedule inside the matrix) and the caller's workspace
         self.buffer = torch.empty(max(int(size.value), 1), dtype=torch.uint8, device=values.device)
-        check(rsp.rsp_spmv_preprocess(handle.ptr, _lib.OP_N, C.byref(one), self._mat, None,
-                                      C.byref(zero), None, _DT[self.dtype], _ptr(self.buffer)),
-              "rsp_spmv_preprocess")
 
     @property
     def nnz_stored(self) -> int:

@@ -50,6 +50,40 @@ def test_spmv_driver_fp32_ftz_both_and_stats():
         assert float(e) < 1e-5
 
 
+def test_spmv_driver_ref_sequence_serena():
+    """--ref-sequence (the default): GPU/spmv.cu:143-195 verbatim, no
+    preprocess call before the 50 timed calls. Timed call 0 must cost no more
+    than 2x the median, and the 50-rep mean must match the mean with an
+    explicit preprocess within 5 % (full-size Serena surrogate)."""
+    def reps(*extra):
+        out = run("test_spmv", "surrogate:Serena", "--rep-times", *extra)
+        m = re.search(rf"REPS first_us=({FLOAT}) median_us=({FLOAT}) mean_us=({FLOAT})", out)
+        assert m, out
+        return [float(v) for v in m.groups()]
+    first, med, mean = reps("--ref-sequence")
+    assert first <= 2.0 * med, (first, med)
+    _, _, mean_pre = reps("--preprocess")
+    assert abs(mean - mean_pre) <= 0.05 * mean_pre, (mean, mean_pre)
+
+
+def test_spmv_driver_ngpu_rccl():
+    """--ngpu=N: the C driver's row-partitioned SpMV over an RCCL clique
+    (ncclCommInitAll + grouped in-place ncclAllGather of the padded x, then
+    the local SpMV). On a one-GPU box N = 1 is the run that exercises RCCL from
+    C; Error= over the reassembled y (mean |host - GPU|, host in column order)
+    must be at rounding level, and asking for more GPUs than visible is a
+    clean error."""
+    out = run("test_spmv", "surrogate:Serena@0.05", "--ngpu=1", "--prec=both", "--reps=10")
+    assert re.search(rf"DOUBLE PRECISION SPMV solve time \(microseconds\) = {FLOAT}", out), out
+    assert re.search(rf"NGPU=1 exchange=allgather chunk=\d+ allgather_us={FLOAT} spmv_us={FLOAT}", out), out
+    errs = [float(e) for e in re.findall(r"Error= (\S+)", out)]
+    assert len(errs) == 2 and errs[0] < 1e-10 and errs[1] < 1e-4, out
+    n = torch.cuda.device_count()
+    r = subprocess.run([os.path.join(BIN, "test_spmv"), "surrogate:Serena@0.01", f"--ngpu={n + 1}"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr
+
+
 def test_ilu0_driver_reference_format():
     out = run("test_ilu0", os.path.join(MTX, "bcspwr01.mtx"))
     pat = (rf"DOUBLE PRECISION SOLVE IN  MILLISECONDS\n Symbolic = {FLOAT}\n Numeric = {FLOAT} \n"

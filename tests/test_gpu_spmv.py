@@ -301,42 +301,72 @@ def test_kernel_variants_same_bits(monkeypatch, variant):
 
 
 def test_shared_workspace_alternating(handle):
-    """Several matrices may share one SpMV workspace (cusparseSpMV without
-    preprocess treats it as scratch). Preprocess A into it, then B, then call
-    A, B, A: every call must re-plan for its own matrix (ownership registry,
-    rsp_api.cpp) and give the canonical-order bits."""
+    """Several matrices may share one SpMV workspace (cusparseSpMV treats it
+    as scratch). The schedule lives in each matrix (built at bufferSize), so
+    calls alternating A, B, A, B on one shared workspace give the
+    canonical-order bits without re-planning (plan generation unchanged)."""
     from respasol_amd import RspError
     from respasol_amd.sparse import SpmvBatch
     A = csr.surrogate("cfd2", 0.05)
-    B = csr.surrogate("ASIC_320ks", 0.1)  # different shape, hub rows (long-row fixup)
+    B = csr.surrogate("ASIC_320ks", 0.1)  # different shape, hub rows (long-row tickets)
     xa, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
     xb, _ = csr.dlarnv(2, [0, 0, 0, 1], B.n)
     ma = SpMat(handle, *upload_csr(A.rowptr, A.colidx, A.values), A.n)
     mb = SpMat(handle, *upload_csr(B.rowptr, B.colidx, B.values), B.n)
-    shared = torch.empty(max(ma.buffer.numel(), mb.buffer.numel()), dtype=torch.uint8, device="cuda")
-    own_a, own_b = ma.buffer, mb.buffer
+    shared = torch.empty(1, dtype=torch.uint8, device="cuda")
     ma.buffer = mb.buffer = shared
-    ma.set_local_cols(A.n)  # re-preprocess A into the shared buffer (whole-matrix plan)
-    mb.set_local_cols(B.n)  # ... then B over it
+    info_a, info_b = ma.plan_info(), mb.plan_info()
     ref_a = ob.spmv(A.rowptr, A.colidx, A.values, xa, order="canon")
     ref_b = ob.spmv(B.rowptr, B.colidx, B.values, xb, order="canon")
     dxa, dxb = torch.from_numpy(xa).cuda(), torch.from_numpy(xb).cuda()
     for mat, dx, ref in ((ma, dxa, ref_a), (mb, dxb, ref_b), (ma, dxa, ref_a), (mb, dxb, ref_b)):
         y = mat.spmv(dx).cpu().numpy()
-        assert same_bits(y, ref), "shared workspace ran another matrix's schedule"
-    # a batch over one workspace twice is rejected; a batch whose schedule was
-    # overwritten by another matrix's preprocess since create is stale
+        assert same_bits(y, ref), "shared workspace changed the result"
+    assert ma.plan_info() == info_a and mb.plan_info() == info_b
     ya, yb = torch.empty(A.m, dtype=torch.float64, device="cuda"), torch.empty(B.m, dtype=torch.float64, device="cuda")
-    with pytest.raises(RspError) as e:
-        SpmvBatch(handle, [ma, mb], [dxa, dxb], [ya, yb])
+    with pytest.raises(RspError) as e:  # one matrix twice in a batch: its tickets would collide
+        SpmvBatch(handle, [ma, ma], [dxa, dxa], [ya, ya])
     assert e.value.status == 3
-    mb.buffer = own_b  # A keeps the shared workspace
-    bt = SpmvBatch(handle, [ma, mb], [dxa, dxb], [ya, yb])
+    bt = SpmvBatch(handle, [ma, mb], [dxa, dxb], [ya, yb])  # same shared workspace: fine
     bt.run()
     assert same_bits(ya.cpu().numpy(), ref_a) and same_bits(yb.cpu().numpy(), ref_b)
-    mb.buffer = shared
-    mb.spmv(dxb)  # B re-plans into A's workspace: the batch's copy of A is stale
+    mb.set_local_cols(B.n)  # B re-planned: the batch's copy of B is stale
     with pytest.raises(RspError) as e:
         bt.run()
     assert e.value.status == 3
     bt.close()
+
+
+def test_reference_call_sequence_plans_nothing_in_rep0(handle):
+    """GPU/spmv.cu:143-195 verbatim (create_csr -> bufferSize -> malloc ->
+    SpMV, no preprocess): the schedule is built by bufferSize, so timed call 0
+    costs what the later calls do (event pair per call, synchronised)."""
+    from respasol_amd import _lib
+    from respasol_amd._lib import check, rsp
+    import ctypes as C
+    A = csr.surrogate("Serena", 0.25)
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
+    mat = C.c_void_p()
+    check(rsp.rsp_create_csr(C.byref(mat), A.m, A.n, A.nnz_stored, C.c_void_p(rp.data_ptr()),
+                             C.c_void_p(ci.data_ptr()), C.c_void_p(va.data_ptr()), _lib.R_64F), "create")
+    one, zero, size = C.c_double(1.0), C.c_double(0.0), C.c_size_t()
+    check(rsp.rsp_spmv_buffer_size(handle.ptr, _lib.OP_N, C.byref(one), mat, C.byref(zero), _lib.R_64F,
+                                   C.byref(size)), "bufferSize")
+    buf = torch.empty(max(size.value, 1), dtype=torch.uint8, device="cuda")
+    x = torch.ones(A.n, dtype=torch.float64, device="cuda")
+    y = torch.empty(A.m, dtype=torch.float64, device="cuda")
+    times = []
+    for _ in range(20):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        check(rsp.rsp_spmv(handle.ptr, _lib.OP_N, C.byref(one), mat, C.c_void_p(x.data_ptr()),
+                           C.byref(zero), C.c_void_p(y.data_ptr()), _lib.R_64F, C.c_void_p(buf.data_ptr())),
+              "spmv")
+        e.record()
+        e.synchronize()
+        times.append(s.elapsed_time(e))
+    med = sorted(times)[len(times) // 2]
+    assert times[0] <= 2.0 * med + 0.02, (times[0], med)
+    ref = ob.spmv(A.rowptr, A.colidx, A.values, np.ones(A.n), order="canon")
+    assert same_bits(y.cpu().numpy(), ref)
+    rsp.rsp_destroy_spmat(mat)

@@ -173,3 +173,50 @@ def test_batch_stale_and_empty(handle):
     torch.cuda.synchronize()
     with pytest.raises(ValueError):
         SpmvBatch(handle, mats[:1], xs[:1], [ys[0][:0]])
+
+
+@pytest.mark.parametrize("variant", [0, 8])
+def test_batch_many_chunk_hub_rows(monkeypatch, variant):
+    """Hub rows of 20-40 chunks (fp64 2047 / fp32 4093 entries each) finished
+    by their last-arriving chunk (release ticket add, acquire fence in the
+    last arriver), with and without the per-matrix XCD swizzle (variant bit
+    3 off spreads a row's chunks over the XCDs): every repeat gives the
+    canonical-order oracle's bits."""
+    import oracle_bind as ob
+    monkeypatch.setenv("RSP_SPMV_VARIANT", str(variant))
+    h = Handle()
+    try:
+        rng = np.random.default_rng(5)
+        n = 60000
+        cols, lens = [], []
+        for i in range(n):
+            if i % 4999 == 0:
+                c = np.sort(rng.choice(n, 40000 + (i % 7) * 3000, replace=False)).astype(np.int32)
+            else:
+                c = np.unique(np.clip(i + rng.integers(-40, 41, 6), 0, n - 1)).astype(np.int32)
+            cols.append(c)
+            lens.append(len(c))
+        rp = np.zeros(n + 1, np.int32)
+        np.cumsum(lens, out=rp[1:])
+        ci = np.concatenate(cols)
+        va = rng.uniform(-1, 1, len(ci))
+        for dt in (torch.float64, torch.float32):
+            x = rng.uniform(-1, 1, n).astype(NP[dt])
+            canon = ob.spmv(rp, ci, va.astype(NP[dt]), x, order="canon")
+            mats, xs, ys = [], [], []
+            for k in range(3):  # three copies: chunks of several matrices in flight together
+                M = SpMat(h, *upload_csr(rp, ci, va, dt), n)
+                mats.append(M)
+                xs.append(torch.from_numpy(x).cuda())
+                ys.append(torch.empty(n, dtype=dt, device="cuda"))
+            B = SpmvBatch(h, mats, xs, ys)
+            for rep in range(10):
+                B.run()
+                torch.cuda.synchronize()
+                for y in ys:
+                    assert same_bits(y.cpu().numpy(), canon), (dt, rep)
+            for M, xd in zip(mats, xs):
+                assert same_bits(M.spmv(xd).cpu().numpy(), canon)
+            B.close()
+    finally:
+        h.close()

@@ -180,3 +180,42 @@ def test_buffer_loader_stays_inside_len():
     assert st == 0
     A = csr._from_struct(s, 0)
     assert A.values.tolist() == [2.5]
+
+
+def test_padded_allgather_layout_c_matches_python():
+    """rsp_padded_chunk / rsp_remap_cols_padded (the C driver's --ngpu layout)
+    equal dist.padded_layout / remap_columns, and an emulated equal-count
+    all-gather of the slices through that layout reproduces the global x at
+    every remapped column (the exchange logic, no GPU)."""
+    import ctypes as C
+    from respasol_amd import _lib
+    from respasol_amd.dist import remap_columns
+    A = csr.surrogate("G2_circuit", 0.3)
+    x = np.random.default_rng(2).uniform(-1, 1, A.n)
+    for P in (1, 2, 3, 8):
+        bounds = csr.partition_rows(A.rowptr, P)
+        ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+        chunk = _lib.host.rsp_padded_chunk(ip(bounds), P)
+        ref_cols, ref_chunk = remap_columns(A.colidx, bounds)
+        assert chunk == ref_chunk
+        out = np.empty_like(A.colidx)
+        assert _lib.host.rsp_remap_cols_padded(len(A.colidx), ip(A.colidx), ip(bounds), P, chunk, ip(out)) == 0
+        assert np.array_equal(out, ref_cols)
+        # every rank contributes its slice (count = chunk, padded); the gathered
+        # buffer read at the remapped columns is x at the original columns
+        xp = np.full(P * chunk, np.nan)
+        for p in range(P):
+            xp[p * chunk: p * chunk + bounds[p + 1] - bounds[p]] = x[bounds[p]:bounds[p + 1]]
+        assert np.array_equal(xp[out], x[A.colidx])
+        # row slices of the product reassemble A x exactly
+        y = np.empty(A.m)
+        for p in range(P):
+            r0, r1 = bounds[p], bounds[p + 1]
+            k0 = A.rowptr[r0]
+            rp = A.rowptr[r0:r1 + 1] - k0
+            y[r0:r1] = ob.spmv(rp, out[k0:A.rowptr[r1]], A.values[k0:A.rowptr[r1]], xp[: P * chunk])
+        assert np.array_equal(y, ob.spmv(A.rowptr, A.colidx, A.values, x))
+    bad = np.array([0, 5, A.n], np.int32)  # column n is out of range
+    b = csr.partition_rows(A.rowptr, 2)
+    assert _lib.host.rsp_remap_cols_padded(3, ip(bad), ip(b), 2, _lib.host.rsp_padded_chunk(ip(b), 2),
+                                           ip(np.empty(3, np.int32))) == -1
