@@ -160,11 +160,25 @@ def cpu_baseline(slices, seconds):
                       f"({el:.1f} s), OpenMP row-parallel CSR, x=dlarnv(1,{{0,0,0,1}})"}
 
 
+def spmv_kernel_sha():
+    """sha256 (16 hex) of the SpMV kernel sources (spmv.hip + rsp_kernels.h):
+    the build a PMC summary must have been recorded for."""
+    import hashlib
+    hsh = hashlib.sha256()
+    for f in ("spmv.hip", "rsp_kernels.h"):
+        with open(os.path.join(ROOT, "respasol_amd", "csrc", f), "rb") as fh:
+            hsh.update(fh.read())
+    return hsh.hexdigest()[:16]
+
+
 def pmc_traffic(workload, batched):
     """HBM bytes per dominant-kernel launch (the batched launch, or one
     per-matrix launch with --no-batch) from a committed rocprofv3 --pmc
-    summary (profiles/*pmc*.json written by scripts/pmc_summary.py), or None."""
-    best = None
+    summary (profiles/*pmc*.json written by scripts/pmc_summary.py) recorded
+    for THIS kernel build (its kernel_sha equals spmv_kernel_sha()); a summary
+    of another build is refused. Returns (bytes or None, source dict)."""
+    sha = spmv_kernel_sha()
+    best, src, seen = None, None, []
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
@@ -172,17 +186,26 @@ def pmc_traffic(workload, batched):
             continue
         if d.get("workload") != workload:
             continue
+        seen.append(os.path.relpath(p, ROOT))
+        if d.get("kernel_sha") != sha:
+            continue
         part = d.get("batch") if batched else d.get("per_matrix", d)
         if part and "hbm_bytes_per_launch" in part:
             best = part["hbm_bytes_per_launch"]
-    return best
+            src = {"file": os.path.relpath(p, ROOT), "kernel_sha": sha, "commit": d.get("commit"),
+                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate runs), calibrated"}
+    if src is None:
+        src = {"file": None, "kernel_sha": sha,
+               "note": "no PMC summary recorded for this kernel build (refused: "
+                       + (", ".join(seen) if seen else "none found") + ")"}
+    return best, src
 
 
 class Workload:
     """One bench step over a set of matrices on this rank: the slices, the
     RCCL halo exchange (N > 1), the batched launches and the step itself."""
 
-    def __init__(self, names, rank, world, handle, device, args):
+    def __init__(self, names, rank, world, handle, device, args, batch=True):
         self.world, self.device = world, device
         self.overlap = overlap = world > 1 and args.exchange == "halo" and not args.no_overlap
         self.slices = slices = [Slice(n, rank, world, handle, device, args.exchange, overlap) for n in names]
@@ -207,7 +230,7 @@ class Workload:
         # step's SpMVs cost one kernel ramp and drain instead of one per
         # matrix (--no-batch: one rsp_spmv per matrix)
         self.batches = {}
-        if not args.no_batch:
+        if batch and not args.no_batch:
             for part in ((0, 1, 2) if overlap else (0,)):
                 self.batches[part] = SpmvBatch(handle, [s.mat64 for s in slices], [s.x64() for s in slices],
                                                [s.y64 for s in slices], part)
@@ -479,7 +502,9 @@ def main():
     # the hard case for scaling (about 11 us of compute per GPU at N = 8)
     config5 = None
     if args.workload == "big" and not args.no_config5:
-        W5 = Workload(["Serena"], rank, world, handle, device, args)
+        # one matrix: rsp_spmv / rsp_spmv_part launches (spmv_tiles), so the
+        # batched kernel's rocprof average covers the headline step alone
+        W5 = Workload(["Serena"], rank, world, handle, device, args, batch=False)
         W5.ramp(20.0, device)
         el5, _, _ = W5.timed(args.steps, args.warmup)
         f5, b5 = W5.totals()
@@ -497,7 +522,8 @@ def main():
         cpu = cpu_baseline(slices, args.cpu_seconds)
 
     if rank == 0:
-        traffic = pmc_traffic(args.workload, bool(batches)) if world == 1 else None  # PMC run was N = 1
+        traffic, traffic_src = (pmc_traffic(args.workload, bool(batches)) if world == 1  # PMC run was N = 1
+                                else (None, {"file": None, "note": "PMC summaries are recorded at N = 1"}))
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -545,6 +571,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_us": round(kern_ms / launches * 1e3, 3),
                 "bytes_per_launch_avg": int(bytes64 / per_step),
                 "note": "achieved/frac count the CSR's algorithmic bytes (SURVEY 8d: 12 B per stored "

@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import sys
 
 
 def load(dirname, counter, kernel="spmv_tiles<double"):
@@ -42,6 +43,8 @@ def main():
     ap.add_argument("--meta", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--workload", default="big")
+    ap.add_argument("--commit", default=os.environ.get("RSP_COMMIT"),
+                    help="git commit the profiled tree was taken from (the GPU box has no .git)")
     args = ap.parse_args()
     meta = json.load(open(args.meta))
     fetch = load(args.fetch, "FETCH_SIZE")
@@ -89,8 +92,12 @@ def main():
                  "moved_bytes_per_launch": round(moved_b), "traffic_over_moved": round(hbm_b / moved_b, 4),
                  "launches": nb}
     top = batch or per_matrix
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import spmv_kernel_sha  # the build bench.py accepts this summary for
     out = {
         "workload": args.workload,
+        "kernel_sha": spmv_kernel_sha(),
+        "commit": args.commit,
         "kernel": top["kernel"],
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs; corrected by a "
                   "diagonal-matrix calibration launch of the same tile code with exactly known bytes",
