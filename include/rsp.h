@@ -253,6 +253,21 @@ rsp_status_t rsp_spmv_batch_info(rsp_spmv_batch_t batch, int64_t *tiles, int64_t
 /* Number of dependency levels found by the analysis (L DAG, L^T DAG). */
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *levels_upper);
 
+/* Tests and profiling (no cuSPARSE counterpart, no device needed): the host
+ * phases of rsp_ilu0_analysis on HOST arrays (base 0) — validation, levels,
+ * symbolic factor, factor and solve plans. Returns the level counts, a 64-bit
+ * digest of every array built (equal to rsp_ilu0_plan_digest of a device
+ * analysis of the same pattern, whatever runs where) and, if phase_ms is not
+ * NULL, the wall time of its 6 phases in ms. Same status codes as the
+ * analysis (INVALID_VALUE for a malformed or unsorted pattern). */
+rsp_status_t rsp_ilu0_analysis_host(int n, const int *row_offsets, const int *col_ind,
+                                    int *levels_lower, int *levels_upper, uint64_t *digest,
+                                    double *phase_ms);
+/* The digest of the plan an rsp_ilu0_analysis built (see above); computed
+ * only when the environment sets RSP_ILU_DIGEST=1 at analysis time
+ * (INVALID_VALUE otherwise). */
+rsp_status_t rsp_ilu0_plan_digest(rsp_ilu0_info_t info, uint64_t *digest);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1048,8 +1048,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     };
     auto levels = [&](const rsp::LevelChunk &ch) {
         const int x0 = ch.x0, nl = ch.l1 - ch.l0;
+#if RSP_THIN_LONG_READLANE
         auto vat = [&](int k) { return lval[k / G].v[k % G]; };
         auto yat = [&](int k) { return yb(lidx[k / G].v[k % G]); };
+#endif
         for (int q = 0; q < nl;) {
             if (narrow(q)) {
                 const int qe = run_end(q, nl);

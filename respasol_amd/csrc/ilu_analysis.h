@@ -1,0 +1,123 @@
+// ilu_analysis.h — host half of the ILU(0) analysis (rsp_ilu0_analysis, the
+// reference's csrilu02_analysis + 2x csrsv2_analysis, GPU/ilu0.cu:196-252):
+// validation, diagonal positions, level sets of the L / L^T / U DAGs, the
+// symbolic factor (update lists, intra-row stages) and the launch plans of
+// the factor and the solves. Pure host C++ (no HIP calls): rsp_api.cpp
+// downloads the pattern, calls plan_host and uploads the result in one
+// arena; rsp_ilu0_analysis_host runs it on host arrays (tests, profiling).
+#ifndef RSP_ILU_ANALYSIS_H
+#define RSP_ILU_ANALYSIS_H
+
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <functional>
+#include <vector>
+
+#include "rsp.h"
+#include "rsp_kernels.h"
+
+namespace rsp_an {
+
+inline int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+struct SolvePlan {
+    std::vector<int> sbase;   // per level: first flat term of its padded short rows, -1 = none
+    std::vector<int> nshort;  // per level
+    std::vector<int> nwave;   // per level: short + wave rows (the rest: hub rows)
+    std::vector<rsp::RowTask> tasks;
+    std::vector<int> tpos, src;
+    std::vector<rsp::LevelSeg> segs;
+    std::vector<rsp::LevelChunk> chunks;
+    std::vector<rsp::ThinRowPlan> trow;
+    std::vector<int> sid;
+    std::vector<rsp::StagedTerm> stg;
+};
+
+// Symbolic ILU(0) data (built by ilu_symbolic below).
+struct IluSymbolic {
+    std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
+    std::vector<int> stage;  // per lower position: its intra-row stage
+};
+
+struct FacPlan {
+    std::vector<rsp::LevelSeg> segs;
+    std::vector<rsp::RndChunk> chunks;
+    std::vector<rsp::RndItem> items;
+    std::vector<int> pairs, staged, rounds;
+};
+
+// One DAG's levels and solve plan.
+struct DagHost {
+    std::vector<int> ptr, rows;  // level pointers, rows in level order
+    SolvePlan sp;
+    int batch = 8, group = 4;
+    bool planned = false;
+};
+
+// Everything the analysis computes on the host.
+struct IluHostPlan {
+    int n = 0, nnz_s = 0, structural_zero = -1;
+    std::vector<int> dpos, hasdiag, udiv;
+    IluSymbolic sym;
+    DagHost L, LT, U;
+    // transposed strict lower part (row k: (position of l_jk, j), j descending)
+    std::vector<int> ltp, lts, ltc;
+    FacPlan fplan;
+    int fac_batch = 8;
+    std::vector<rsp::FacRow> frow;
+    // fat factor levels in the slot layout: per L level (stride 0: FacRow
+    // path), the rows to write (desc) and their offsets, total ints
+    std::vector<rsp::FacSlotLevel> fslev;
+    std::vector<int4> slot_desc;
+    std::vector<long long> slot_offs;
+    long long slot_total = 0;
+};
+
+// Phase timer (RSP_ILU_TIMING=1 prints; phase_ms collects when given).
+struct Phases {
+    bool print = false;
+    int n = 0;
+    double *ms = nullptr;  // [kPhases]
+    int next = 0;
+    void mark(const char *what);
+    void start();
+    double t_last = 0.0;
+};
+constexpr int kPhases = 6;  // phase slots of Phases::ms (marks in call order)
+
+// The host analysis in phases (rsp_ilu0_analysis runs validate and symbolic
+// on the GPU instead, and fills hp.dpos / hasdiag / structural_zero / sym
+// from there):
+//   plan_validate: pattern checks, diagonal positions, structural zero;
+//   plan_levels:   level sets of L and L^T, the transposed L (sequential);
+//   plan_symbolic: update lists, stages, stage order, divisor positions;
+//   plan_rest:     factor and solve plans, FacRow records, slot layout
+//                  (needs sym.upd_ptr / upd_l / upd_u / stage).
+rsp_status_t plan_validate(int n, const int *rp, const int *ci, IluHostPlan &hp);
+void plan_levels(const int *rp, const int *ci, IluHostPlan &hp);
+rsp_status_t plan_symbolic(const int *rp, const int *ci, IluHostPlan &hp);
+void plan_rest(const int *rp, const int *ci, long long slot_cap, bool want_u, IluHostPlan &hp);
+// The symbolic factor of the given rows on the host (the device analysis'
+// long rows): counts when cnt != nullptr, else pairs at ptr + stages, stage
+// order, divisor positions (arrays indexed by position).
+void symbolic_rows(const std::vector<int> &rows, int n, const int *rp, const int *ci, const int *dpos,
+                   const int *hasdiag, int *cnt, const int *ptr, int *upd_l, int *upd_u, int *stage, int *lord,
+                   int *lend, int *udiv);
+// All of it. rp / ci: base 0, rp[n] stored entries. slot_cap_ints:
+// budget of the fat-level slot layout. The U DAG plan (the --true-lu
+// extension) is built only when want_u. Returns INVALID_VALUE for a malformed
+// or unsorted pattern, ALLOC_FAILED if the update lists overflow int.
+rsp_status_t plan_host(int n, const int *rp, const int *ci, long long slot_cap_ints, bool want_u,
+                       IluHostPlan &hp, Phases &ph);
+// Build the U DAG's levels and solve plan (lazily, on first use).
+void plan_u(const int *rp, const int *ci, IluHostPlan &hp);
+// 64-bit digest (FNV-1a) of every array of the plan (tests: identical plans).
+uint64_t digest(const IluHostPlan &hp);
+
+}  // namespace rsp_an
+
+#endif

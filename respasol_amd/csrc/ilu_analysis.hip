@@ -1,0 +1,314 @@
+// ilu_analysis.hip — the data-parallel half of the ILU(0) analysis on the
+// MI355X (rsp_ilu0_analysis; the reference's csrilu02_analysis,
+// GPU/ilu0.cu:196-217): pattern validation, diagonal positions, the
+// structural-zero min-reduce, and the symbolic factor (every position's
+// update list, the intra-row stages, the stage order of each row's lower
+// positions, the divisor positions). What stays on the host (ilu_analysis.cpp)
+// is what is sequential along the dependency chains: the level sets (a row's
+// level needs its producers' levels: longest paths of the DAG, one O(nnz)
+// pass) and the greedy chunking of the launch plans.
+//
+// Update lists: position t = (i, j) receives the pair (p = (i, k), q = (k, j))
+// for every lower position p of row i with k < j and j in row k's upper part,
+// in ascending k — the same lists, in the same order, as the host's
+// ilu_symbolic (count pass, exclusive scan, fill pass over the identical
+// traversal; see an_pairs). Bitwise-equal plans are asserted through
+// rsp_ilu0_plan_digest against rsp_ilu0_analysis_host.
+//
+// Integer work (HBM/latency-bound, no MFMA). Compiled once (no FTZ variant).
+
+#include <hip/hip_runtime.h>
+#include <limits.h>
+
+#include <algorithm>
+
+#include "rsp_kernels.h"
+
+namespace rsp_k {
+
+namespace {
+
+constexpr int kAnThreads = 256;
+
+// first position in [lo, hi) of ci with ci >= v (rows are sorted)
+__device__ __forceinline__ int lower_bound_dev(const int *__restrict__ ci, int lo, int hi, int v) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ci[mid] < v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// Validation + diagonal positions + structural zero, one thread per row.
+// flags[0] |= 1 for a column out of range or a row not strictly increasing;
+// flags[1] = min row without a diagonal (INT_MAX = none).
+__global__ __launch_bounds__(kAnThreads) void an_rows(int n, const int *__restrict__ rp,
+                                                       const int *__restrict__ ci, int *__restrict__ dpos,
+                                                       int *__restrict__ hasdiag, int *__restrict__ flags) {
+    const int i = blockIdx.x * kAnThreads + threadIdx.x;
+    if (i >= n) return;
+    const int rs = rp[i], re = rp[i + 1];
+    bool bad = false;
+    int prev = -1;
+    for (int p = rs; p < re; p++) {
+        const int c = ci[p];
+        bad |= c < 0 || c >= n || c <= prev;
+        prev = c;
+    }
+    if (bad) {
+        atomicOr(flags, 1);
+        dpos[i] = rs;
+        hasdiag[i] = 0;
+        return;
+    }
+    const int d = lower_bound_dev(ci, rs, re, i);
+    const int hd = (d < re && ci[d] == i) ? 1 : 0;
+    dpos[i] = d;
+    hasdiag[i] = hd;
+    if (!hd) atomicMin(flags + 1, i);
+}
+
+// Update lists, push form, one wave (64-thread workgroup) per row i of a
+// length class: for each lower position p = (i, k) in ascending order, the
+// lanes take row k's upper entries q (columns > k, 64 at a time), find each
+// column in row i after p (binary search: rows are sorted) and, on a hit at
+// t, count (FILL = 0) or append (p, q) to t's list (FILL = 1). A row's
+// per-position counters / cursors live in LDS (LDS_CAP entries; the wave's
+// LDS accesses are in order, and the lanes of one step hit distinct columns),
+// so every list comes out in ascending k, exactly as the host's ilu_symbolic.
+// Rows longer than any LDS class (LDS_CAP = 0) use global cursors advanced by
+// atomics, each step waited for before the next.
+template <bool FILL, int LDS_CAP>
+__global__ __launch_bounds__(64) void an_pairs(const int *__restrict__ rows, const int *__restrict__ rp,
+                                               const int *__restrict__ ci, const int *__restrict__ dpos,
+                                               const int *__restrict__ hasdiag, int *__restrict__ cnt_or_ptr,
+                                               int *__restrict__ gcur, int *__restrict__ upd_l,
+                                               int *__restrict__ upd_u) {
+    __shared__ int c[LDS_CAP > 0 ? LDS_CAP : 1];
+    const int lane = threadIdx.x;
+    const int i = rows[blockIdx.x];
+    const int rs = rp[i], re = rp[i + 1], di = dpos[i];
+    int *cur = LDS_CAP > 0 ? c - rs : gcur;  // indexed by position
+    for (int t = rs + lane; t < re; t += 64) cur[t] = FILL ? cnt_or_ptr[t] : 0;
+    __syncthreads();
+    for (int p = rs; p < di; p++) {
+        const int k = ci[p];
+        const int q1 = rp[k + 1];
+        for (int qb = dpos[k] + hasdiag[k]; qb < q1; qb += 64) {
+            const int q = qb + lane;
+            if (q < q1) {
+                const int col = ci[q];
+                const int t = lower_bound_dev(ci, p + 1, re, col);
+                if (t < re && ci[t] == col) {
+                    if (LDS_CAP > 0) {
+                        const int m = cur[t];
+                        cur[t] = m + 1;
+                        if (FILL) {
+                            upd_l[m] = p;
+                            upd_u[m] = q;
+                        }
+                    } else {
+                        const int m = atomicAdd(cur + t, 1);
+                        if (FILL) {
+                            upd_l[m] = p;
+                            upd_u[m] = q;
+                        }
+                    }
+                }
+            }
+            if (LDS_CAP == 0) __builtin_amdgcn_s_waitcnt(0);  // this step's atomics before the next's
+        }
+    }
+    __syncthreads();
+    if (!FILL)
+        for (int t = rs + lane; t < re; t += 64) cnt_or_ptr[t] = cur[t];
+}
+
+// Per row (one thread): intra-row stages of the lower positions (stage(t) =
+// 1 + max stage of the l_ik its pairs read, 0 without pairs; positions in
+// ascending order, so every read stage is final), the stable order of the
+// lower positions by stage (lord; counting sort through `scratch`, which
+// holds one counter per lower position), and lend (end of each position's
+// stage group in lord order). Divisor positions of the lower entries (udiv).
+__global__ __launch_bounds__(kAnThreads) void an_stages(int n, int maxlen, const int *__restrict__ rp,
+                                                         const int *__restrict__ ci,
+                                                         const int *__restrict__ dpos,
+                                                         const int *__restrict__ hasdiag,
+                                                         const int *__restrict__ ptr,
+                                                         const int *__restrict__ upd_l, int *__restrict__ stage,
+                                                         int *__restrict__ lord, int *__restrict__ lend,
+                                                         int *__restrict__ udiv, int *__restrict__ scratch) {
+    const int i = blockIdx.x * kAnThreads + threadIdx.x;
+    if (i >= n) return;
+    const int rs = rp[i], di = dpos[i], re = rp[i + 1];
+    if (re - rs > maxlen) return;  // done on the host
+    int smax = -1;
+    for (int t = rs; t < di; t++) {
+        int s = 0;
+        for (int u = ptr[t]; u < ptr[t + 1]; u++) s = max(s, stage[upd_l[u]] + 1);
+        stage[t] = s;
+        smax = max(smax, s);
+        const int k = ci[t];
+        udiv[t] = hasdiag[k] ? dpos[k] : -1;
+        scratch[t] = 0;
+    }
+    for (int t = di; t < re; t++) {
+        stage[t] = 0;
+        udiv[t] = -1;
+        lord[t] = 0;
+        lend[t] = 0;
+    }
+    if (di == rs) return;
+    // counting sort by stage (stage < di - rs): counters at scratch[rs + s]
+    for (int t = rs; t < di; t++) scratch[rs + stage[t]]++;
+    int run = 0;
+    for (int s = 0; s <= smax; s++) {
+        const int c = scratch[rs + s];
+        scratch[rs + s] = run;
+        run += c;
+    }
+    for (int t = rs; t < di; t++) lord[rs + scratch[rs + stage[t]]++] = t;
+    for (int x = di - rs - 1; x >= 0; x--) {
+        const bool last = x == di - rs - 1 || stage[lord[rs + x]] != stage[lord[rs + x + 1]];
+        lend[rs + x] = last ? rs + x + 1 : lend[rs + x + 1];
+    }
+}
+
+inline unsigned grid_of(long long count) { return (unsigned)((count + kAnThreads - 1) / kAnThreads); }
+
+}  // namespace
+
+hipError_t ilu_an_rows(int n, const int *rp, const int *ci, int *dpos, int *hasdiag, int *flags,
+                       hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    an_rows<<<grid_of(n), kAnThreads, 0, s>>>(n, rp, ci, dpos, hasdiag, flags);
+    return hipGetLastError();
+}
+
+// Row length classes of the pair kernels: <= 1024 entries (4 KB of LDS per
+// wave), <= 16384 (64 KB), longer (global cursors). rows_c*: the rows of each
+// class (device), counts n_c*.
+template <bool FILL>
+static hipError_t an_pairs_launch(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+                                  const int *dpos, const int *hasdiag, int *cnt_or_ptr, int *gcur, int *upd_l,
+                                  int *upd_u, hipStream_t s) {
+    if (n_c[0] > 0)
+        an_pairs<FILL, 1024><<<n_c[0], 64, 0, s>>>(rows_c[0], rp, ci, dpos, hasdiag, cnt_or_ptr, gcur, upd_l, upd_u);
+    if (n_c[1] > 0)
+        an_pairs<FILL, 16384><<<n_c[1], 64, 0, s>>>(rows_c[1], rp, ci, dpos, hasdiag, cnt_or_ptr, gcur, upd_l, upd_u);
+    if (n_c[2] > 0)
+        an_pairs<FILL, 0><<<n_c[2], 64, 0, s>>>(rows_c[2], rp, ci, dpos, hasdiag, cnt_or_ptr, gcur, upd_l, upd_u);
+    return hipGetLastError();
+}
+
+hipError_t ilu_an_count(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+                        const int *dpos, const int *hasdiag, int *cnt, int *gcur, hipStream_t s) {
+    return an_pairs_launch<false>(rows_c, n_c, rp, ci, dpos, hasdiag, cnt, gcur, nullptr, nullptr, s);
+}
+
+// Exclusive prefix sum of `count` ints (cnt -> ptr) in three passes: block
+// sums (1024 elements per 256-thread block), a one-block scan of those, then
+// each block's local scan plus its offset. temp holds the block sums; with
+// temp == nullptr only *temp_bytes is set.
+namespace {
+constexpr int kScanPer = 1024;  // elements per block (4 per thread)
+
+__device__ __forceinline__ int block_excl_scan(int v, int *lds, int *total) {
+    // inclusive scan over 256 threads in LDS (Hillis-Steele), returns exclusive
+    const int t = threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        const int a = t >= d ? lds[t - d] : 0;
+        __syncthreads();
+        lds[t] += a;
+        __syncthreads();
+    }
+    const int incl = lds[t];
+    if (total) *total = lds[255];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(256) void scan_sums(const int *__restrict__ in, int count, int *__restrict__ sums) {
+    __shared__ int lds[256];
+    const int base = blockIdx.x * kScanPer + threadIdx.x * 4;
+    int v = 0;
+    for (int j = 0; j < 4; j++) v += base + j < count ? in[base + j] : 0;
+    int tot;
+    block_excl_scan(v, lds, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// one block scans the (<= 256 * 1024) block sums in place, exclusive
+__global__ __launch_bounds__(256) void scan_top(int *__restrict__ sums, int nb) {
+    __shared__ int lds[256];
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += 256 * 4) {
+        const int base = b0 + threadIdx.x * 4;
+        int v[4], loc = 0;
+        for (int j = 0; j < 4; j++) {
+            v[j] = base + j < nb ? sums[base + j] : 0;
+            loc += v[j];
+        }
+        int tot;
+        int ex = block_excl_scan(loc, lds, &tot) + carry;
+        for (int j = 0; j < 4; j++) {
+            if (base + j < nb) sums[base + j] = ex;
+            ex += v[j];
+        }
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void scan_apply(const int *__restrict__ in, int count,
+                                                  const int *__restrict__ sums, int *__restrict__ out) {
+    __shared__ int lds[256];
+    const int base = blockIdx.x * kScanPer + threadIdx.x * 4;
+    int v[4], loc = 0;
+    for (int j = 0; j < 4; j++) {
+        v[j] = base + j < count ? in[base + j] : 0;
+        loc += v[j];
+    }
+    int ex = block_excl_scan(loc, lds, nullptr) + sums[blockIdx.x];
+    for (int j = 0; j < 4; j++) {
+        if (base + j < count) out[base + j] = ex;
+        ex += v[j];
+    }
+}
+}  // namespace
+
+hipError_t ilu_an_scan(const int *cnt, int *ptr, int count, void *temp, size_t *temp_bytes, hipStream_t s) {
+    const int nb = (count + kScanPer - 1) / kScanPer;
+    if (!temp) {
+        *temp_bytes = (size_t)std::max(nb, 1) * sizeof(int);
+        return hipSuccess;
+    }
+    if (count <= 0) return hipSuccess;
+    int *sums = (int *)temp;
+    scan_sums<<<nb, 256, 0, s>>>(cnt, count, sums);
+    scan_top<<<1, 256, 0, s>>>(sums, nb);
+    scan_apply<<<nb, 256, 0, s>>>(cnt, count, sums, ptr);
+    return hipGetLastError();
+}
+
+hipError_t ilu_an_fill(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+                       const int *dpos, const int *hasdiag, const int *ptr, int *gcur, int *upd_l, int *upd_u,
+                       hipStream_t s) {
+    return an_pairs_launch<true>(rows_c, n_c, rp, ci, dpos, hasdiag, const_cast<int *>(ptr), gcur, upd_l, upd_u,
+                                 s);
+}
+
+hipError_t ilu_an_stages(int n, int maxlen, const int *rp, const int *ci, const int *dpos, const int *hasdiag,
+                         const int *ptr, const int *upd_l, int *stage, int *lord, int *lend, int *udiv,
+                         int *scratch, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    an_stages<<<grid_of(n), kAnThreads, 0, s>>>(n, maxlen, rp, ci, dpos, hasdiag, ptr, upd_l, stage, lord, lend,
+                                                udiv, scratch);
+    return hipGetLastError();
+}
+
+}  // namespace rsp_k

@@ -23,6 +23,9 @@
 #include <vector>
 
 #include "rsp_kernels.h"
+#include "ilu_analysis.h"
+
+using rsp_an::env_int;
 
 using rsp::SpmvBlock;
 using rsp::SpmvLongRow;
@@ -112,6 +115,14 @@ struct rsp_ilu0_info {
     std::vector<rsp::FacSlotLevel> fslev;      // per L level (stride 0: FacRow path)
     int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
     int fac_batch;
+    void *d_arena = nullptr;    // one allocation holding the analysis' arrays (Arena)
+    void *d_arena_u = nullptr;  // the U plan's (built on first use)
+    void *d_arena_sym = nullptr;    // device analysis: dpos, hasdiag, upd_ptr, lord, lend, udiv, scratch
+    void *d_arena_pairs = nullptr;  // device analysis: upd_l, upd_u
+    void *d_usval = nullptr;    // U solve term values (trsv_stream), in d_arena_u
+    unsigned long long digest = 0;  // rsp_an::digest of the host plan
+    std::unique_ptr<rsp_an::IluHostPlan> host;  // kept for the U plan
+    std::vector<int> host_rp, host_ci;
 };
 
 #define RSP_CHECK_HIP(call)                                                     \
@@ -933,33 +944,25 @@ rsp_status_t rsp_scatter(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, c
 /* --------------------------------------------------------------- ILU(0) */
 
 static void ilu_free_device(rsp_ilu0_info *f) {
-    int **ptrs[] = {&f->d_dpos,     &f->d_hasdiag, &f->L.d_rows,  &f->L.d_ptr,
-                    &f->LT.d_rows,  &f->LT.d_ptr,  &f->U.d_rows,  &f->U.d_ptr,
-                    &f->d_zero,
-                    &f->d_upd_ptr,  &f->d_upd_l,   &f->d_upd_u,   &f->d_lord,
-                    &f->d_lend,     &f->d_udiv};
-    for (int **p : ptrs) {
-        if (*p) (void)hipFree(*p);
-        *p = nullptr;
-    }
-    for (void **p : {&f->d_sval, &f->d_sx, &f->d_sdg}) {
-        if (*p) (void)hipFree(*p);
-        *p = nullptr;
-    }
+    // every array except the slot layout lives in the arenas
+    if (f->d_arena) (void)hipFree(f->d_arena);
+    if (f->d_arena_u) (void)hipFree(f->d_arena_u);
+    if (f->d_arena_sym) (void)hipFree(f->d_arena_sym);
+    if (f->d_arena_pairs) (void)hipFree(f->d_arena_pairs);
+    f->d_arena_sym = f->d_arena_pairs = nullptr;
+    if (f->d_fslots) (void)hipFree(f->d_fslots);
+    f->d_arena = f->d_arena_u = nullptr;
+    f->d_usval = nullptr;
+    f->d_fslots = nullptr;
+    f->d_dpos = f->d_hasdiag = f->d_zero = nullptr;
+    f->d_upd_ptr = f->d_upd_l = f->d_upd_u = f->d_lord = f->d_lend = f->d_udiv = nullptr;
+    f->d_sval = f->d_sx = f->d_sdg = nullptr;
     f->fslev.clear();
-    for (void **p : {(void **)&f->d_frow, (void **)&f->d_fslots, (void **)&f->d_rchunks, (void **)&f->d_ritems,
-                     (void **)&f->d_rpairs, (void **)&f->d_rstaged, (void **)&f->d_rrounds}) {
-        if (*p) (void)hipFree(*p);
-        *p = nullptr;
-    }
-    for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) {
-        for (void **p : {(void **)&d->d_tasks, (void **)&d->d_tpos, (void **)&d->d_src,
-                         (void **)&d->d_chunks, (void **)&d->d_nshort, (void **)&d->d_trow,
-                         (void **)&d->d_sid, (void **)&d->d_stg}) {
-            if (*p) (void)hipFree(*p);
-            *p = nullptr;
-        }
-    }
+    f->d_frow = nullptr;
+    f->d_rchunks = nullptr;
+    f->d_ritems = nullptr;
+    f->d_rpairs = f->d_rstaged = f->d_rrounds = nullptr;
+    for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) *d = rsp_ilu0_info::Dag();
 }
 
 rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
@@ -993,226 +996,9 @@ rsp_status_t rsp_ilu0_buffer_size(rsp_handle_t h, int n, int nnz, rsp_datatype_t
     return RSP_STATUS_SUCCESS;
 }
 
-// rows grouped by level (stable: ascending row within a level)
-static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int> &ptr,
-                         std::vector<int> &rows) {
-    ptr.assign((size_t)nlev + 1, 0);
-    for (int v : lev) ptr[(size_t)v + 1]++;
-    for (int l = 0; l < nlev; l++) ptr[(size_t)l + 1] += ptr[(size_t)l];
-    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
-    rows.assign(lev.size(), 0);
-    for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
-}
+}  // extern "C"
 
-
-static const int kThinThreadsHost = rsp::kThinThreads;
-
-static int env_int(const char *name, int dflt) {
-    const char *v = getenv(name);
-    return (v && *v) ? atoi(v) : dflt;
-}
-
-// fma-chain batch for a mean chain length of total / count
-static int chain_batch(long long total, long long count) {
-    const double mean = count > 0 ? (double)total / (double)count : 0.0;
-    return mean <= 2.5 ? 2 : (mean <= 5.0 ? 4 : 8);
-}
-
-}  // extern "C" (C++ helpers)
-
-// Solve plan of one DAG (see LevelPlan): tasks in level order over flat
-// terms (term k of row i: matrix value at tpos[k], y of column col_of(k)),
-// segments (a level is thin if it has <= thin_rows rows and its terms fit one
-// chunk), the LDS-staged chunks of every thin run (<= kChunkRows rows and
-// <= kChunkTerms terms each), and the y source of every term of a thin run:
-// the LDS window slot (run index mod kYWin) if the column was produced earlier
-// in the run and no later row of the run can have reused that slot by the end
-// of the consumer's level, else the column (global y, or its value staged at
-// the chunk start — the producer is then in an earlier chunk or before the
-// run, so its store is visible after the chunk's full barrier).
-struct SolvePlan {
-    std::vector<int> sbase;   // per level: first flat term of its padded short rows, -1 = none
-    std::vector<int> nshort;  // per level
-    std::vector<int> nwave;   // per level: short + wave rows (the rest: hub rows)
-    std::vector<rsp::RowTask> tasks;
-    std::vector<int> tpos, src;
-    std::vector<rsp::LevelSeg> segs;
-    std::vector<rsp::LevelChunk> chunks;
-    std::vector<rsp::ThinRowPlan> trow;
-    std::vector<int> sid;
-    std::vector<rsp::StagedTerm> stg;
-};
-
-// row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
-template <typename RowTerms>
-static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
-                             int thin_rows, int group, const std::vector<int> &diag,
-                             RowTerms row_terms, SolvePlan &sp) {
-    const int nlev = (int)ptr.size() - 1;
-    std::vector<int> order(rows);
-    // segments: runs of thin levels / fat levels. A thin level's rows have
-    // their terms padded to whole groups of `group` (at least one group):
-    // pads are (position -1, source kPadSrc), i.e. a zero value times the zero
-    // slot of the LDS y buffer — an exact no-op fma — so the thin kernel reads
-    // a row as whole groups with vector loads and no length tests.
-    auto nterms = [&](int i) {
-        int cnt = 0;
-        row_terms(i, [&](int, int) { cnt++; });
-        return cnt;
-    };
-    auto padded = [&](int cnt) { return std::max(1, (cnt + group - 1) / group) * group; };
-    std::vector<int> lpad((size_t)std::max(nlev, 1), 0);
-    for (int l = 0; l < nlev; l++)
-        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) lpad[(size_t)l] += padded(nterms(order[(size_t)x]));
-    sp.segs.clear();
-    for (int l = 0; l < nlev; l++) {
-        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
-        const int thin = (cnt <= thin_rows && cnt <= rsp::kThinThreads && cnt <= rsp::kChunkRows &&
-                          lpad[(size_t)l] <= rsp::kChunkTerms) ? 1 : 0;
-        if (!sp.segs.empty() && sp.segs.back().thin == thin && sp.segs.back().le == l)
-            sp.segs.back().le = l + 1;
-        else
-            sp.segs.push_back({l, l + 1, thin, 0, 0, 0});
-    }
-    std::vector<char> thin_lev((size_t)std::max(nlev, 1), 0);
-    for (const rsp::LevelSeg &sg : sp.segs)
-        for (int l = sg.lb; l < sg.le; l++) thin_lev[(size_t)l] = (char)sg.thin;
-    // within each level: short rows first (a thread each), longer rows after
-    // them (a wave each). Short: <= kLongTerms terms in a thin run (LDS
-    // operands); <= kFatLongTerms in a fat level, where a thread pays one
-    // global round trip per batch of terms and a wave one per 64 terms.
-    // A fat level's rows of > kHubTerms terms come last, a workgroup each.
-    const int fat_long = env_int("RSP_ILU_FAT_LONG", rsp::kFatLongTerms);
-    const int hub = env_int("RSP_ILU_HUB", rsp::kHubTerms);
-    sp.nshort.assign((size_t)std::max(nlev, 1), 0);
-    sp.nwave.assign((size_t)std::max(nlev, 1), 0);
-    for (int l = 0; l < nlev; l++) {
-        const int lim = thin_lev[(size_t)l] ? rsp::kLongTerms : fat_long;
-        auto b = order.begin() + ptr[(size_t)l], e = order.begin() + ptr[(size_t)l + 1];
-        auto mid = std::stable_partition(b, e, [&](int i) { return nterms(i) <= lim; });
-        sp.nshort[(size_t)l] = (int)(mid - b);
-        auto hb = thin_lev[(size_t)l] ? e : std::stable_partition(mid, e, [&](int i) { return nterms(i) <= hub; });
-        sp.nwave[(size_t)l] = (int)(hb - b);
-    }
-    std::vector<int> col;
-    sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
-    sp.tpos.clear();
-    // fat levels: each short row owns kFatLongTerms flat terms (its terms,
-    // then pads), so trsv_level finds a row's terms at sbase + r * 8 without
-    // reading its task first; t1 stays at the row's last real term
-    const bool pad_fat = fat_long == rsp::kFatLongTerms && env_int("RSP_ILU_FAT_PAD", 1) != 0;
-    sp.sbase.assign((size_t)std::max(nlev, 1), -1);
-    for (int l = 0; l < nlev; l++) {
-        const bool padl = pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0;
-        if (padl) sp.sbase[(size_t)l] = (int)sp.tpos.size();
-        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-            const int i = order[(size_t)x];
-            rsp::RowTask &t = sp.tasks[(size_t)x];
-            t.i = i;
-            t.t0 = (int)sp.tpos.size();
-            row_terms(i, [&](int tp, int c) {
-                sp.tpos.push_back(tp);
-                col.push_back(c);
-            });
-            if (thin_lev[(size_t)l])
-                while ((int)sp.tpos.size() - t.t0 < padded((int)sp.tpos.size() - t.t0)) {
-                    sp.tpos.push_back(-1);
-                    col.push_back(-1);
-                }
-            t.t1 = (int)sp.tpos.size();
-            if (padl && x - ptr[(size_t)l] < sp.nshort[(size_t)l])
-                while ((int)sp.tpos.size() - t.t0 < rsp::kFatLongTerms) {
-                    sp.tpos.push_back(-1);
-                    col.push_back(-1);
-                }
-            t.d = diag.empty() ? -1 : diag[(size_t)i];
-        }
-    }
-    std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
-    for (int l = 0; l < nlev; l++)
-        if (ptr[(size_t)l + 1] > ptr[(size_t)l])
-            lterms[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l + 1] - 1].t1 - sp.tasks[(size_t)ptr[(size_t)l]].t0;
-    sp.src = col;
-    for (size_t k = 0; k < col.size(); k++)
-        if (col[k] < 0) sp.src[k] = rsp::kPadSrc;
-    for (rsp::LevelSeg &sg : sp.segs)
-        if (sg.thin) sg.nth = rsp::kThinThreads;
-    // chunks of the thin runs + term sources
-    std::vector<int> slot_of((size_t)n, -1);
-    for (size_t x = 0; x < order.size(); x++) slot_of[(size_t)order[x]] = (int)x;
-    sp.chunks.clear();
-    for (rsp::LevelSeg &sg : sp.segs) {
-        if (!sg.thin) continue;
-        sg.c0 = (int)sp.chunks.size();
-        int crow = 0, cterm = 0;
-        for (int l = sg.lb; l < sg.le; l++) {
-            const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
-            if (sp.chunks.size() == (size_t)sg.c0 || crow + cnt > rsp::kChunkRows ||
-                cterm + lterms[(size_t)l] > rsp::kChunkTerms) {
-                sp.chunks.push_back({l, l + 1, 0, 0, 0, 0, 0, 0});
-                crow = 0;
-                cterm = 0;
-            } else {
-                sp.chunks.back().l1 = l + 1;
-            }
-            crow += cnt;
-            cterm += lterms[(size_t)l];
-        }
-        sg.c1 = (int)sp.chunks.size();
-        const int base = ptr[(size_t)sg.lb];
-        for (int l = sg.lb; l < sg.le; l++) {
-            const int r_end = ptr[(size_t)l + 1] - base;
-            for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++)
-                for (int k = sp.tasks[(size_t)x].t0; k < sp.tasks[(size_t)x].t1; k++) {
-                    if (col[(size_t)k] < 0) continue;  // pad
-                    const int sj = slot_of[(size_t)col[(size_t)k]];
-                    if (sj < base || sj >= ptr[(size_t)l]) continue;  // before the run
-                    const int rj = sj - base;
-                    if (r_end - rj <= rsp::kYWin) sp.src[(size_t)k] = -((rj & (rsp::kYWin - 1)) + 1);
-                }
-        }
-    }
-    if (sp.tpos.empty()) {  // keep the device arrays non-empty
-        sp.tpos.push_back(0);
-        sp.src.push_back(0);
-    }
-    // per chunk: slot and term ranges, the static row records (first group,
-    // y window slot), each term's y index in the LDS y buffer (window slot,
-    // the zero slot for pads, or its staged slot) and the staged terms
-    sp.trow.assign(std::max<size_t>(rows.size(), 1), rsp::ThinRowPlan{0, 0, 0, -1});
-    sp.sid.assign(sp.tpos.size(), rsp::kYWin);
-    sp.stg.clear();
-    for (const rsp::LevelSeg &sg : sp.segs) {
-        if (!sg.thin) continue;
-        const int base = ptr[(size_t)sg.lb];
-        for (int c = sg.c0; c < sg.c1; c++) {
-            rsp::LevelChunk &ch = sp.chunks[(size_t)c];
-            ch.x0 = ptr[(size_t)ch.l0];
-            ch.x1 = ptr[(size_t)ch.l1];
-            ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
-            ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
-            ch.st0 = (int)sp.stg.size();
-            for (int x = ch.x0; x < ch.x1; x++) {
-                const rsp::RowTask &t = sp.tasks[(size_t)x];
-                sp.trow[(size_t)x] = {(t.t0 - ch.k0) / group | ((t.t1 - t.t0) / group) << 16,
-                                      (x - base) & (rsp::kYWin - 1), t.i, t.d};
-                for (int k = t.t0; k < t.t1; k++) {
-                    const int sc = sp.src[(size_t)k];
-                    if (sc < 0) {
-                        sp.sid[(size_t)k] = -sc - 1;  // window slot, or the zero slot for a pad
-                    } else {
-                        sp.sid[(size_t)k] = rsp::kYWin + 1 + (k - ch.k0);
-                        sp.stg.push_back({k - ch.k0, sc});
-                    }
-                }
-            }
-            ch.st1 = (int)sp.stg.size();
-        }
-    }
-    if (sp.stg.empty()) sp.stg.push_back({0, 0});
-    if (sp.chunks.empty()) sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
-}
-
+// Device helpers of the ILU analysis upload.
 template <typename V>
 static hipError_t upload_vec(V **dst, const std::vector<V> &v) {
     size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(V);
@@ -1222,317 +1008,210 @@ static hipError_t upload_vec(V **dst, const std::vector<V> &v) {
     return e;
 }
 
-// Symbolic ILU(0) data (built by ilu_symbolic below).
-struct IluSymbolic {
-    std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
-    std::vector<int> stage;  // per lower position: its intra-row stage
-};
-
-// Factor plan of the L DAG (see IluArgs): segments (a level is thin if it
-// has <= thin_rows rows and its positions / update pairs fit one chunk), the
-// LDS-staged chunks of every thin run, and per chunk its items (the positions
-// of its rows: lower ones in intra-row stage order, then upper ones) and update
-// pairs with their sources: a chunk-local item when the producing row is in
-// the chunk, else the position (its final value is staged at the chunk start).
-// Factor plan of the L DAG (see IluArgs): segments (fat levels: one launch
-// each; thin levels: one single-workgroup launch per run) and, for the thin
-// runs, ROUNDS: a level's positions ("items") grouped so that a round's items
-// are independent — a lower item of intra-row stage s is in round s, a row's
-// upper items (diagonal included) in the round after its last lower stage.
-// Every item depends only on earlier rounds (its own row's l_ik) and earlier
-// levels (u_kj, u_kk). The run's items, in round order, are cut into LDS
-// chunks (<= kRndItems items, kRndPairs update pairs, kRndStaged staged
-// values, kRndRounds rounds; a round may be split between chunks). An item's
-// operands are indices into the kernel's LDS value buffer by class: its own
-// chunk's slots, the previous chunk's slots (kept in the other LDS buffer),
-// values staged from vals at the chunk start (producers two or more chunks
-// back, or before the run), or the zero slot (a missing u_kk).
-struct FacPlan {
-    std::vector<rsp::LevelSeg> segs;
-    std::vector<rsp::RndChunk> chunks;
-    std::vector<rsp::RndItem> items;
-    std::vector<int> pairs, staged, rounds;
-};
-
-static void build_factor_plan(int n, const std::vector<int> &rp, const std::vector<int> &ci,
-                              const std::vector<int> &dpos, const std::vector<int> &hasdiag,
-                              const IluSymbolic &sym, const std::vector<int> &ptr,
-                              const std::vector<int> &rows, int thin_rows, FacPlan &fp) {
-    const int nlev = (int)ptr.size() - 1;
-    const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
-    const int thin_items = env_int("RSP_ILU_THIN_FACTOR_ITEMS", rsp::kRndLevelItems);
-    auto npairs = [&](int p) { return sym.upd_ptr[(size_t)p + 1] - sym.upd_ptr[(size_t)p]; };
-    fp.segs.clear();
-    for (int l = 0; l < nlev; l++) {
-        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
-        long long items = 0;
-        int maxp = 0;
-        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-            const int i = rows[(size_t)x];
-            items += rp[(size_t)i + 1] - rp[(size_t)i];
-            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) maxp = std::max(maxp, npairs(p));
-        }
-        const int thin = (cnt <= thin_rows && items <= thin_items && maxp <= rsp::kRndItemPairs) ? 1 : 0;
-        if (!fp.segs.empty() && fp.segs.back().thin == thin && fp.segs.back().le == l)
-            fp.segs.back().le = l + 1;
-        else
-            fp.segs.push_back({l, l + 1, thin, 0, 0, kThinThreadsHost});
-    }
-    fp.chunks.clear();
-    fp.items.clear();
-    fp.pairs.clear();
-    fp.staged.clear();
-    fp.rounds.clear();
-    // where each position was placed: chunk and slot (-1: not in this run yet)
-    std::vector<int> pchunk((size_t)rp[(size_t)n], -1), pslot((size_t)rp[(size_t)n], 0);
-    std::vector<int> stg_of((size_t)rp[(size_t)n], -1);  // staged slot in the current chunk
-    std::vector<int> stg_list;                            // positions staged in the current chunk
-    struct RItem {
-        int round, pos, row;
+// Many arrays in ONE device allocation: add() records each array (host data
+// to copy, or space only), commit() makes one hipMalloc and one copy per
+// array. (One allocation per array — ~40 per analysis — had cost more than
+// the copies themselves.)
+struct Arena {
+    struct Item {
+        void **dst;
+        const void *src;
+        size_t bytes, copy, off;
     };
-    std::vector<RItem> ritems;  // a level's items
-    for (rsp::LevelSeg &sg : fp.segs) {
-        if (!sg.thin) continue;
-        sg.c0 = (int)fp.chunks.size();
-        rsp::RndChunk ch{};
-        int c = -1;  // current chunk id
-        auto open_chunk = [&]() {
-            for (int q : stg_list) stg_of[(size_t)q] = -1;
-            stg_list.clear();
-            c = (int)fp.chunks.size();
-            ch = rsp::RndChunk{(int)fp.items.size(), (int)fp.items.size(), (int)fp.pairs.size(),
-                               (int)fp.pairs.size(), (int)fp.staged.size(), (int)fp.staged.size(),
-                               (int)fp.rounds.size(), (int)fp.rounds.size()};
-            fp.chunks.push_back(ch);
-        };
-        auto close_chunk = [&]() {
-            ch.i1 = (int)fp.items.size();
-            ch.p1 = (int)fp.pairs.size();
-            ch.s1 = (int)fp.staged.size();
-            ch.r1 = (int)fp.rounds.size();
-            fp.chunks[(size_t)c] = ch;
-        };
-        // operand class index of position q for an item of chunk c (new staged
-        // values are appended to `fresh`; the caller commits or rolls back)
-        auto ref = [&](int q, std::vector<int> &fresh) {
-            const int qc = pchunk[(size_t)q];
-            if (qc == c) return pslot[(size_t)q];
-            if (qc >= 0 && qc == c - 1) return K + pslot[(size_t)q];
-            if (stg_of[(size_t)q] >= 0) return 2 * K + stg_of[(size_t)q];
-            for (size_t f = 0; f < fresh.size(); f++)
-                if (fresh[f] == q) return 2 * K + (int)(stg_list.size() + f);
-            fresh.push_back(q);
-            return 2 * K + (int)(stg_list.size() + fresh.size() - 1);
-        };
-        open_chunk();
-        long long last_round_key = -1;  // (level, round) of the chunk's last round
-        std::vector<int> fresh, ipairs;
-        for (int l = sg.lb; l < sg.le; l++) {
-            ritems.clear();
-            for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-                const int i = rows[(size_t)x], rs = rp[(size_t)i], di = dpos[(size_t)i];
-                int nst = 0;
-                for (int p = rs; p < di; p++) {
-                    ritems.push_back({sym.stage[(size_t)p], p, i});
-                    nst = std::max(nst, sym.stage[(size_t)p] + 1);
-                }
-                for (int p = di; p < rp[(size_t)i + 1]; p++) ritems.push_back({nst, p, i});
-            }
-            std::stable_sort(ritems.begin(), ritems.end(),
-                             [](const RItem &u, const RItem &v) { return u.round < v.round; });
-            for (const RItem &ri : ritems) {
-                const int p = ri.pos, i = ri.row;
-                const long long key = (long long)(l - sg.lb) * 1000000007LL + ri.round;
-                const bool lower = p < dpos[(size_t)i];
-                for (int attempt = 0; attempt < 2; attempt++) {
-                    fresh.clear();
-                    ipairs.clear();
-                    for (int u = sym.upd_ptr[(size_t)p]; u < sym.upd_ptr[(size_t)p + 1]; u++) {
-                        const int lc = ref(sym.upd_l[(size_t)u], fresh), uc = ref(sym.upd_u[(size_t)u], fresh);
-                        ipairs.push_back(lc | uc << 16);
-                    }
-                    int d = -1;
-                    if (lower) {
-                        const int k = ci[(size_t)p];
-                        d = hasdiag[(size_t)k] ? ref(dpos[(size_t)k], fresh) : kZero;
-                    }
-                    const int slot = (int)fp.items.size() - ch.i0;
-                    const bool new_round = key != last_round_key;
-                    const bool fits = slot < K && (int)(fp.pairs.size() - ch.p0 + ipairs.size()) <= rsp::kRndPairs &&
-                                      (int)(stg_list.size() + fresh.size()) <= S &&
-                                      (int)(fp.rounds.size() - ch.r0) + (new_round ? 1 : 0) <= rsp::kRndRounds;
-                    if (!fits && attempt == 0 && slot > 0) {  // next chunk (references re-resolved there)
-                        close_chunk();
-                        open_chunk();
-                        last_round_key = -1;
-                        continue;
-                    }
-                    // commit the item
-                    for (int q : fresh) {
-                        stg_of[(size_t)q] = (int)stg_list.size();
-                        stg_list.push_back(q);
-                        fp.staged.push_back(q);
-                    }
-                    if (new_round) {
-                        fp.rounds.push_back(slot);
-                        last_round_key = key;
-                    }
-                    const int pstart = (int)fp.pairs.size() - ch.p0;
-                    fp.pairs.insert(fp.pairs.end(), ipairs.begin(), ipairs.end());
-                    const int zr = (!lower && p == dpos[(size_t)i] && hasdiag[(size_t)i]) ? i : -1;
-                    fp.items.push_back({p, pstart | (int)ipairs.size() << 16, d, zr});
-                    pchunk[(size_t)p] = c;
-                    pslot[(size_t)p] = slot;
-                    break;
-                }
-            }
-        }
-        close_chunk();
-        sg.c1 = (int)fp.chunks.size();
-        for (int x = ptr[(size_t)sg.lb]; x < ptr[(size_t)sg.le]; x++) {  // positions leave the run
-            const int i = rows[(size_t)x];
-            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) pchunk[(size_t)p] = -1;
-        }
-        for (int q : stg_list) stg_of[(size_t)q] = -1;
-        stg_list.clear();
+    std::vector<Item> items;
+    size_t total = 0;
+    void add(void **dst, const void *src, size_t bytes, size_t copy) {
+        items.push_back({dst, src, bytes, copy, total});
+        total += (bytes + 255) & ~(size_t)255;
     }
-    if (fp.items.empty()) fp.items.push_back({0, 0, -1, -1});
-    for (std::vector<int> *v : {&fp.pairs, &fp.staged, &fp.rounds})
-        if (v->empty()) v->push_back(0);
-    if (fp.chunks.empty()) fp.chunks.push_back(rsp::RndChunk{});
+    template <typename V>
+    void up(V **dst, const std::vector<V> &v) {
+        add((void **)dst, v.empty() ? nullptr : v.data(), std::max<size_t>(v.size(), 1) * sizeof(V),
+            v.size() * sizeof(V));
+    }
+    void space(void **dst, size_t bytes) { add(dst, nullptr, bytes, 0); }
+    hipError_t commit(void **base, hipStream_t s) {
+        *base = nullptr;
+        if (total == 0) return hipSuccess;
+        hipError_t e = hipMalloc(base, total);
+        if (e != hipSuccess) return e;
+        for (const Item &it : items) {
+            *it.dst = (char *)*base + it.off;
+            if (it.copy && e == hipSuccess)
+                e = hipMemcpyAsync(*it.dst, it.src, it.copy, hipMemcpyHostToDevice, s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        return e;
+    }
+};
+
+// Upload one DAG's solve plan (into the arena `ar`) and keep its host parts.
+static void dag_upload(Arena &ar, rsp_ilu0_info::Dag &d, const rsp_an::DagHost &h) {
+    d.ptr = h.ptr;
+    d.batch = h.batch;
+    d.group = h.group;
+    d.segs = h.sp.segs;
+    d.nshort = h.sp.nshort;
+    d.nwave = h.sp.nwave;
+    d.sbase = h.sp.sbase;
+    d.nterms = (int)h.sp.tpos.size();
+    ar.up(&d.d_rows, h.rows);
+    ar.up(&d.d_ptr, h.ptr);
+    ar.up(&d.d_tasks, h.sp.tasks);
+    ar.up(&d.d_nshort, h.sp.nshort);
+    ar.up(&d.d_tpos, h.sp.tpos);
+    ar.up(&d.d_src, h.sp.src);
+    ar.up(&d.d_chunks, h.sp.chunks);
+    ar.up(&d.d_trow, h.sp.trow);
+    ar.up(&d.d_sid, h.sp.sid);
+    ar.up(&d.d_stg, h.sp.stg);
 }
 
 extern "C" {
 
-static hipError_t upload(int **dst, const std::vector<int> &v) {
-    size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(int);
-    hipError_t e = hipMalloc((void **)dst, bytes);
-    if (e != hipSuccess) return e;
-    if (!v.empty()) e = hipMemcpy(*dst, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice);
-    return e;
-}
 
-// Symbolic ILU(0): the update list of every position (see IluArgs) and the
-// intra-row stages of the lower positions. Row i is scattered into a dense
-// column -> position map, then each lower k (ascending) walks row k's upper
-// part; a hit at column j appends (pos l_ik, pos u_kj) to position (i, j).
-
-// Host worker threads for the analysis: OMP_NUM_THREADS (the box's share of
-// its cores; the machine may have many more) or the hardware count, <= 64.
-static int host_threads() {
-    int t = env_int("OMP_NUM_THREADS", 0);
-    if (t <= 0) t = (int)std::thread::hardware_concurrency();
-    return std::max(1, std::min(t, 64));
-}
-
-// f(r0, r1) over contiguous row blocks of [0, n) on host_threads() threads.
-}  // extern "C"
-template <typename F>
-static void parallel_rows(int n, F f) {
-    const int nt = n < 8192 ? 1 : host_threads();
-    if (nt == 1) {
-        f(0, n);
-        return;
+// Budget of the fat factor slot layout (ints): RSP_ILU_SLOT_CAP_MB if set,
+// else the smaller of 2 GB and 1/8 of the device memory free now.
+static long long slot_cap_ints() {
+    long long cap_mb = env_int("RSP_ILU_SLOT_CAP_MB", -1);
+    if (cap_mb < 0) {
+        size_t fr = 0, tot = 0;
+        cap_mb = 2048;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap_mb = std::min<long long>(cap_mb, (long long)(fr >> 23));
     }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; t++)
-        th.emplace_back(f, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
-    for (std::thread &x : th) x.join();
+    return cap_mb * (1LL << 20) / 4;
 }
-extern "C" {
 
-static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<int> &ci,
-                         const std::vector<int> &dpos, const std::vector<int> &hasdiag,
-                         IluSymbolic &s) {
-    const int nnz = rp[(size_t)n];
-    std::vector<int> cnt((size_t)nnz, 0);
-    // pass 1: counts (rows are independent: a row writes only its own
-    // positions' counts; each worker scatters its rows into its own map)
-    std::mutex mu;
-    long long total = 0;
-    parallel_rows(n, [&](int r0, int r1) {
-        std::vector<int> map((size_t)n, -1);
-        long long part = 0;
-        for (int i = r0; i < r1; i++) {
-            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
-            for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) {
-                const int k = ci[(size_t)p];
-                for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
-                    const int t = map[(size_t)ci[(size_t)q]];
-                    if (t > p) {
-                        cnt[(size_t)t]++;
-                        part++;
-                    }
-                }
+// The data-parallel analysis on the device (ilu_analysis.hip), overlapped
+// with the host level sets: validation, diagonal positions and structural
+// zero, then the symbolic factor (update lists, stages, stage order, divisor
+// positions), which stays on the device for the factor kernels; the host gets
+// back the pattern, dpos / hasdiag, the update lists and stages its plans
+// read. Rows longer than kAnDevRow entries (circuit hubs: a long serial chain
+// of lower positions, slow at one GPU lane's memory latency) are done on the
+// host (rsp_an::symbolic_rows) and their ranges uploaded. Fills hp (levels
+// included).
+static constexpr int kAnDevRow = 1024;
+static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const int *d_rp, const int *d_ci,
+                                        const std::vector<int> &rp, std::vector<int> &ci, rsp_an::IluHostPlan &hp,
+                                        rsp_an::Phases &ph) {
+    const int n = hp.n, nnz_s = hp.nnz_s;
+    hipStream_t s = h->stream;
+    std::vector<int> dev_rows, long_rows;
+    for (int i = 0; i < n; i++) (rp[(size_t)i + 1] - rp[(size_t)i] <= kAnDevRow ? dev_rows : long_rows).push_back(i);
+    size_t scan_bytes = 0;
+    RSP_CHECK_HIP(rsp_k::ilu_an_scan(nullptr, nullptr, nnz_s + 1, nullptr, &scan_bytes, s));
+    Arena ar;
+    int *d_flags = nullptr, *d_cnt = nullptr, *d_stage = nullptr, *d_scratch = nullptr, *d_rows = nullptr;
+    void *d_scan = nullptr;
+    ar.space((void **)&f->d_dpos, (size_t)std::max(n, 1) * 4);
+    ar.space((void **)&f->d_hasdiag, (size_t)std::max(n, 1) * 4);
+    ar.space((void **)&d_flags, 2 * 4);
+    ar.space((void **)&d_cnt, ((size_t)nnz_s + 1) * 4);
+    ar.space((void **)&f->d_upd_ptr, ((size_t)nnz_s + 1) * 4);
+    ar.space((void **)&d_stage, (size_t)std::max(nnz_s, 1) * 4);
+    ar.space((void **)&f->d_lord, (size_t)std::max(nnz_s, 1) * 4);
+    ar.space((void **)&f->d_lend, (size_t)std::max(nnz_s, 1) * 4);
+    ar.space((void **)&f->d_udiv, (size_t)std::max(nnz_s, 1) * 4);
+    ar.space((void **)&d_scratch, (size_t)std::max(nnz_s, 1) * 4);
+    ar.space(&d_scan, std::max<size_t>(scan_bytes, 16));
+    ar.up(&d_rows, dev_rows);
+    RSP_CHECK_HIP(ar.commit(&f->d_arena_sym, s));
+    const int flags0[2] = {0, INT_MAX};
+    int flags[2] = {0, INT_MAX};
+    RSP_CHECK_HIP(hipMemcpyAsync(d_flags, flags0, sizeof(flags0), hipMemcpyHostToDevice, s));
+    RSP_CHECK_HIP(rsp_k::ilu_an_rows(n, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_flags, s));
+    RSP_CHECK_HIP(hipMemcpyAsync(flags, d_flags, sizeof(flags), hipMemcpyDeviceToHost, s));
+    RSP_CHECK_HIP(hipStreamSynchronize(s));
+    if (flags[0]) return RSP_STATUS_INVALID_VALUE;  // a column out of range or a row not increasing
+    hp.structural_zero = flags[1] == INT_MAX ? -1 : flags[1];
+    const int n_c[3] = {(int)dev_rows.size(), 0, 0};
+    const int *rows_c[3] = {d_rows, nullptr, nullptr};
+    RSP_CHECK_HIP(rsp_k::ilu_an_count(rows_c, n_c, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_cnt, d_scratch, s));
+    hp.dpos.resize((size_t)n);
+    hp.hasdiag.resize((size_t)n);
+    if (n > 0) {
+        RSP_CHECK_HIP(hipMemcpyAsync(hp.dpos.data(), f->d_dpos, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        RSP_CHECK_HIP(hipMemcpyAsync(hp.hasdiag.data(), f->d_hasdiag, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (nnz_s > 0) RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), d_ci, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
+    RSP_CHECK_HIP(hipStreamSynchronize(s));
+    // the long rows' counts on the host
+    std::vector<int> hcnt(long_rows.empty() ? 0 : (size_t)nnz_s);
+    rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), hcnt.data(),
+                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+    for (int i : long_rows)
+        RSP_CHECK_HIP(hipMemcpyAsync(d_cnt + rp[(size_t)i], hcnt.data() + rp[(size_t)i],
+                                     (size_t)(rp[(size_t)i + 1] - rp[(size_t)i]) * 4, hipMemcpyHostToDevice, s));
+    RSP_CHECK_HIP(hipMemsetAsync(d_cnt + nnz_s, 0, 4, s));
+    RSP_CHECK_HIP(rsp_k::ilu_an_scan(d_cnt, f->d_upd_ptr, nnz_s + 1, d_scan, &scan_bytes, s));
+    hp.sym.upd_ptr.resize((size_t)nnz_s + 1);
+    RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_ptr.data(), f->d_upd_ptr, ((size_t)nnz_s + 1) * 4,
+                                 hipMemcpyDeviceToHost, s));
+    RSP_CHECK_HIP(hipStreamSynchronize(s));
+    ph.mark("device rows");
+    // a pair count past int would overflow the plans' indices
+    const int total = hp.sym.upd_ptr[(size_t)nnz_s];
+    if (total < 0) return RSP_STATUS_ALLOC_FAILED;
+    Arena ap;
+    ap.space((void **)&f->d_upd_l, (size_t)std::max(total, 1) * 4);
+    ap.space((void **)&f->d_upd_u, (size_t)std::max(total, 1) * 4);
+    RSP_CHECK_HIP(ap.commit(&f->d_arena_pairs, s));
+    RSP_CHECK_HIP(rsp_k::ilu_an_fill(rows_c, n_c, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, d_scratch,
+                                     f->d_upd_l, f->d_upd_u, s));
+    RSP_CHECK_HIP(rsp_k::ilu_an_stages(n, kAnDevRow, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, f->d_upd_l,
+                                       d_stage, f->d_lord, f->d_lend, f->d_udiv, d_scratch, s));
+    // the level sets on the host while the device fills the update lists
+    rsp_an::plan_levels(rp.data(), ci.data(), hp);
+    ph.mark("levels");
+    hp.sym.upd_l.resize((size_t)total);
+    hp.sym.upd_u.resize((size_t)total);
+    hp.sym.stage.resize((size_t)nnz_s);
+    if (total > 0) {
+        RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_l.data(), f->d_upd_l, (size_t)total * 4, hipMemcpyDeviceToHost, s));
+        RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_u.data(), f->d_upd_u, (size_t)total * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (nnz_s > 0)
+        RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.stage.data(), d_stage, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
+    RSP_CHECK_HIP(hipStreamSynchronize(s));
+    if (!long_rows.empty()) {  // the long rows' lists, stages, stage order, divisors on the host
+        std::vector<int> lord((size_t)nnz_s), lend((size_t)nnz_s), udiv((size_t)nnz_s);
+        rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), nullptr,
+                              hp.sym.upd_ptr.data(), hp.sym.upd_l.data(), hp.sym.upd_u.data(), hp.sym.stage.data(),
+                              lord.data(), lend.data(), udiv.data());
+        for (int i : long_rows) {
+            const size_t rs = (size_t)rp[(size_t)i], len = (size_t)(rp[(size_t)i + 1] - rp[(size_t)i]);
+            const size_t q0 = (size_t)hp.sym.upd_ptr[rs], nq = (size_t)hp.sym.upd_ptr[rs + len] - q0;
+            if (nq > 0) {
+                RSP_CHECK_HIP(hipMemcpyAsync(f->d_upd_l + q0, hp.sym.upd_l.data() + q0, nq * 4, hipMemcpyHostToDevice, s));
+                RSP_CHECK_HIP(hipMemcpyAsync(f->d_upd_u + q0, hp.sym.upd_u.data() + q0, nq * 4, hipMemcpyHostToDevice, s));
             }
-            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
+            RSP_CHECK_HIP(hipMemcpyAsync(f->d_lord + rs, lord.data() + rs, len * 4, hipMemcpyHostToDevice, s));
+            RSP_CHECK_HIP(hipMemcpyAsync(f->d_lend + rs, lend.data() + rs, len * 4, hipMemcpyHostToDevice, s));
+            RSP_CHECK_HIP(hipMemcpyAsync(f->d_udiv + rs, udiv.data() + rs, len * 4, hipMemcpyHostToDevice, s));
         }
-        std::lock_guard<std::mutex> g(mu);
-        total += part;
-    });
-    if (total > INT_MAX) return false;
-    s.upd_ptr.assign((size_t)nnz + 1, 0);
-    for (int p = 0; p < nnz; p++) s.upd_ptr[(size_t)p + 1] = s.upd_ptr[(size_t)p] + cnt[(size_t)p];
-    s.upd_l.resize((size_t)total);
-    s.upd_u.resize((size_t)total);
-    // pass 2: fill (k ascending per target, since p ascends) + stages
-    std::vector<int> &stage = s.stage;
-    stage.assign((size_t)nnz, 0);
-    s.lord.assign((size_t)nnz, 0);
-    s.lend.assign((size_t)nnz, 0);
-    parallel_rows(n, [&](int r0, int r1) {
-        std::vector<int> map((size_t)n, -1), order;
-        for (int i = r0; i < r1; i++) {
-            const int rs = rp[(size_t)i], di = dpos[(size_t)i];
-            for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
-            for (int p = rs; p < rp[(size_t)i + 1]; p++) cnt[(size_t)p] = s.upd_ptr[(size_t)p];  // fill
-            for (int p = rs; p < di; p++) {
-                const int k = ci[(size_t)p];
-                for (int q = dpos[(size_t)k] + hasdiag[(size_t)k]; q < rp[(size_t)k + 1]; q++) {
-                    const int t = map[(size_t)ci[(size_t)q]];
-                    if (t > p) {
-                        const int u = cnt[(size_t)t]++;
-                        s.upd_l[(size_t)u] = p;
-                        s.upd_u[(size_t)u] = q;
-                        if (t < di) stage[(size_t)t] = std::max(stage[(size_t)t], stage[(size_t)p] + 1);
-                    }
-                }
-            }
-            for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = -1;
-            // lower positions by (stage, column)
-            order.assign((size_t)(di - rs), 0);
-            for (int p = rs; p < di; p++) order[(size_t)(p - rs)] = p;
-            std::stable_sort(order.begin(), order.end(),
-                             [&](int a, int b) { return stage[(size_t)a] < stage[(size_t)b]; });
-            for (int x = 0; x < di - rs; x++) s.lord[(size_t)(rs + x)] = order[(size_t)x];
-            for (int x = di - rs - 1; x >= 0; x--) {
-                const bool last = x == di - rs - 1 ||
-                                  stage[(size_t)order[(size_t)x]] != stage[(size_t)order[(size_t)x + 1]];
-                s.lend[(size_t)(rs + x)] = last ? rs + x + 1 : s.lend[(size_t)(rs + x + 1)];
-            }
-        }
-    });
-    return true;
+        RSP_CHECK_HIP(hipStreamSynchronize(s));
+    }
+    ph.mark("device symbolic");
+    return RSP_STATUS_SUCCESS;
 }
 
 rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_offsets,
                                const int *d_col_ind, rsp_ilu0_info_t f) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     // diagnostics: RSP_ILU_TIMING=1 prints the wall time of each analysis phase
-    const bool timing = env_int("RSP_ILU_TIMING", 0) != 0;
-    auto t_last = std::chrono::steady_clock::now();
-    auto phase = [&](const char *what) {
-        if (!timing) return;
-        const auto t = std::chrono::steady_clock::now();
-        fprintf(stderr, "rsp_ilu0_analysis n=%d %-14s %8.2f ms\n", n, what,
-                std::chrono::duration<double, std::milli>(t - t_last).count());
-        t_last = t;
-    };
+    rsp_an::Phases ph;
+    ph.print = env_int("RSP_ILU_TIMING", 0) != 0;
+    ph.n = n;
+    ph.start();
     if (!f || n < 0 || nnz < 0 || (n > 0 && !d_row_offsets)) return RSP_STATUS_INVALID_VALUE;
     ilu_free_device(f);
     f->analysed = 0;
     f->factored = 0;
     f->structural_zero = -1;
+    f->host.reset();
+    // the pattern to the host (row offsets first: the stored entries must lie
+    // inside the declared arrays before colidx is read)
     std::vector<int> rp((size_t)n + 1, 0);
     if (n > 0) {
         RSP_CHECK_HIP(hipMemcpyAsync(rp.data(), d_row_offsets, ((size_t)n + 1) * sizeof(int),
@@ -1546,263 +1225,67 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     if (nnz_s > 0 && !d_col_ind) return RSP_STATUS_INVALID_VALUE;
     if (nnz_s > nnz) return RSP_STATUS_INVALID_VALUE;  // entries past the declared arrays
     std::vector<int> ci((size_t)nnz_s);
-    if (nnz_s > 0) {
-        RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), d_col_ind, (size_t)nnz_s * sizeof(int),
-                                     hipMemcpyDeviceToHost, h->stream));
-        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    std::unique_ptr<rsp_an::IluHostPlan> hp(new (std::nothrow) rsp_an::IluHostPlan());
+    if (!hp) return RSP_STATUS_ALLOC_FAILED;
+    hp->n = n;
+    hp->nnz_s = nnz_s;
+    rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph);
+    if (st != RSP_STATUS_SUCCESS) {
+        ilu_free_device(f);
+        return st;
     }
-    for (int v : ci)
-        if (v < 0 || v >= n) return RSP_STATUS_INVALID_VALUE;
-    // The diagonal search, update pairs and stages assume each row's columns
-    // strictly increasing (the reference loader sorts rows,
-    // loadMatrixMarket.cpp:237-242; csrilu02 requires sorted, duplicate-free
-    // rows). Unsorted rows or a repeated column are rejected here instead of
-    // silently factoring the wrong pattern.
-    for (int i = 0; i < n; i++)
-        for (int p = rp[(size_t)i] + 1; p < rp[(size_t)i + 1]; p++)
-            if (ci[(size_t)p] <= ci[(size_t)p - 1]) return RSP_STATUS_INVALID_VALUE;
-    std::vector<int> dpos((size_t)n), hasdiag((size_t)n);
-    for (int i = 0; i < n; i++) {
-        const int *b = ci.data() + rp[(size_t)i], *e = ci.data() + rp[(size_t)i + 1];
-        const int *p = std::lower_bound(b, e, i);
-        dpos[(size_t)i] = (int)(p - ci.data());
-        hasdiag[(size_t)i] = (p != e && *p == i) ? 1 : 0;
-        if (!hasdiag[(size_t)i] && f->structural_zero < 0) f->structural_zero = i;
-    }
-    // levels of the lower DAG (factor + L solve)
-    std::vector<int> lv((size_t)n, 0);
-    int nl = n > 0 ? 1 : 0;
-    for (int i = 0; i < n; i++) {
-        int l = 0;
-        for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) l = std::max(l, lv[(size_t)ci[(size_t)p]] + 1);
-        lv[(size_t)i] = l;
-        nl = std::max(nl, l + 1);
-    }
-    // transposed strict lower: row k lists (j, pos) for l_jk, j descending
-    std::vector<int> ltp((size_t)n + 1, 0);
-    for (int j = 0; j < n; j++)
-        for (int p = rp[(size_t)j]; p < dpos[(size_t)j]; p++) ltp[(size_t)ci[(size_t)p] + 1]++;
-    for (int k = 0; k < n; k++) ltp[(size_t)k + 1] += ltp[(size_t)k];
-    std::vector<int> lts((size_t)ltp[(size_t)n]), ltc((size_t)ltp[(size_t)n]);
-    {
-        std::vector<int> fill(ltp.begin(), ltp.end() - 1);
-        for (int j = n - 1; j >= 0; j--)
-            for (int p = rp[(size_t)j]; p < dpos[(size_t)j]; p++) {
-                int k = ci[(size_t)p];
-                int slot = fill[(size_t)k]++;
-                lts[(size_t)slot] = p;
-                ltc[(size_t)slot] = j;
-            }
-    }
-    // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
-    std::vector<int> lvt((size_t)n, 0);
-    int nlt = n > 0 ? 1 : 0;
-    for (int j = n - 1; j >= 0; j--) {
-        nlt = std::max(nlt, lvt[(size_t)j] + 1);
-        for (int p = rp[(size_t)j]; p < dpos[(size_t)j]; p++) {
-            int k = ci[(size_t)p];
-            lvt[(size_t)k] = std::max(lvt[(size_t)k], lvt[(size_t)j] + 1);
+    // the U DAG (--true-lu extension) is planned on its first use
+    rsp_an::plan_rest(rp.data(), ci.data(), slot_cap_ints(), false, *hp);
+    ph.mark("plans");
+    f->structural_zero = hp->structural_zero;
+    f->n_updates = (long long)hp->sym.upd_l.size();
+    f->fac_batch = hp->fac_batch;
+    f->fac_segs = hp->fplan.segs;
+    f->fslev = hp->fslev;
+    if (env_int("RSP_ILU_DIGEST", 0)) {  // tests only: the device-only symbolic arrays too
+        hp->sym.lord.resize((size_t)nnz_s);
+        hp->sym.lend.resize((size_t)nnz_s);
+        hp->udiv.resize((size_t)nnz_s);
+        hipError_t e = hipSuccess;
+        if (nnz_s > 0) {
+            e = hipMemcpyAsync(hp->sym.lord.data(), f->d_lord, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(hp->sym.lend.data(), f->d_lend, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(hp->udiv.data(), f->d_udiv, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         }
+        f->digest = e == hipSuccess ? rsp_an::digest(*hp) : 0;
     }
-    // levels of the U DAG (extension): row i waits for j > i with u_ij != 0
-    std::vector<int> lvu((size_t)n, 0);
-    int nlu = n > 0 ? 1 : 0;
-    for (int i = n - 1; i >= 0; i--) {
-        int l = 0;
-        for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++)
-            l = std::max(l, lvu[(size_t)ci[(size_t)p]] + 1);
-        lvu[(size_t)i] = l;
-        nlu = std::max(nlu, l + 1);
+    // everything in one device allocation
+    Arena ar;
+    ar.up(&f->d_rchunks, hp->fplan.chunks);
+    ar.up(&f->d_ritems, hp->fplan.items);
+    ar.up(&f->d_rpairs, hp->fplan.pairs);
+    ar.up(&f->d_rstaged, hp->fplan.staged);
+    ar.up(&f->d_rrounds, hp->fplan.rounds);
+    ar.up(&f->d_frow, hp->frow);
+    dag_upload(ar, f->L, hp->L);
+    dag_upload(ar, f->LT, hp->LT);
+    // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
+    const size_t nt = (size_t)std::max({f->L.nterms, f->LT.nterms, 1});
+    ar.space(&f->d_sval, nt * sizeof(double));
+    ar.space(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
+    ar.space(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
+    ar.space((void **)&f->d_zero, sizeof(int));
+    int4 *d_desc = nullptr;
+    long long *d_offs = nullptr;
+    if (!hp->slot_desc.empty()) {
+        ar.up(&d_desc, hp->slot_desc);
+        ar.up(&d_offs, hp->slot_offs);
     }
-    std::vector<int> rows_l, rows_lt, rows_u;
-    phase("copy+levels");
-    group_levels(lv, nl, f->L.ptr, rows_l);
-    group_levels(lvt, nlt, f->LT.ptr, rows_lt);
-    group_levels(lvu, nlu, f->U.ptr, rows_u);
-    // RSP_ILU_THIN_SOLVE / RSP_ILU_THIN_FACTOR: tuning knobs (0 = no thin runs)
-    const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
-    const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
-    IluSymbolic sym;
-    std::vector<int4> slot_desc;        // fat factor slot rows: {x, rm, qm, 0}
-    std::vector<long long> slot_offs;   // ... and their offsets in f->d_fslots
-    phase("group");
-    if (!ilu_symbolic(n, rp, ci, dpos, hasdiag, sym)) return RSP_STATUS_ALLOC_FAILED;
-    phase("symbolic");
-    f->n_updates = (long long)sym.upd_l.size();
-    {
-        long long nl = 0, nu = 0;
-        for (int i = 0; i < n; i++) {
-            nl += dpos[(size_t)i] - rp[(size_t)i];
-            nu += rp[(size_t)i + 1] - dpos[(size_t)i] - hasdiag[(size_t)i];
-        }
-        f->L.batch = f->LT.batch = chain_batch(nl, n);
-        f->U.batch = chain_batch(nu, n);
-        for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U})  // thin-run term groups
-            d->group = env_int("RSP_ILU_GROUP", d->batch == 2 ? 2 : 4) == 2 ? 2 : 4;
-        f->fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
-    }
-    // the factor plan and the three solve plans (flat terms in level order,
-    // thin-run chunks, y sources) are independent: built concurrently
-    FacPlan fplan;
-    SolvePlan sps[3];
-    std::vector<int> udiag((size_t)n);
-    for (int i = 0; i < n; i++) udiag[(size_t)i] = hasdiag[(size_t)i] ? dpos[(size_t)i] : -1;
-    {
-        std::vector<std::thread> th;
-        th.emplace_back([&] {
-            build_factor_plan(n, rp, ci, dpos, hasdiag, sym, f->L.ptr, rows_l, thin_factor, fplan);
-        });
-        th.emplace_back([&] {
-            build_solve_plan(n, f->L.ptr, rows_l, thin_solve, f->L.group, std::vector<int>(),
-                             [&](int i, auto emit) {
-                                 for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
-                             }, sps[0]);
-        });
-        th.emplace_back([&] {
-            build_solve_plan(n, f->LT.ptr, rows_lt, thin_solve, f->LT.group, std::vector<int>(),
-                             [&](int i, auto emit) {
-                                 for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++)
-                                     emit(lts[(size_t)q], ltc[(size_t)q]);
-                             }, sps[1]);
-        });
-        th.emplace_back([&] {
-            build_solve_plan(n, f->U.ptr, rows_u, thin_solve, f->U.group, udiag, [&](int i, auto emit) {
-                for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++)
-                    emit(p, ci[(size_t)p]);
-            }, sps[2]);
-        });
-        for (std::thread &x : th) x.join();
-    }
-    phase("plans");
-    f->fac_segs = fplan.segs;
-    hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = upload_vec(&f->d_rchunks, fplan.chunks);
-    if (e == hipSuccess) e = upload_vec(&f->d_ritems, fplan.items);
-    if (e == hipSuccess) e = upload_vec(&f->d_rpairs, fplan.pairs);
-    if (e == hipSuccess) e = upload_vec(&f->d_rstaged, fplan.staged);
-    if (e == hipSuccess) e = upload_vec(&f->d_rrounds, fplan.rounds);
-    if (e == hipSuccess) e = upload(&f->d_upd_ptr, sym.upd_ptr);
-    if (e == hipSuccess) e = upload(&f->d_upd_l, sym.upd_l);
-    if (e == hipSuccess) e = upload(&f->d_upd_u, sym.upd_u);
-    if (e == hipSuccess) e = upload(&f->d_lord, sym.lord);
-    if (e == hipSuccess) e = upload(&f->d_lend, sym.lend);
-    {  // per lower position (i, k): the position of its divisor u_kk (-1: none, or upper)
-        std::vector<int> udiv((size_t)nnz_s, -1);
-        for (int i = 0; i < n; i++)
-            for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) {
-                const int k = ci[(size_t)p];
-                if (hasdiag[(size_t)k]) udiv[(size_t)p] = dpos[(size_t)k];
-            }
-        if (e == hipSuccess) e = upload(&f->d_udiv, udiv);
-        std::vector<rsp::FacRow> frow(std::max<size_t>(rows_l.size(), 1), rsp::FacRow{});
-        for (size_t x = 0; x < rows_l.size(); x++) {
-            const int i = rows_l[x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
-            frow[x] = rsp::FacRow{i, rs, dpos[(size_t)i], re, sym.upd_ptr[(size_t)rs], sym.upd_ptr[(size_t)re],
-                                  hasdiag[(size_t)i], 0};
-        }
-        if (e == hipSuccess) e = upload_vec(&f->d_frow, frow);
-        // fat factor levels in the slot layout (rsp::FacSlotLevel): each row's
-        // structure at a fixed stride, so ilu0_level_slot reads it in one
-        // round trip. Levels past RSP_ILU_SLOT_CAP_MB of slots keep FacRow.
-        const std::vector<int> &lp = f->L.ptr;
-        const int nlev = (int)lp.size() - 1;
-        f->fslev.assign((size_t)std::max(nlev, 0), rsp::FacSlotLevel{0, 0, 0, 0, 0});
-        // Slot budget (ints): RSP_ILU_SLOT_CAP_MB if set, else the smaller of
-        // 2 GB and 1/8 of the device memory free now. A level whose padded
-        // slots would take more than twice its rows' own structure (one large
-        // row among many small ones) keeps the FacRow path.
-        long long cap_mb = env_int("RSP_ILU_SLOT_CAP_MB", -1);
-        if (cap_mb < 0) {
-            size_t fr = 0, tot = 0;
-            cap_mb = 2048;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap_mb = std::min<long long>(cap_mb, (long long)(fr >> 23));
-        }
-        const long long cap = cap_mb * (1LL << 20) / 4;
-        long long total = 0;
-        std::vector<int> slot_levels;
-        slot_desc.clear();
-        slot_offs.clear();
-        for (const rsp::LevelSeg &sg : fplan.segs) {
-            if (sg.thin) continue;
-            for (int l = sg.lb; l < sg.le; l++) {
-                int rm = 0, qm = 0;
-                long long own = 0;
-                for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
-                    const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
-                    const int nq = sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs];
-                    if (re - rs <= rsp::kFacRow && nq <= rsp::kFacPairs) {
-                        rm = std::max(rm, re - rs);
-                        qm = std::max(qm, nq);
-                    }
-                    own += (rsp::fac_pairs_at(std::min(re - rs, rsp::kFacRow)) + 2 * std::min(nq, rsp::kFacPairs) + 3) & ~3;
-                }
-                if (rm == 0 || qm == 0) continue;
-                const int stride = (rsp::fac_pairs_at(rm) + 2 * qm + 3) & ~3;
-                const long long cnt = lp[(size_t)l + 1] - lp[(size_t)l];
-                if (cnt * stride > 2 * own) continue;  // padding would dominate
-                if (total + cnt * stride > cap) continue;
-                f->fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, rm, qm, 0};
-                total += cnt * stride;
-                slot_levels.push_back(l);
-            }
-        }
-        if (total > 0) {  // written on the device from the symbolic arrays (ilu0_build_slots)
-            for (int l : slot_levels) {
-                const rsp::FacSlotLevel &sl = f->fslev[(size_t)l];
-                for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
-                    slot_desc.push_back(int4{x, sl.rm, sl.qm, 0});
-                    slot_offs.push_back(sl.off + (long long)(x - lp[(size_t)l]) * sl.stride);
-                }
-            }
-            // the slot layout is an optimisation: without its memory the
-            // FacRow path factors every fat level (same bits)
-            if (e == hipSuccess && hipMalloc((void **)&f->d_fslots, (size_t)total * sizeof(int)) != hipSuccess) {
-                (void)hipGetLastError();
-                f->d_fslots = nullptr;
-                f->fslev.assign(f->fslev.size(), rsp::FacSlotLevel{0, 0, 0, 0, 0});
-                slot_desc.clear();
-                slot_offs.clear();
-            }
-        }
-    }
-    if (e == hipSuccess) e = upload(&f->d_dpos, dpos);
-    if (e == hipSuccess) e = upload(&f->d_hasdiag, hasdiag);
-    if (e == hipSuccess) e = upload(&f->L.d_rows, rows_l);
-    if (e == hipSuccess) e = upload(&f->L.d_ptr, f->L.ptr);
-    if (e == hipSuccess) e = upload(&f->LT.d_rows, rows_lt);
-    if (e == hipSuccess) e = upload(&f->LT.d_ptr, f->LT.ptr);
-    if (e == hipSuccess) e = upload(&f->U.d_rows, rows_u);
-    if (e == hipSuccess) e = upload(&f->U.d_ptr, f->U.ptr);
-    for (int kind = 0; kind < 3 && e == hipSuccess; kind++) {
-        rsp_ilu0_info::Dag &d = kind == 0 ? f->L : (kind == 1 ? f->LT : f->U);
-        SolvePlan &sp = sps[kind];
-        d.segs = sp.segs;
-        d.nshort = sp.nshort;
-        d.nwave = sp.nwave;
-        d.sbase = sp.sbase;
-        e = upload_vec(&d.d_tasks, sp.tasks);
-        if (e == hipSuccess) e = upload_vec(&d.d_nshort, sp.nshort);
-        if (e == hipSuccess) e = upload_vec(&d.d_tpos, sp.tpos);
-        if (e == hipSuccess) e = upload_vec(&d.d_src, sp.src);
-        if (e == hipSuccess) e = upload_vec(&d.d_chunks, sp.chunks);
-        if (e == hipSuccess) e = upload_vec(&d.d_trow, sp.trow);
-        if (e == hipSuccess) e = upload_vec(&d.d_sid, sp.sid);
-        if (e == hipSuccess) e = upload_vec(&d.d_stg, sp.stg);
-        d.nterms = (int)sp.tpos.size();
-    }
-    {  // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
-        const size_t nt = (size_t)std::max({f->L.nterms, f->LT.nterms, f->U.nterms, 1});
-        if (e == hipSuccess) e = hipMalloc(&f->d_sval, nt * sizeof(double));
-        if (e == hipSuccess) e = hipMalloc(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
-        if (e == hipSuccess) e = hipMalloc(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
-    }
-    if (e == hipSuccess) e = hipMalloc((void **)&f->d_zero, sizeof(int));
+    hipError_t e = ar.commit(&f->d_arena, h->stream);
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
-    if (e == hipSuccess && !slot_desc.empty()) {  // fat factor slots, written on the device
-        int4 *d_desc = nullptr;
-        long long *d_offs = nullptr;
-        hipError_t es = upload_vec(&d_desc, slot_desc);
-        if (es == hipSuccess) es = upload_vec(&d_offs, slot_offs);
+    // fat factor slots, written on the device from the uploaded symbolic
+    // arrays; the layout is an optimisation: without its memory, or if the
+    // build fails, the FacRow path factors every fat level (same bits)
+    if (e == hipSuccess && hp->slot_total > 0) {
+        hipError_t es = hipMalloc((void **)&f->d_fslots, (size_t)hp->slot_total * sizeof(int));
         if (es == hipSuccess) {
             rsp::IluArgs a{};
             a.n = n;
@@ -1816,28 +1299,85 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
             a.lend = f->d_lend;
             a.udiv = f->d_udiv;
             a.plan.rows = f->L.d_rows;
-            es = rsp_k::ilu0_build_slots(a, d_desc, d_offs, (int)slot_desc.size(), f->d_fslots, h->stream);
+            es = rsp_k::ilu0_build_slots(a, d_desc, d_offs, (int)hp->slot_desc.size(), f->d_fslots, h->stream);
             if (es == hipSuccess) es = hipStreamSynchronize(h->stream);
         }
-        if (d_desc) (void)hipFree(d_desc);
-        if (d_offs) (void)hipFree(d_offs);
-        if (es != hipSuccess) {  // no slots: fall back to the FacRow path, not a failed analysis
+        if (es != hipSuccess) {
             (void)hipGetLastError();
-            (void)hipFree(f->d_fslots);
+            if (f->d_fslots) (void)hipFree(f->d_fslots);
             f->d_fslots = nullptr;
             f->fslev.assign(f->fslev.size(), rsp::FacSlotLevel{0, 0, 0, 0, 0});
         }
     }
-    phase("uploads");
+    ph.mark("upload");
     if (e != hipSuccess) {
         ilu_free_device(f);
         return e == hipErrorOutOfMemory ? RSP_STATUS_ALLOC_FAILED : RSP_STATUS_EXECUTION_FAILED;
     }
+    // host copies kept for the U plan, built on first use (rsp_trsv_upper)
+    hp->sym = rsp_an::IluSymbolic();
+    hp->fplan = rsp_an::FacPlan();
+    hp->L = rsp_an::DagHost();
+    hp->LT = rsp_an::DagHost();
+    hp->ltp.clear();
+    hp->lts.clear();
+    hp->ltc.clear();
+    hp->udiv.clear();
+    hp->frow.clear();
+    hp->slot_desc.clear();
+    hp->slot_offs.clear();
+    f->host_rp.swap(rp);
+    f->host_ci.swap(ci);
+    f->host = std::move(hp);
     f->n = n;
     f->nnz_s = nnz_s;
     f->rowptr = d_row_offsets;
     f->colidx = d_col_ind;
     f->analysed = 1;
+    return RSP_STATUS_SUCCESS;
+}
+
+// The U DAG's plan (rsp_trsv_upper, the --true-lu extension), on first use.
+static rsp_status_t ilu_plan_u(rsp_handle_t h, rsp_ilu0_info *f) {
+    if (f->U.d_ptr) return RSP_STATUS_SUCCESS;
+    if (!f->host) return RSP_STATUS_INTERNAL_ERROR;
+    rsp_an::plan_u(f->host_rp.data(), f->host_ci.data(), *f->host);
+    Arena ar;
+    dag_upload(ar, f->U, f->host->U);
+    // its streams (the L / L^T ones are sized for those DAGs' terms)
+    ar.space(&f->d_usval, (size_t)std::max(f->U.nterms, 1) * sizeof(double));
+    hipError_t e = ar.commit(&f->d_arena_u, h->stream);
+    f->host->U = rsp_an::DagHost();
+    if (e != hipSuccess) {
+        if (f->d_arena_u) (void)hipFree(f->d_arena_u);
+        f->d_arena_u = nullptr;
+        f->U = rsp_ilu0_info::Dag();
+        return e == hipErrorOutOfMemory ? RSP_STATUS_ALLOC_FAILED : RSP_STATUS_EXECUTION_FAILED;
+    }
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_ilu0_analysis_host(int n, const int *row_offsets, const int *col_ind,
+                                    int *levels_lower, int *levels_upper, uint64_t *digest,
+                                    double *phase_ms) {
+    rsp_an::Phases ph;
+    ph.n = n;
+    ph.ms = phase_ms;
+    if (phase_ms)
+        for (int i = 0; i < rsp_an::kPhases; i++) phase_ms[i] = 0.0;
+    ph.start();
+    rsp_an::IluHostPlan hp;
+    rsp_status_t st = rsp_an::plan_host(n, row_offsets, col_ind, 1LL << 29, false, hp, ph);
+    if (st != RSP_STATUS_SUCCESS) return st;
+    if (levels_lower) *levels_lower = (int)hp.L.ptr.size() - 1;
+    if (levels_upper) *levels_upper = (int)hp.LT.ptr.size() - 1;
+    if (digest) *digest = rsp_an::digest(hp);
+    return RSP_STATUS_SUCCESS;
+}
+
+rsp_status_t rsp_ilu0_plan_digest(rsp_ilu0_info_t f, uint64_t *digest) {
+    if (!f || !digest || !f->analysed || !f->digest) return RSP_STATUS_INVALID_VALUE;
+    *digest = f->digest;
     return RSP_STATUS_SUCCESS;
 }
 
@@ -2044,8 +1584,11 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f
     if (!f || !f->analysed || !alpha) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
+    rsp_status_t st = ilu_plan_u(h, f);  // planned on first use
+    if (st != RSP_STATUS_SUCCESS) return st;
     rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
     a.plan = level_plan(f->U, f->U.segs, f->U.batch);
+    a.sval = f->d_usval;
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::trsv_upper_f64(a, h->stream);

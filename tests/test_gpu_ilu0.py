@@ -281,3 +281,30 @@ def test_unsorted_or_duplicate_rows_rejected(handle):
         il.analysis()
     assert e.value.status == 3
     il.close()
+
+
+@pytest.mark.parametrize("name,scale", [("ASIC_320ks", 1.0), ("dc1", 1.0), ("FEM_3D_thermal2", 0.2),
+                                        ("ecology2", 0.2), ("Goodwin_095", 0.2), ("G2_circuit", 0.3)])
+def test_device_analysis_same_plan_as_host(handle, monkeypatch, name, scale):
+    """rsp_ilu0_analysis validates the pattern, finds the diagonals and builds
+    the symbolic factor (update lists, stages, stage order, divisor positions)
+    with MI355X kernels; rsp_ilu0_analysis_host builds everything on the
+    host. Every array of the plan must be identical (64-bit digest over all of
+    them), hub rows (ASIC_320ks: the long-row kernel classes) included."""
+    import ctypes as C
+    from respasol_amd._lib import rsp
+    monkeypatch.setenv("RSP_ILU_DIGEST", "1")
+    A = csr.surrogate(name, scale)
+    rp, ci, _ = upload_csr(A.rowptr, A.colidx, A.values)
+    il = Ilu0(handle, rp, ci)
+    il.analysis()
+    dev = C.c_uint64()
+    assert rsp.rsp_ilu0_plan_digest(il._info, C.byref(dev)) == 0
+    lo, up, hst = C.c_int(), C.c_int(), C.c_uint64()
+    r = np.ascontiguousarray(A.rowptr, np.int32)
+    c = np.ascontiguousarray(A.colidx, np.int32)
+    assert rsp.rsp_ilu0_analysis_host(A.n, r.ctypes.data, c.ctypes.data, C.byref(lo), C.byref(up),
+                                      C.byref(hst), None) == 0
+    assert dev.value == hst.value
+    assert il.levels() == (lo.value, up.value)
+    il.close()

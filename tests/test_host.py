@@ -219,3 +219,49 @@ def test_padded_allgather_layout_c_matches_python():
     b = csr.partition_rows(A.rowptr, 2)
     assert _lib.host.rsp_remap_cols_padded(3, ip(bad), ip(b), 2, _lib.host.rsp_padded_chunk(ip(b), 2),
                                            ip(np.empty(3, np.int32))) == -1
+
+
+def _py_levels(rowptr, colidx, transpose):
+    n = len(rowptr) - 1
+    lev = np.zeros(n, np.int64)
+    for i in (range(n - 1, -1, -1) if transpose else range(n)):
+        row = colidx[rowptr[i]:rowptr[i + 1]]
+        low = row[row < i]
+        if transpose:
+            if low.size:
+                np.maximum.at(lev, low, lev[i] + 1)
+        elif low.size:
+            lev[i] = lev[low].max() + 1
+    return int(lev.max()) + 1 if n else 0
+
+
+def _analysis_host(A):
+    import ctypes as C
+    lo, up, dg = C.c_int(), C.c_int(), C.c_uint64()
+    ph = (C.c_double * 6)()
+    rp = np.ascontiguousarray(A.rowptr, np.int32)
+    ci = np.ascontiguousarray(A.colidx, np.int32)
+    st = _lib.rsp.rsp_ilu0_analysis_host(A.n, rp.ctypes.data, ci.ctypes.data, C.byref(lo), C.byref(up),
+                                         C.byref(dg), ph)
+    return st, lo.value, up.value, dg.value, list(ph)
+
+
+@pytest.mark.parametrize("name,scale", [("G2_circuit", 0.05), ("ASIC_320ks", 0.05), ("ecology2", 0.01),
+                                        ("FEM_3D_thermal2", 0.02)])
+def test_ilu_analysis_host_levels_and_digest(name, scale):
+    """rsp_ilu0_analysis_host (the analysis' host phases, no device): the L and
+    L^T level counts equal a direct restatement of the DAG's longest paths,
+    and the plan digest is deterministic (threads and all)."""
+    A = csr.surrogate(name, scale)
+    st, lo, up, dg, ph = _analysis_host(A)
+    assert st == 0
+    assert lo == _py_levels(A.rowptr, A.colidx, False)
+    assert up == _py_levels(A.rowptr, A.colidx, True)
+    assert _analysis_host(A)[3] == dg and dg != 0
+    assert all(v >= 0 for v in ph)
+
+
+def test_ilu_analysis_host_rejects_malformed():
+    for rp, ci in (([0, 2, 4], [1, 0, 0, 1]), ([0, 2, 4], [0, 0, 0, 1]), ([0, 1, 2], [0, 5])):
+        A = csr.CsrMatrix(0, 2, 2, len(ci), np.array(rp, np.int32), np.array(ci, np.int32), np.ones(len(ci)))
+        assert _analysis_host(A)[0] == 3
