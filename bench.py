@@ -137,12 +137,43 @@ def workload_names(w):
     return w.split(",")
 
 
+def host_cpu_facts():
+    """What the CPU baseline ran on: this process's CPU set (the box's share),
+    the machine's logical CPUs and the CPU model."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpuset_cpus": len(os.sched_getaffinity(0)), "machine_logical_cpus": os.cpu_count(), "model": model}
+
+
 def cpu_baseline(slices, seconds):
-    """Oracle OpenMP fp64 SpMV (test_spmv.c's CPU path restated) over the same
-    matrices, repeated until `seconds` of CPU work; GFLOP/s."""
+    """The reference's CPU path (test_spmv.c's CSR SpMV, restated by the
+    oracle as an OpenMP row-parallel loop) on the same matrices, two ways
+    (BASELINE.md §4):
+      B (value): all threads of this process's CPU set, steady-state mean,
+        repeated until `seconds` of CPU work;
+      A (method_a): the reference's own methodology - 4 threads
+        (run_spmv.sh:45 OMP_NUM_THREADS=4 taskset -c 0-3), ONE cold call per
+        matrix (test_spmv.c:165-183)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bind as ob
     xs = [csr.dlarnv(1, [0, 0, 0, 1], s.n)[0] for s in slices]
+    facts = host_cpu_facts()
+    threads_b = ob.lib.oracle_num_threads()
+    # method A first: 4 threads, one cold call per matrix
+    ob.lib.oracle_set_threads(4)
+    t_a, flops_a = 0.0, 0.0
+    for s, x in zip(slices, xs):
+        t0 = time.perf_counter()
+        ob.spmv(s.host[0], s.host[1], s.host[2], x, threads=True)
+        t_a += time.perf_counter() - t0
+        flops_a += 2.0 * s.nnz_local
+    ob.lib.oracle_set_threads(threads_b)
     for s, x in zip(slices, xs):  # warm (page-in) pass
         ob.spmv(s.host[0], s.host[1], s.host[2], x, threads=True)
     flops, t0, passes = 0.0, time.perf_counter(), 0
@@ -154,20 +185,32 @@ def cpu_baseline(slices, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": round(flops / el / 1e9, 3), "unit": "GFLOP/s", "cores": ob.lib.oracle_num_threads(),
+    return {"value": round(flops / el / 1e9, 3), "unit": "GFLOP/s", "cores": threads_b,
             "kind": "port",
-            "sample": f"{passes} full fp64 passes over the {len(slices)}-matrix workload "
-                      f"({el:.1f} s), OpenMP row-parallel CSR, x=dlarnv(1,{{0,0,0,1}})"}
+            "sample": f"method B: {passes} full fp64 passes over the {len(slices)}-matrix workload "
+                      f"({el:.1f} s), OpenMP row-parallel CSR on {threads_b} threads "
+                      f"(= this process's CPU set of {facts['cpuset_cpus']} CPUs), x=dlarnv(1,{{0,0,0,1}})",
+            "host": facts,
+            "method_a": {"value": round(flops_a / t_a / 1e9, 3), "unit": "GFLOP/s", "threads": 4,
+                         "note": "the reference's methodology: OMP_NUM_THREADS=4, one cold call per matrix "
+                                 "(run_spmv.sh:45, test_spmv.c:165-183), summed over the workload"}}
 
 
 def spmv_kernel_sha():
-    """sha256 (16 hex) of the SpMV kernel sources (spmv.hip + rsp_kernels.h):
-    the build a PMC summary must have been recorded for."""
+    """sha256 (16 hex) of the SpMV kernel sources — spmv.hip and the SpMV
+    part of rsp_kernels.h (schedule records, tile geometry, batch records: up
+    to the ILU level-schedule section) — the build a PMC summary must have been
+    recorded for. (The ILU declarations further down the header do not change
+    the SpMV kernel.)"""
     import hashlib
     hsh = hashlib.sha256()
-    for f in ("spmv.hip", "rsp_kernels.h"):
-        with open(os.path.join(ROOT, "respasol_amd", "csrc", f), "rb") as fh:
-            hsh.update(fh.read())
+    src = os.path.join(ROOT, "respasol_amd", "csrc")
+    with open(os.path.join(src, "spmv.hip"), "rb") as fh:
+        hsh.update(fh.read())
+    with open(os.path.join(src, "rsp_kernels.h"), "rb") as fh:
+        head = fh.read()
+    cut = head.find(b"// Level schedule of one dependency DAG.")
+    hsh.update(head if cut < 0 else head[:cut])
     return hsh.hexdigest()[:16]
 
 

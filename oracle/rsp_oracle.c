@@ -71,6 +71,7 @@ void oracle_spmv_f32_omp(int m, const int *rp, const int *ci, const float *v, co
 }
 
 int oracle_num_threads(void) { return omp_get_max_threads(); }
+void oracle_set_threads(int t) { omp_set_num_threads(t > 0 ? t : 1); }
 
 /* Canonical summation order of the GPU SpMV (spmv.hip), a function of the
  * row alone (independent of tiling, lanes per row and row partition):

@@ -44,6 +44,7 @@ void oracle_spmv_f64_omp(int m, const int *rowptr, const int *colidx, const doub
 void oracle_spmv_f32_omp(int m, const int *rowptr, const int *colidx, const float *vals,
                          const float *x, float *y);
 int oracle_num_threads(void);
+void oracle_set_threads(int threads); /* OpenMP threads of the _omp kernels */
 /* Same products in the CANONICAL summation order of the GPU SpMV (see
  * rsp_oracle.c): 8-way interleave + fixed tree for rows of <= 256 products,
  * chunked (cap = tile capacity: 2047 fp64 / 4093 fp32) 256-way interleave +

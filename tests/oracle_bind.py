@@ -28,6 +28,8 @@ def _load():
         getattr(lib, name).argtypes = [C.c_int, ip, ip, vp, vp, vp, C.c_int]
         getattr(lib, name).restype = None
     lib.oracle_num_threads.restype = C.c_int
+    lib.oracle_set_threads.argtypes = [C.c_int]
+    lib.oracle_set_threads.restype = None
     lib.oracle_ilu0_f64.argtypes = [C.c_int, ip, ip, vp, ip]
     lib.oracle_ilu0_f64.restype = C.c_int
     lib.oracle_ilu0_f32.argtypes = [C.c_int, ip, ip, vp, ip, C.c_int]
