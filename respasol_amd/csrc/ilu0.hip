@@ -731,6 +731,180 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
     y[t.i] = s;
 }
 
+// Flow segments (a solve DAG's runs of two or more fat levels): ONE launch of
+// a.flow_grid workgroups instead of a launch per level. Wave w of the grid
+// takes the segment's work items (rsp::FlowItem, level order) w, w + W, ...
+// (W = the grid's waves); an item starts as soon as the y values it reads
+// exist, not when its whole previous level has ended. Existence is read from
+// the value itself: trsv_stream sets every y to kNotYet, a signalling-NaN
+// bit pattern that no y can have (every y is an arithmetic result — alpha x_i,
+// an fma, a division — and arithmetic only produces quiet NaNs); a row's y is
+// written once, by one 4- / 8-byte device-scope (sc1) store, and a consumer
+// reads its operands with device-scope (sc1) loads, re-reading (after an
+// s_sleep) those still kNotYet: the data-tagged hand-off of the price list
+// in MI355X_MICROARCH.md (handoff-1to1) — no flag, no fence.
+// Deadlock-free: an item waits only for items of lower index, each wave runs
+// its items in index order, and the grid (one 4-wave workgroup per CU by
+// default) is resident at once, so the lowest unfinished item always makes
+// progress. A wait beyond kFlowTimeout (never expected) gives up and counts
+// in a.flow_timeouts (rsp_ilu0_zero_pivot then returns EXECUTION_FAILED)
+// instead of hanging the GPU.
+// Same terms, same order, same fma chain as trsv_level: the same bits.
+template <typename T>
+struct FlowWord;
+template <>
+struct FlowWord<double> {
+    typedef unsigned long long U;
+    static constexpr U kNotYet = 0x7ff5eed15eed1001ull;
+};
+template <>
+struct FlowWord<float> {
+    typedef unsigned int U;
+    static constexpr U kNotYet = 0x7fa5eed1u;
+};
+constexpr unsigned long long kFlowTimeout = 20000000ull;  // wall-clock ticks (100 MHz): 0.2 s
+
+template <typename T>
+__device__ __forceinline__ typename FlowWord<T>::U flow_load(const T *p) {
+    return __hip_atomic_load((typename FlowWord<T>::U *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void flow_store(T *p, T v) {
+    typedef typename FlowWord<T>::U U;
+    __hip_atomic_store((U *)p, __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Re-read this lane's operand words [0, n) that are still kNotYet until none
+// of the wave's is (wave-uniform loop; the pause between polls doubles up to
+// max_sleep s_sleep units of 64 clocks).
+template <typename T, int NB>
+__device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], const int (&id)[NB], int n,
+                                          const T *y, int *timeouts, int max_sleep) {
+    constexpr auto kNot = FlowWord<T>::kNotYet;
+    auto pending = [&] {
+        bool p = false;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) p |= b < n && w[b] == kNot;
+        return p;
+    };
+    if (!__ballot(pending())) return;
+    const unsigned long long t0 = wall_clock64();
+    for (int sl = 1;; sl = min(2 * sl, max_sleep)) {
+        for (int q = 0; q < sl; ++q) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            if (b < n && w[b] == kNot) w[b] = flow_load(y + id[b]);
+        if (!__ballot(pending())) return;
+        if (wall_clock64() - t0 > kFlowTimeout) {
+            if ((threadIdx.x & 63) == 0) atomicAdd(timeouts, 1);
+            return;
+        }
+    }
+}
+
+// An item's gate: before polling its own operands, a wave waits (one lane,
+// one word) for the y of the last row of the level three below its own (plan:
+// RSP_ILU_FLOW_GATE; 2 and 1 measured slower) — only
+// a throttle, so that waves whose items are far ahead of the progress front
+// poll one word instead of a word per operand (the operand polls alone, up to
+// 8 per lane, slowed the loads on the critical path). Row g's item has a
+// lower index, so the gate cannot deadlock.
+template <typename T>
+__device__ __forceinline__ void flow_gate(int g, const T *y, int *timeouts, int max_sleep) {
+    if (g < 0) return;
+    typename FlowWord<T>::U w[1] = {0};
+    int id[1] = {g};
+    if ((threadIdx.x & 63) == 0) w[0] = flow_load(y + g);
+    flow_wait<T, 1>(w, id, (threadIdx.x & 63) == 0 ? 1 : 0, y, timeouts, max_sleep);
+}
+
+template <typename T, int KIND>
+__global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1) {
+    typedef typename FlowWord<T>::U U;
+    constexpr int F = rsp::kFatLongTerms;
+    __shared__ T fwv[4][64], fwy[4][64];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int W = gridDim.x * 4;
+    const T *sval = (const T *)a.sval, *sx = (const T *)a.sx;
+    T *y = (T *)a.y;
+    const int *src = a.plan.src;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    };
+    for (int it = it0 + blockIdx.x * 4 + wv; it < it1; it += W) {
+        const rsp::FlowItem f = a.plan.fitems[it];
+        if (f.n > 0) {  // short rows, a lane each (lanes past them repeat the last row)
+            const int r = min(lane, f.n - 1), x = f.x0 + r;
+            const rsp::RowTask t = a.plan.tasks[x];
+            T v[F];
+            int id[F], n;
+            if (f.t0 >= 0) {  // padded: the terms load with the task
+                const int t0 = f.t0 + r * F;
+#pragma unroll
+                for (int b = 0; b < F; ++b) {
+                    v[b] = sval[t0 + b];
+                    id[b] = src[t0 + b];
+                }
+                n = t.t1 - t0;
+            } else {
+                n = t.t1 - t.t0;
+                const int kl = max(t.t1 - 1, 0);
+#pragma unroll
+                for (int b = 0; b < F; ++b) {
+                    const int k = min(t.t0 + b, kl);
+                    v[b] = sval[k];
+                    id[b] = src[k];
+                }
+            }
+            T s = sx[x];
+            flow_gate<T>(f.gate, y, a.flow_timeouts, a.flow_sleep);
+            U w[F];
+#pragma unroll
+            for (int b = 0; b < F; ++b) w[b] = b < n ? flow_load(y + id[b]) : U(0);
+            flow_wait<T, F>(w, id, n, y, a.flow_timeouts, a.flow_sleep);
+#pragma unroll
+            for (int b = 0; b < F; ++b)
+                if (b < n) s = fma_t(-v[b], __builtin_bit_cast(T, w[b]), s);
+            if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
+            if (lane < f.n) flow_store(y + t.i, s);
+        } else {  // one row of more terms: a wave, 64 terms at a time on LDS broadcast operands
+            const int x = f.x0;
+            const rsp::RowTask t = a.plan.tasks[x];
+            T s = sx[x];
+            flow_gate<T>(f.gate, y, a.flow_timeouts, a.flow_sleep);
+            for (int base = t.t0; base < t.t1; base += 64) {
+                const int k = min(base + lane, t.t1 - 1);
+                const T v = sval[k];
+                int id[1] = {src[k]};
+                U w[1] = {flow_load(y + id[0])};
+                flow_wait<T, 1>(w, id, 1, y, a.flow_timeouts, a.flow_sleep);
+                fwv[wv][lane] = v;
+                fwy[wv][lane] = __builtin_bit_cast(T, w[0]);
+                wave_sync();
+                const int cnt = min(64, t.t1 - base);
+                int j = 0;
+                for (; j + 4 <= cnt; j += 4) {
+                    T p[4], q[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        p[u] = fwv[wv][j + u];
+                        q[u] = fwy[wv][j + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) s = fma_t(-p[u], q[u], s);
+                }
+                for (; j < cnt; ++j) s = fma_t(-fwv[wv][j], fwy[wv][j], s);
+                wave_sync();  // this group's reads before the next group's stores
+            }
+            if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
+            if (lane == 0) flow_store(y + t.i, s);
+        }
+    }
+}
+
 // Thin run (levels cut into LDS-staged chunks [c0, c1)), one 1024-thread
 // workgroup. A chunk holds <= kChunkRows rows and <= kChunkTerms term slots;
 // every row of a thin run has its terms padded to whole groups of G = 4 (or 2,
@@ -792,6 +966,9 @@ __global__ __launch_bounds__(256) void trsv_stream(TrsvArgs a, T alpha) {
         const rsp::RowTask t = a.plan.tasks[k];
         ((T *)a.sx)[k] = alpha * ((const T *)a.x)[t.i];
         if constexpr (KIND == 2) ((T *)a.sdg)[k] = t.d >= 0 ? vals[t.d] : T(0);
+        // flow segments read "not produced yet" from y itself (trsv_flow);
+        // every other row's y is written by its own segment before any reader
+        if (a.flow && a.plan.has_flow) ((typename FlowWord<T>::U *)a.y)[t.i] = FlowWord<T>::kNotYet;
     }
 }
 
@@ -811,7 +988,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     __shared__ int lrowi[rsp::kChunkRows];
     __shared__ T ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
     __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];
+    __shared__ int lds_done;  // multi-wave narrow runs: absolute levels completed
     const int tid = threadIdx.x;
+    if (tid == 0) lds_done = INT_MIN;  // ordered before any use by the first chunk's barriers
     const T *sval = (const T *)a.sval, *sx = (const T *)a.sx, *sdg = (const T *)a.sdg;
     T *y = (T *)a.y;
     const int *ptr = a.plan.ptr_dev;
@@ -1046,6 +1225,60 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             p3 = p4;
         }
     };
+    // Narrow run on K waves (a.narrow_waves): wave w computes levels q0 + w,
+    // q0 + w + K, ... A level reads its row records, term indices and values
+    // first (nothing there depends on a y), then waits until the run's
+    // earlier levels are complete — an LDS counter of absolute levels done,
+    // advanced by each level's wave after its y stores — and only then does
+    // the critical part: y loads -> fma chain -> y stores. While one wave is
+    // on its critical part, the others prepare their next levels, so a level
+    // costs about its critical part alone (one wave did all of it in line).
+    // The counter store follows the y stores of the same wave with no wait:
+    // a wave's LDS operations are performed in order (compiler barrier only),
+    // and a waiting wave issues its y loads after its poll has returned.
+    // Same terms, same order, same fma chain as narrow_run: same bits.
+    auto narrow_run_mw = [&](const rsp::LevelChunk &ch, int q0, int q1, int K) {
+        const int w = tid >> 6, lane = tid & 63, x0 = ch.x0;
+        const int L0 = ch.l0 + q0;
+        for (int q = q0 + w; q < q1; q += K) {
+            const int p0 = lptr[q], p1 = lptr[q + 1];
+            const int cr = max(p0 - x0 + min(lane, p1 - p0 - 1), 0);
+            const ThinRow<T> R = lrow[cr];
+            const int g0 = R.g & 0xffff, ng = R.g >> 16;
+            const bool two = __ballot(ng >= 2) != 0;
+            const int gi = ng >= 2 ? g0 + 1 : kPadGroup;
+            const TermIds<G> i1 = lidx[g0];
+            const TermGroup<T, G> v1 = lval[g0];
+            TermIds<G> i2;
+            TermGroup<T, G> v2;
+            if (two) {
+                i2 = lidx[gi];
+                v2 = lval[gi];
+            }
+            const int L = ch.l0 + q;
+            if (L > L0) {
+                // bounded (a missing producer would be a plan bug: wrong
+                // bits in the tests, never a hung GPU)
+                for (int it = 0; it < (1 << 26) &&
+                                 __hip_atomic_load(&lds_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < L;
+                     ++it) {
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+            }
+            T s = group_fma(R.x, v1, i1);
+            if (two) {
+                s = group_fma(s, v2, i2);
+                if (__ballot(ng >= 3))
+                    for (int g = 2; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+            }
+            if constexpr (KIND == 2) s = s / ldg[cr];
+            put(R.out, s);
+            asm volatile("" ::: "memory");  // y stores before the counter (in-order LDS)
+            if (lane == 0) __hip_atomic_store(&lds_done, L + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (a.trace && lane == 0 && L < a.trace_cap / 2)  // diagnostics: level end stamps
+                a.trace[a.trace_cap / 2 + L] = a.trace_clk ? clock64() : wall_clock64();
+        }
+    };
     auto levels = [&](const rsp::LevelChunk &ch) {
         const int x0 = ch.x0, nl = ch.l1 - ch.l0;
 #if RSP_THIN_LONG_READLANE
@@ -1055,7 +1288,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         for (int q = 0; q < nl;) {
             if (narrow(q)) {
                 const int qe = run_end(q, nl);
-                if (tid < 64) {
+                const int K = min(a.narrow_waves, (int)(blockDim.x >> 6));  // waves of this launch
+                if (K > 1) {
+                    if (tid < 64 * K) narrow_run_mw(ch, q, qe, K);
+                } else if (tid < 64) {
                     if (a.trace)
                         narrow_run(ch, q, qe, std::true_type());
                     else
@@ -1195,6 +1431,11 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             else
                 hipLaunchKernelGGL((trsv_thin_pf<T, KIND, 4>), dim3(1), dim3(kThinThreads), 0, s, a,
                                    sg.c0, sg.c1, P.ptr_host[sg.lb]);
+            continue;
+        }
+        if (a.flow && sg.c1 > sg.c0) {  // flow segment: one persistent launch
+            const int grid = min(a.flow_grid, (sg.c1 - sg.c0 + 3) / 4);
+            hipLaunchKernelGGL((trsv_flow<T, KIND>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

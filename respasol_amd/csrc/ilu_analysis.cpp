@@ -160,6 +160,41 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
             t.d = diag.empty() ? -1 : diag[(size_t)i];
         }
     }
+    // flow segments: fat segments of two or more levels run as one persistent
+    // launch (trsv_flow) over work items in level order — a level's short rows
+    // in groups of 64 (a lane each), then its wave and hub rows (a wave each).
+    // Short rows must fit one batch of kFatLongTerms terms (RSP_ILU_FAT_LONG).
+    sp.fitems.clear();
+    const int gate_d = env_int("RSP_ILU_FLOW_GATE", 3);  // levels between an item and its gate (0: none)
+    if (fat_long <= rsp::kFatLongTerms && env_int("RSP_ILU_FLOW_PLAN", 1) != 0)
+        for (rsp::LevelSeg &sg : sp.segs) {
+            if (sg.thin || sg.le - sg.lb < 2) continue;
+            sg.c0 = (int)sp.fitems.size();
+            for (int l = sg.lb; l < sg.le; l++) {
+                const int p0 = ptr[(size_t)l], cnt = ptr[(size_t)l + 1] - p0, ns = sp.nshort[(size_t)l];
+                const int sb = sp.sbase[(size_t)l];
+                // gate: the last row of level l - gate_d when it is in this segment
+                const int lg = l - gate_d;
+                const int gate = gate_d > 0 && lg >= sg.lb && ptr[(size_t)lg + 1] > ptr[(size_t)lg]
+                                     ? order[(size_t)ptr[(size_t)lg + 1] - 1] : -1;
+                for (int r = 0; r < ns; r += 64)
+                    sp.fitems.push_back({p0 + r, std::min(64, ns - r), sb >= 0 ? sb + r * rsp::kFatLongTerms : -1, gate});
+                for (int r = ns; r < cnt; r++) sp.fitems.push_back({p0 + r, 0, -1, gate});
+            }
+            sg.c1 = (int)sp.fitems.size();
+        }
+    if (env_int("RSP_ILU_PLANSTATS", 0)) {  // diagnostics: the segment structure of this DAG
+        int nthin = 0, nfat = 0, nflow = 0, lthin = 0, lfat = 0, lflow = 0;
+        for (const rsp::LevelSeg &sg : sp.segs) {
+            const int nl = sg.le - sg.lb;
+            if (sg.thin) nthin++, lthin += nl;
+            else if (sg.c1 > sg.c0) nflow++, lflow += nl;
+            else nfat++, lfat += nl;
+        }
+        fprintf(stderr, "rsp_ilu0 plan n=%d levels=%d group=%d thin %d segs / %d levels, fat %d / %d, flow %d / %d (%zu items)\n",
+                n, nlev, group, nthin, lthin, nfat, lfat, nflow, lflow, sp.fitems.size());
+    }
+    if (sp.fitems.empty()) sp.fitems.push_back({0, 0, -1, -1});  // keep the device array non-empty
     std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
     for (int l = 0; l < nlev; l++)
         if (ptr[(size_t)l + 1] > ptr[(size_t)l])
@@ -890,6 +925,7 @@ uint64_t digest(const IluHostPlan &hp) {
         f.vec(d->sp.nshort);
         f.vec(d->sp.nwave);
         f.vec(d->sp.sbase);
+        f.vec(d->sp.fitems);
     }
     f.vec(hp.fplan.segs);
     f.vec(hp.fplan.chunks);

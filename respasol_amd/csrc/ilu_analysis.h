@@ -35,6 +35,7 @@ struct SolvePlan {
     std::vector<rsp::ThinRowPlan> trow;
     std::vector<int> sid;
     std::vector<rsp::StagedTerm> stg;
+    std::vector<rsp::FlowItem> fitems;  // flow segments' work items (LevelSeg c0 / c1 of a fat segment)
 };
 
 // Symbolic ILU(0) data (built by ilu_symbolic below).

@@ -97,6 +97,7 @@ struct rsp_ilu0_info {
         rsp::ThinRowPlan *d_trow = nullptr;    // solve: thin-run row records
         int *d_sid = nullptr;                  // solve: thin-run y indices per term
         rsp::StagedTerm *d_stg = nullptr;      // solve: thin-run staged terms
+        rsp::FlowItem *d_fitems = nullptr;     // solve: flow segments' work items
         int nterms = 0;                        // solve: flat terms
         int *d_nshort = nullptr;               // solve: short rows per level (device)
         std::vector<int> nshort;               // (host)
@@ -1065,6 +1066,7 @@ static void dag_upload(Arena &ar, rsp_ilu0_info::Dag &d, const rsp_an::DagHost &
     ar.up(&d.d_trow, h.sp.trow);
     ar.up(&d.d_sid, h.sp.sid);
     ar.up(&d.d_stg, h.sp.stg);
+    ar.up(&d.d_fitems, h.sp.fitems);
 }
 
 extern "C" {
@@ -1272,7 +1274,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     ar.space(&f->d_sval, nt * sizeof(double));
     ar.space(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
     ar.space(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
-    ar.space((void **)&f->d_zero, sizeof(int));
+    ar.space((void **)&f->d_zero, 2 * sizeof(int));  // zero pivot, flow time-outs
     int4 *d_desc = nullptr;
     long long *d_offs = nullptr;
     if (!hp->slot_desc.empty()) {
@@ -1281,6 +1283,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     }
     hipError_t e = ar.commit(&f->d_arena, h->stream);
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
+    if (e == hipSuccess) e = hipMemsetD32(f->d_zero + 1, 0, 1);
     // fat factor slots, written on the device from the uploaded symbolic
     // arrays; the layout is an optimisation: without its memory, or if the
     // build fails, the FacRow path factors every fat level (same bits)
@@ -1394,12 +1397,11 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
     *position = -1;
     if (!f->analysed) return RSP_STATUS_INVALID_VALUE;
     int pos = f->structural_zero;
-    if (f->factored) {
-        int z = INT_MAX;
-        RSP_CHECK_HIP(hipMemcpyAsync(&z, f->d_zero, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
-        if (z != INT_MAX && (pos < 0 || z < pos)) pos = z;
-    }
+    int z[2] = {INT_MAX, 0};  // zero pivot, flow time-outs of earlier solves
+    RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
+    RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    if (z[1] != 0) return RSP_STATUS_EXECUTION_FAILED;  // a flow solve gave up waiting: its y is wrong
+    if (f->factored && z[0] != INT_MAX && (pos < 0 || z[0] < pos)) pos = z[0];
     if (pos >= 0) {
         *position = pos;
         return RSP_STATUS_ZERO_PIVOT;
@@ -1426,6 +1428,9 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<
     p.trow = d.d_trow;
     p.sid = d.d_sid;
     p.stg = d.d_stg;
+    p.fitems = d.d_fitems;
+    p.has_flow = 0;
+    for (const rsp::LevelSeg &sg : segs) p.has_flow |= !sg.thin && sg.c1 > sg.c0;
     p.nterms = d.nterms;
     p.nshort = d.d_nshort;
     p.nshort_host = d.nshort.data();
@@ -1501,7 +1506,7 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
 }
 
-static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype_t t,
+static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alpha, rsp_datatype_t t,
                                const void *vals, const void *x, void *y) {
     rsp::TrsvArgs a;
     a.n = f->n;
@@ -1521,6 +1526,14 @@ static rsp::TrsvArgs trsv_args(rsp_ilu0_info *f, const void *alpha, rsp_datatype
     a.trace_cap = 0;
     a.trace_clk = 0;
     a.wave_lds = env_int("RSP_ILU_WAVE_LDS", 1);
+    a.narrow_waves = std::min(std::max(env_int("RSP_ILU_NARROW_WAVES", 4), 1), rsp::kThinThreads / 64);
+    a.flow = env_int("RSP_ILU_FLOW", 1) != 0;
+    // every workgroup of a flow launch must be resident at once (an item waits
+    // for items of lower index only, and workgroups take items in index
+    // order): 256-thread workgroups, RSP_ILU_FLOW_WPC (default 4) waves per CU
+    a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 4), 4), 16) / 4;
+    a.flow_timeouts = f->d_zero + 1;
+    a.flow_sleep = std::min(std::max(env_int("RSP_ILU_FLOW_SLEEP", 1), 1), 64);
     return a;
 }
 
@@ -1531,7 +1544,7 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
     if (!f || !f->analysed || !alpha) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
-    rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
+    rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
     // diagnostics: RSP_ILU_TRACE=<file> appends per-chunk timestamps of the
     // prefetching thin kernel (host-blocking; never set in timed runs)
     const char *trace_file = getenv("RSP_ILU_TRACE");
@@ -1586,7 +1599,7 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     rsp_status_t st = ilu_plan_u(h, f);  // planned on first use
     if (st != RSP_STATUS_SUCCESS) return st;
-    rsp::TrsvArgs a = trsv_args(f, alpha, value_type, d_values, d_x, d_y);
+    rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
     a.plan = level_plan(f->U, f->U.segs, f->U.batch);
     a.sval = f->d_usval;
     hipError_t e;

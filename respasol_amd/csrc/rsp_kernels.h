@@ -126,6 +126,10 @@ constexpr int kSpmvVariantFixup = 256;
 // barriers between levels (one launch for the whole run; a solve run is cut
 // into LDS-staged chunks [c0, c1) of `chunks`); a fat segment is one launch
 // per level.
+//
+// A solve DAG's fat segment of two or more levels is a FLOW segment: c0 / c1
+// delimit its work items (FlowItem), which one persistent launch runs in
+// order, each item waiting only for the y values it reads (trsv_flow).
 struct LevelSeg {
     int lb, le, thin, c0, c1;
     int nth;  // thin solve runs: workgroup size (64 / 256 / 1024, >= the run's widest level)
@@ -141,6 +145,13 @@ struct alignas(16) LevelChunk {  // levels [l0, l1) of a thin solve run, staged 
     int x0, x1;    // its level-order slots: ptr[l0], ptr[l1]
     int k0, k1;    // its flat terms: tasks[x0].t0, tasks[x1 - 1].t1
     int st0, st1;  // its staged terms: stg[st0 .. st1)
+};
+// Work item of a flow segment (level order): n > 0 = short rows x0 .. x0+n-1
+// (<= 64, a lane each; t0 >= 0: the padded layout, row r's kFatLongTerms flat
+// terms at t0 + r * kFatLongTerms), n == 0 = the one row at slot x0, a wave;
+// gate = a row of an earlier level to wait for first (-1 = none; trsv_flow).
+struct alignas(16) FlowItem {
+    int x0, n, t0, gate;
 };
 // Static LDS record of a thin-run row (per level-order slot): first term group
 // (chunk-relative) | groups << 16, its y window slot, the row, its diagonal.
@@ -171,6 +182,8 @@ struct LevelPlan {
     const ThinRowPlan *trow;  // thin runs: static row records (per level-order slot)
     const int *sid;       // thin runs: per term, its y's index in the LDS y buffer
     const StagedTerm *stg;  // thin runs: staged terms, per chunk [st0, st1)
+    const FlowItem *fitems; // flow segments: work items, per segment [c0, c1)
+    int has_flow;           // the DAG has a flow segment
     int nterms;           // flat terms
     const int *nshort;    // per level: short rows come first (host copy: nshort_host)
     const int *nshort_host;
@@ -292,6 +305,11 @@ struct TrsvArgs {
     int trace_cap;
     int trace_clk;              // level stamps in shader clock cycles (s_memtime) instead
     int wave_lds;               // fat-level wave rows: chain on LDS broadcast operands (RSP_ILU_WAVE_LDS)
+    int narrow_waves;           // thin runs: waves sharing a narrow run, levels round-robin (RSP_ILU_NARROW_WAVES)
+    int flow;                   // run flow segments persistently (RSP_ILU_FLOW, default 1)
+    int flow_grid;              // flow launch: 256-thread workgroups (RSP_ILU_FLOW_WPC waves per CU)
+    int *flow_timeouts;         // device counter: flow waits that gave up (never expected)
+    int flow_sleep;             // flow polls: longest pause, s_sleep units (RSP_ILU_FLOW_SLEEP)
 };
 
 }  // namespace rsp

@@ -44,6 +44,7 @@ def gpu_ilu(handle, A, dtype, ftz=False, x=None, true_lu=False):
     z = il.solve_lower(va, xx)
     y = il.solve_upper(va, z) if true_lu else il.solve_lower(va, z, transpose=True)
     torch.cuda.synchronize()
+    assert il.zero_pivot() == zp  # (raises if a flow solve gave up waiting)
     handle.set_ftz(False)
     return va.cpu().numpy(), zp, z.cpu().numpy(), y.cpu().numpy(), il
 
@@ -308,3 +309,30 @@ def test_device_analysis_same_plan_as_host(handle, monkeypatch, name, scale):
     assert dev.value == hst.value
     assert il.levels() == (lo.value, up.value)
     il.close()
+
+
+@pytest.mark.parametrize("waves", [1, 2, 3, 8])
+@pytest.mark.parametrize("name,scale", [("dc1", 1.0), ("G2_circuit", 0.5), ("thermomech_TK", 0.5)])
+def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, name, scale):
+    """Narrow solve levels on one wave, or shared round-robin by 2-8 waves (an
+    LDS counter of completed levels orders them; the default is 4): bitwise
+    equal to the oracle for L, L^T and the U extension, fp64 and fp32."""
+    monkeypatch.setenv("RSP_ILU_NARROW_WAVES", str(waves))
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float64, handle, x=x)
+    compare(A, torch.float32, handle, x=x, true_lu=True)
+
+
+@pytest.mark.parametrize("flow,wpc", [(0, 8), (1, 4), (1, 8), (1, 16)])
+@pytest.mark.parametrize("name,scale", [("xenon2", 0.3), ("offshore", 0.2), ("cfd2", 0.3), ("ss1", 0.2)])
+def test_flow_segments(handle, monkeypatch, flow, wpc, name, scale):
+    """Fat solve segments as one persistent launch (trsv_flow: items start
+    when the y they read exist, read from y itself) or a launch per level,
+    2-4 workgroups per CU: bitwise equal to the oracle for L, L^T and U."""
+    monkeypatch.setenv("RSP_ILU_FLOW", str(flow))
+    monkeypatch.setenv("RSP_ILU_FLOW_WPC", str(wpc))
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float64, handle, x=x)
+    compare(A, torch.float32, handle, x=x, true_lu=True)
