@@ -302,6 +302,79 @@ __global__ __launch_bounds__(64) void ilu0_level_lds(IluArgs a, int off) {
     for (int x = lane; x < nr; x += 64) vals[rs + x] = rv[x];
 }
 
+// ------------------------------------------------- flow hand-offs (helpers)
+// Words handed between workgroups of one persistent launch (trsv_flow,
+// ilu0_flow): written once by a 4- / 8-byte device-scope (sc1) store, read by
+// device-scope (sc1) loads, which bypass the reader's L1 — MI355X_MICROARCH.md
+// (inter-workgroup visibility; price list, handoff-1to1 / handoff-flag).
+template <typename T>
+struct FlowWord;
+template <>
+struct FlowWord<double> {
+    typedef unsigned long long U;
+    static constexpr U kNotYet = 0x7ff5eed15eed1001ull;
+};
+template <>
+struct FlowWord<float> {
+    typedef unsigned int U;
+    static constexpr U kNotYet = 0x7fa5eed1u;
+};
+constexpr unsigned long long kFlowTimeout = 20000000ull;  // wall-clock ticks (100 MHz): 0.2 s
+
+template <typename T>
+__device__ __forceinline__ typename FlowWord<T>::U flow_load(const T *p) {
+    return __hip_atomic_load((typename FlowWord<T>::U *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void flow_store(T *p, T v) {
+    typedef typename FlowWord<T>::U U;
+    __hip_atomic_store((U *)p, __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Re-read this lane's operand words [0, n) that are still kNotYet until none
+// of the wave's is (wave-uniform loop; the pause between polls doubles up to
+// max_sleep s_sleep units of 64 clocks).
+template <typename T, int NB>
+__device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], const int (&id)[NB], int n,
+                                          const T *y, int *timeouts, int max_sleep) {
+    constexpr auto kNot = FlowWord<T>::kNotYet;
+    auto pending = [&] {
+        bool p = false;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) p |= b < n && w[b] == kNot;
+        return p;
+    };
+    if (!__ballot(pending())) return;
+    const unsigned long long t0 = wall_clock64();
+    for (int sl = 1;; sl = min(2 * sl, max_sleep)) {
+        for (int q = 0; q < sl; ++q) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            if (b < n && w[b] == kNot) w[b] = flow_load(y + id[b]);
+        if (!__ballot(pending())) return;
+        if (wall_clock64() - t0 > kFlowTimeout) {
+            if ((threadIdx.x & 63) == 0) atomicAdd(timeouts, 1);
+            return;
+        }
+    }
+}
+
+// An item's gate: before polling its own operands, a wave waits (one lane,
+// one word) for the y of the last row of the level three below its own (plan:
+// RSP_ILU_FLOW_GATE; 2 and 1 measured slower) — only
+// a throttle, so that waves whose items are far ahead of the progress front
+// poll one word instead of a word per operand (the operand polls alone, up to
+// 8 per lane, slowed the loads on the critical path). Row g's item has a
+// lower index, so the gate cannot deadlock.
+template <typename T>
+__device__ __forceinline__ void flow_gate(int g, const T *y, int *timeouts, int max_sleep) {
+    if (g < 0) return;
+    typename FlowWord<T>::U w[1] = {0};
+    int id[1] = {g};
+    if ((threadIdx.x & 63) == 0) w[0] = flow_load(y + g);
+    flow_wait<T, 1>(w, id, (threadIdx.x & 63) == 0 ? 1 : 0, y, timeouts, max_sleep);
+}
+
 // Fat level in the slot layout (rsp::FacSlotLevel): the row's structure is
 // one fixed-stride slot, so its header, divisor positions, packed stage
 // structure and update pairs are one memory round trip, issued together
@@ -371,6 +444,144 @@ __global__ __launch_bounds__(64) void ilu0_level_slot(IluArgs a, const int *__re
     }
     row_lds_factor<T>(rv, dv, pu, up, lo, le, pl, nlo, nr, lane, hasdiag, i, a.zero_pivot);
     for (int x = lane; x < nr; x += 64) vals[rs + x] = rv[x];
+}
+
+// Poll the per-row done flags of this lane's wanted rows (need[b]) until each
+// reads gen (wave-uniform loop, bounded like flow_wait).
+template <int NB>
+__device__ __forceinline__ void flag_wait(const int (&row)[NB], const bool (&need)[NB], const int *fdone, int gen,
+                                          int *timeouts, int max_sleep) {
+    bool miss[NB];
+    bool any = false;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        miss[b] = need[b] && __hip_atomic_load((int *)fdone + row[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen;
+        any |= miss[b];
+    }
+    if (!__ballot(any)) return;
+    const unsigned long long t0 = wall_clock64();
+    for (int sl = 1;; sl = min(2 * sl, max_sleep)) {
+        for (int q = 0; q < sl; ++q) __builtin_amdgcn_s_sleep(1);
+        any = false;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            if (miss[b])
+                miss[b] = __hip_atomic_load((int *)fdone + row[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen;
+            any |= miss[b];
+        }
+        if (!__ballot(any)) return;
+        if (wall_clock64() - t0 > kFlowTimeout) {
+            if ((threadIdx.x & 63) == 0) atomicAdd(timeouts, 1);
+            return;
+        }
+    }
+}
+
+// Flow run of the factor (rsp::FacFlowRun): ONE launch of a.flow_grid
+// workgroups over the run's rows in level order instead of a launch per fat
+// level. Wave w takes items w, w + W, ... (W = the grid's waves); a row waits
+// for the rows it reads — the columns k of its lower entries, whose u_kk and
+// u_kj are its operands — only where those rows are inside this run (level >=
+// lb; earlier rows finished in earlier launches), by their done flags: the
+// producing wave stores its row's values device-scope (sc1, write-through),
+// waits for them (s_waitcnt vmcnt(0)), then stores its flag = this call's
+// generation (sc1); the consumer polls the flags with sc1 loads and only then
+// reads the operands with sc1 loads (MI355X_MICROARCH.md, the valid hand-off
+// form: one signalling wave per storing wave, every load of the handed-off
+// bytes sc1, one workgroup per CU). A gate row three levels back is awaited
+// first (one word) so that waves far ahead of the front poll little. Flags
+// carry the call's generation, so nothing is reset between calls.
+// Deadlock-free as trsv_flow (items wait for lower items only; the grid is
+// resident); a wait past kFlowTimeout gives up and counts in flow_timeouts.
+// Structure and arithmetic as ilu0_level_slot (the level's rm / qm at run
+// time, budgets KR / KQ at their maximum): the same bits.
+template <typename T>
+__global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, int lb) {
+    constexpr int R = rsp::kFacRow, Q = rsp::kFacPairs, KR = R / 64, KQ = Q / 64;
+    __shared__ T rv_[4][R], dv_[4][R], pu_[4][Q];
+    __shared__ int up_[4][R + 1], lo_[4][R], le_[4][R];
+    __shared__ unsigned short pl_[4][Q];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int W = gridDim.x * 4;
+    T *rv = rv_[wv], *dv = dv_[wv], *pu = pu_[wv];
+    int *up = up_[wv], *lo = lo_[wv], *le = le_[wv];
+    unsigned short *pl = pl_[wv];
+    T *vals = (T *)a.vals;
+    for (int it = it0 + blockIdx.x * 4 + wv; it < it1; it += W) {
+        const rsp::FacFlowItem f = a.fitems[it];
+        const int *slot = a.fslots + f.off;
+        const int rm = f.rmqm & 0xffff, qm = f.rmqm >> 16, pa = rsp::fac_pairs_at(rm);
+        int dpos_[KR], bw[KR], dep[KR];
+        int2 pr[KQ];
+#pragma unroll
+        for (int k = 0; k < KR; ++k)
+            if (64 * k < rm) {
+                const int x = min(lane + 64 * k, rm - 1);
+                dpos_[k] = slot[8 + x];
+                bw[k] = slot[8 + rm + x];
+            }
+#pragma unroll
+        for (int k = 0; k < KQ; ++k)
+            if (64 * k < qm) pr[k] = *reinterpret_cast<const int2 *>(slot + pa + 2 * min(lane + 64 * k, qm - 1));
+        const int i = slot[0], rs = slot[1], nlo = slot[2], nr = slot[3], nq = slot[4], hasdiag = slot[5];
+        // the rows this row reads, and whether each is inside the run
+        bool need[KR];
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            const int x = lane + 64 * k;
+            dep[k] = x < nlo ? a.colidx[rs + x] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < KR; ++k) need[k] = lane + 64 * k < nlo && a.lev[dep[k]] >= lb;
+        T av[KR];
+#pragma unroll
+        for (int k = 0; k < KR; ++k)
+            if (64 * k < rm) av[k] = vals[rs + min(lane + 64 * k, max(nr - 1, 0))];  // the row's own a_ij
+        if (f.gate >= 0) {
+            int g[1] = {f.gate};
+            bool gn[1] = {lane == 0};
+            flag_wait<1>(g, gn, a.fdone, a.gen, a.flow_timeouts, a.flow_sleep);
+        }
+        flag_wait<KR>(dep, need, a.fdone, a.gen, a.flow_timeouts, a.flow_sleep);
+        T dd[KR], uv[KQ];
+#pragma unroll
+        for (int k = 0; k < KR; ++k)
+            if (64 * k < rm) {
+                typedef typename FlowWord<T>::U U;
+                const U b = flow_load(vals + max(dpos_[k], 0));
+                dd[k] = __builtin_bit_cast(T, b);
+            }
+#pragma unroll
+        for (int k = 0; k < KQ; ++k)
+            if (64 * k < qm) uv[k] = __builtin_bit_cast(T, flow_load(vals + pr[k].x));
+        if (nr > 0) {
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                const int x = lane + 64 * k;
+                if (64 * k < rm && x < nr) {
+                    rv[x] = av[k];
+                    dv[x] = dpos_[k] >= 0 ? dd[k] : T(0);
+                    up[x] = bw[k] & 0x7ff;
+                    lo[x] = (bw[k] >> 11) & 0x1ff;
+                    le[x] = (bw[k] >> 20) & 0x1ff;
+                }
+            }
+            if (lane == 0) up[nr] = nq;
+#pragma unroll
+            for (int k = 0; k < KQ; ++k) {
+                const int u = lane + 64 * k;
+                if (64 * k < qm && u < nq) {
+                    pl[u] = (unsigned short)pr[k].y;
+                    pu[u] = uv[k];
+                }
+            }
+            row_lds_factor<T>(rv, dv, pu, up, lo, le, pl, nlo, nr, lane, hasdiag, i, a.zero_pivot);
+            for (int x = lane; x < nr; x += 64) flow_store(vals + rs + x, rv[x]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the row's stores performed before its flag
+        if (lane == 0) __hip_atomic_store(a.fdone + i, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // Thin run of the factor in ROUNDS (plan: build_factor_plan; rsp::RndChunk,
@@ -750,74 +961,6 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
 // in a.flow_timeouts (rsp_ilu0_zero_pivot then returns EXECUTION_FAILED)
 // instead of hanging the GPU.
 // Same terms, same order, same fma chain as trsv_level: the same bits.
-template <typename T>
-struct FlowWord;
-template <>
-struct FlowWord<double> {
-    typedef unsigned long long U;
-    static constexpr U kNotYet = 0x7ff5eed15eed1001ull;
-};
-template <>
-struct FlowWord<float> {
-    typedef unsigned int U;
-    static constexpr U kNotYet = 0x7fa5eed1u;
-};
-constexpr unsigned long long kFlowTimeout = 20000000ull;  // wall-clock ticks (100 MHz): 0.2 s
-
-template <typename T>
-__device__ __forceinline__ typename FlowWord<T>::U flow_load(const T *p) {
-    return __hip_atomic_load((typename FlowWord<T>::U *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void flow_store(T *p, T v) {
-    typedef typename FlowWord<T>::U U;
-    __hip_atomic_store((U *)p, __builtin_bit_cast(U, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Re-read this lane's operand words [0, n) that are still kNotYet until none
-// of the wave's is (wave-uniform loop; the pause between polls doubles up to
-// max_sleep s_sleep units of 64 clocks).
-template <typename T, int NB>
-__device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], const int (&id)[NB], int n,
-                                          const T *y, int *timeouts, int max_sleep) {
-    constexpr auto kNot = FlowWord<T>::kNotYet;
-    auto pending = [&] {
-        bool p = false;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) p |= b < n && w[b] == kNot;
-        return p;
-    };
-    if (!__ballot(pending())) return;
-    const unsigned long long t0 = wall_clock64();
-    for (int sl = 1;; sl = min(2 * sl, max_sleep)) {
-        for (int q = 0; q < sl; ++q) __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-            if (b < n && w[b] == kNot) w[b] = flow_load(y + id[b]);
-        if (!__ballot(pending())) return;
-        if (wall_clock64() - t0 > kFlowTimeout) {
-            if ((threadIdx.x & 63) == 0) atomicAdd(timeouts, 1);
-            return;
-        }
-    }
-}
-
-// An item's gate: before polling its own operands, a wave waits (one lane,
-// one word) for the y of the last row of the level three below its own (plan:
-// RSP_ILU_FLOW_GATE; 2 and 1 measured slower) — only
-// a throttle, so that waves whose items are far ahead of the progress front
-// poll one word instead of a word per operand (the operand polls alone, up to
-// 8 per lane, slowed the loads on the critical path). Row g's item has a
-// lower index, so the gate cannot deadlock.
-template <typename T>
-__device__ __forceinline__ void flow_gate(int g, const T *y, int *timeouts, int max_sleep) {
-    if (g < 0) return;
-    typename FlowWord<T>::U w[1] = {0};
-    int id[1] = {g};
-    if ((threadIdx.x & 63) == 0) w[0] = flow_load(y + g);
-    flow_wait<T, 1>(w, id, (threadIdx.x & 63) == 0 ? 1 : 0, y, timeouts, max_sleep);
-}
-
 template <typename T, int KIND>
 __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1) {
     typedef typename FlowWord<T>::U U;
@@ -1381,9 +1524,25 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
 
 // --------------------------------------------------------------- launchers
 
+// Workgroups of a flow launch: every one must be resident at once (a wait is
+// for lower items only, so the lowest unfinished item must be running). The
+// occupancy query, less one workgroup per CU of margin (it can overstate by
+// one, MI355X_MICROARCH.md residency notes), caps the requested grid.
+template <auto KERNEL>
+static int flow_grid(int want, int cus, int items) {
+    static int occ = 0;  // per kernel
+    if (occ == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KERNEL, 256, 0) != hipSuccess) nb = 1;
+        occ = max(nb - 1, 1);
+    }
+    return max(1, min(min(want, cus * occ), (items + 3) / 4));
+}
+
 template <typename T, int B>
 static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
     const LevelPlan &P = a.plan;
+    int fr = 0;  // next flow run (sorted by level)
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
@@ -1391,6 +1550,14 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {
+            while (fr < a.nfruns && a.fruns[fr].lb < l) ++fr;
+            if (a.flow && fr < a.nfruns && a.fruns[fr].lb == l) {  // flow run: one persistent launch
+                const rsp::FacFlowRun r = a.fruns[fr];
+                const int grid = flow_grid<ilu0_flow<T>>(a.flow_grid, a.flow_cus, r.c1 - r.c0);
+                hipLaunchKernelGGL((ilu0_flow<T>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, r.lb);
+                l = r.le - 1;
+                continue;
+            }
             const int off = P.ptr_host[l], cnt = P.ptr_host[l + 1] - off;
             if (cnt <= 0) continue;
             const rsp::FacSlotLevel *sl = a.fat_slots && a.fslev ? &a.fslev[l] : nullptr;
@@ -1434,7 +1601,7 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             continue;
         }
         if (a.flow && sg.c1 > sg.c0) {  // flow segment: one persistent launch
-            const int grid = min(a.flow_grid, (sg.c1 - sg.c0 + 3) / 4);
+            const int grid = flow_grid<trsv_flow<T, KIND>>(a.flow_grid, a.flow_cus, sg.c1 - sg.c0);
             hipLaunchKernelGGL((trsv_flow<T, KIND>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1);
             continue;
         }

@@ -852,6 +852,50 @@ void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, 
         }
     }
     hp.slot_total = total;
+    // flow runs: maximal runs of >= 2 slot-layout fat levels without
+    // global-path rows; items in level order, gated like the solve's
+    hp.fruns.clear();
+    hp.ffitems.clear();
+    if (env_int("RSP_ILU_FLOW_PLAN", 1) != 0) {
+        const int gate_d = env_int("RSP_ILU_FLOW_GATE", 3);
+        auto flowable = [&](int l) {
+            const rsp::FacSlotLevel &sl = hp.fslev[(size_t)l];
+            if (sl.stride <= 0) return false;
+            for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
+                const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
+                if (re - rs > rsp::kFacRow || sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs] > rsp::kFacPairs)
+                    return false;
+            }
+            return true;
+        };
+        for (const rsp::LevelSeg &sg : hp.fplan.segs) {
+            if (sg.thin) continue;
+            for (int l = sg.lb; l < sg.le;) {
+                if (!flowable(l)) {
+                    l++;
+                    continue;
+                }
+                int e = l + 1;
+                while (e < sg.le && flowable(e)) e++;
+                if (e - l >= 2) {
+                    rsp::FacFlowRun r{l, e, (int)hp.ffitems.size(), 0};
+                    for (int v = l; v < e; v++) {
+                        const rsp::FacSlotLevel &sl = hp.fslev[(size_t)v];
+                        const int lg = v - gate_d;
+                        const int gate = gate_d > 0 && lg >= l && lp[(size_t)lg + 1] > lp[(size_t)lg]
+                                             ? rows_l[(size_t)lp[(size_t)lg + 1] - 1] : -1;
+                        for (int x = lp[(size_t)v]; x < lp[(size_t)v + 1]; x++)
+                            hp.ffitems.push_back({sl.off + (long long)(x - lp[(size_t)v]) * sl.stride,
+                                                  sl.rm | sl.qm << 16, gate});
+                    }
+                    r.c1 = (int)hp.ffitems.size();
+                    hp.fruns.push_back(r);
+                }
+                l = e;
+            }
+        }
+    }
+    if (hp.ffitems.empty()) hp.ffitems.push_back({0, 0, -1});  // keep the device array non-empty
     for (int l : slot_levels) {
         const rsp::FacSlotLevel &sl = hp.fslev[(size_t)l];
         for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
@@ -937,6 +981,8 @@ uint64_t digest(const IluHostPlan &hp) {
     f.vec(hp.fslev);
     f.vec(hp.slot_desc);
     f.vec(hp.slot_offs);
+    f.vec(hp.fruns);
+    f.vec(hp.ffitems);
     return f.h;
 }
 

@@ -76,6 +76,9 @@ struct IluHostPlan {
     std::vector<int4> slot_desc;
     std::vector<long long> slot_offs;
     long long slot_total = 0;
+    // flow runs of the factor (rsp::FacFlowRun / FacFlowItem)
+    std::vector<rsp::FacFlowRun> fruns;
+    std::vector<rsp::FacFlowItem> ffitems;
 };
 
 // Phase timer (RSP_ILU_TIMING=1 prints; phase_ms collects when given).

@@ -113,6 +113,11 @@ struct rsp_ilu0_info {
     rsp::RndItem *d_ritems = nullptr;
     rsp::FacRow *d_frow = nullptr;
     int *d_fslots = nullptr;                   // fat factor levels, slot layout (ilu0_level_slot)
+    std::vector<rsp::FacFlowRun> fruns;        // factor flow runs (ilu0_flow)
+    rsp::FacFlowItem *d_ffitems = nullptr;
+    int *d_lev = nullptr;                      // L level of each row
+    int *d_fdone = nullptr;                    // per row: generation of the factor call that finished it
+    int fac_gen = 0;
     std::vector<rsp::FacSlotLevel> fslev;      // per L level (stride 0: FacRow path)
     int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
     int fac_batch;
@@ -959,6 +964,9 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     f->d_upd_ptr = f->d_upd_l = f->d_upd_u = f->d_lord = f->d_lend = f->d_udiv = nullptr;
     f->d_sval = f->d_sx = f->d_sdg = nullptr;
     f->fslev.clear();
+    f->fruns.clear();
+    f->d_ffitems = nullptr;
+    f->d_lev = f->d_fdone = nullptr;
     f->d_frow = nullptr;
     f->d_rchunks = nullptr;
     f->d_ritems = nullptr;
@@ -1267,6 +1275,15 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     ar.up(&f->d_rstaged, hp->fplan.staged);
     ar.up(&f->d_rrounds, hp->fplan.rounds);
     ar.up(&f->d_frow, hp->frow);
+    ar.up(&f->d_ffitems, hp->ffitems);
+    f->fruns = hp->fruns;
+    // the L level of each row (flow runs: which producers are inside the run;
+    // kept alive until the commit below copies it)
+    std::vector<int> lev((size_t)std::max(n, 1), 0);
+    for (size_t l = 0; l + 1 < hp->L.ptr.size(); l++)
+        for (int x = hp->L.ptr[l]; x < hp->L.ptr[l + 1]; x++) lev[(size_t)hp->L.rows[(size_t)x]] = (int)l;
+    ar.up(&f->d_lev, lev);
+    ar.space((void **)&f->d_fdone, (size_t)std::max(n, 1) * sizeof(int));
     dag_upload(ar, f->L, hp->L);
     dag_upload(ar, f->LT, hp->LT);
     // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
@@ -1284,6 +1301,8 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     hipError_t e = ar.commit(&f->d_arena, h->stream);
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero + 1, 0, 1);
+    if (e == hipSuccess) e = hipMemsetD32(f->d_fdone, 0, (size_t)std::max(n, 1));
+    f->fac_gen = 0;
     // fat factor slots, written on the device from the uploaded symbolic
     // arrays; the layout is an optimisation: without its memory, or if the
     // build fails, the FacRow path factors every fat level (same bits)
@@ -1310,6 +1329,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
             if (f->d_fslots) (void)hipFree(f->d_fslots);
             f->d_fslots = nullptr;
             f->fslev.assign(f->fslev.size(), rsp::FacSlotLevel{0, 0, 0, 0, 0});
+            f->fruns.clear();  // the flow runs read the slots too
         }
     }
     ph.mark("upload");
@@ -1470,6 +1490,21 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.rstaged = f->d_rstaged;
     a.rrounds = f->d_rrounds;
     a.plan = level_plan(f->L, f->fac_segs, f->fac_batch);
+    a.fitems = f->d_ffitems;
+    a.fruns = f->fruns.empty() ? nullptr : f->fruns.data();
+    a.nfruns = a.fat_slots ? (int)f->fruns.size() : 0;
+    a.lev = f->d_lev;
+    a.fdone = f->d_fdone;
+    if (f->fac_gen >= (1 << 30)) {  // generations wrap: clear the flags
+        RSP_CHECK_HIP(hipMemsetD32Async(f->d_fdone, 0, (size_t)std::max(f->n, 1), h->stream));
+        f->fac_gen = 0;
+    }
+    a.gen = ++f->fac_gen;
+    a.flow = env_int("RSP_ILU_FLOW", 1) != 0;
+    a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 4), 4), 16) / 4;
+    a.flow_cus = h->num_cus;
+    a.flow_sleep = std::min(std::max(env_int("RSP_ILU_FLOW_SLEEP", 1), 1), 64);
+    a.flow_timeouts = f->d_zero + 1;
     // diagnostics: RSP_ILU_FTRACE=<file> appends per-chunk shader-clock stamps
     // of the thin factor runs (host-blocking; never set in timed runs)
     const char *trace_file = getenv("RSP_ILU_FTRACE");
@@ -1532,6 +1567,7 @@ static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alp
     // for items of lower index only, and workgroups take items in index
     // order): 256-thread workgroups, RSP_ILU_FLOW_WPC (default 4) waves per CU
     a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 4), 4), 16) / 4;
+    a.flow_cus = h->num_cus;
     a.flow_timeouts = f->d_zero + 1;
     a.flow_sleep = std::min(std::max(env_int("RSP_ILU_FLOW_SLEEP", 1), 1), 64);
     return a;

@@ -251,6 +251,20 @@ struct FacSlotLevel {
 };
 __host__ __device__ constexpr int fac_pairs_at(int rm) { return (8 + 2 * rm + 1) & ~1; }
 
+// Flow runs of the factor: two or more consecutive fat levels, all in the
+// slot layout and without global-path rows, run as ONE persistent launch
+// (ilu0_flow) over their rows in level order, a row starting when the rows it
+// reads are done (per-row flags). A run: levels [lb, le), items [c0, c1).
+// An item: its row's slot (fslots offset), the level's rm | qm << 16, and a
+// row of an earlier level to wait for first (gate, -1 = none).
+struct alignas(16) FacFlowItem {
+    long long off;
+    int rmqm, gate;
+};
+struct FacFlowRun {
+    int lb, le, c0, c1;
+};
+
 struct IluArgs {
     int n;
     const int *rowptr;
@@ -285,6 +299,16 @@ struct IluArgs {
     unsigned long long *trace;  // diagnostics (RSP_ILU_FTRACE): 4 words per thin-run chunk, or null
     int trace_cap;
     int defer_rounds;  // narrow runs of at least this many rounds flush their items after the run
+    // flow runs (ilu0_flow)
+    const FacFlowItem *fitems;  // device
+    const FacFlowRun *fruns;    // host
+    int nfruns;
+    const int *lev;             // device: L level of each row
+    int *fdone;                 // device: per row, the generation of the factor that finished it
+    int gen;                    // this factor call's generation (>= 1)
+    int flow, flow_grid, flow_sleep;
+    int flow_cus;               // CUs of the device (residency cap of a flow grid)
+    int *flow_timeouts;
 };
 
 struct TrsvArgs {
@@ -308,6 +332,7 @@ struct TrsvArgs {
     int narrow_waves;           // thin runs: waves sharing a narrow run, levels round-robin (RSP_ILU_NARROW_WAVES)
     int flow;                   // run flow segments persistently (RSP_ILU_FLOW, default 1)
     int flow_grid;              // flow launch: 256-thread workgroups (RSP_ILU_FLOW_WPC waves per CU)
+    int flow_cus;               // CUs of the device (residency cap of a flow grid)
     int *flow_timeouts;         // device counter: flow waits that gave up (never expected)
     int flow_sleep;             // flow polls: longest pause, s_sleep units (RSP_ILU_FLOW_SLEEP)
 };

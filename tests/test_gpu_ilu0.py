@@ -93,7 +93,13 @@ def test_identity(handle):
     assert zp == -1 and np.all(y == 1.0)
 
 
-def test_numerical_zero_pivot(handle):
+@pytest.mark.parametrize("fat", [False, True])
+def test_numerical_zero_pivot(handle, monkeypatch, fat):
+    """u_11 = 0 after the update; with every level forced fat the three
+    one-row levels form a flow run (ilu0_flow) that still reports it."""
+    if fat:
+        monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
+        monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
     A = csr.CsrMatrix(0, 3, 3, 7, np.array([0, 2, 4, 7], np.int32),
                       np.array([0, 1, 0, 1, 0, 1, 2], np.int32), np.array([1, 1, 1, 1, 1, 1, 1.0]))
     v, zp, _, _, _ = gpu_ilu(handle, A, torch.float64)
@@ -327,9 +333,11 @@ def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, name, scale):
 @pytest.mark.parametrize("flow,wpc", [(0, 8), (1, 4), (1, 8), (1, 16)])
 @pytest.mark.parametrize("name,scale", [("xenon2", 0.3), ("offshore", 0.2), ("cfd2", 0.3), ("ss1", 0.2)])
 def test_flow_segments(handle, monkeypatch, flow, wpc, name, scale):
-    """Fat solve segments as one persistent launch (trsv_flow: items start
-    when the y they read exist, read from y itself) or a launch per level,
-    2-4 workgroups per CU: bitwise equal to the oracle for L, L^T and U."""
+    """Fat solve segments and fat factor levels as one persistent launch each
+    (trsv_flow: items start when the y they read exist, read from y itself;
+    ilu0_flow: rows start when the rows they read have set their done flags)
+    or a launch per level, 1-4 workgroups per CU: bitwise equal to the oracle
+    for the factor, L, L^T and U."""
     monkeypatch.setenv("RSP_ILU_FLOW", str(flow))
     monkeypatch.setenv("RSP_ILU_FLOW_WPC", str(wpc))
     A = csr.surrogate(name, scale)
