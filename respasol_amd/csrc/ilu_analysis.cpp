@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <thread>
@@ -33,19 +34,94 @@ void Phases::mark(const char *what) {
     t_last = t;
 }
 
-// rows grouped by level (stable: ascending row within a level)
-static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int> &ptr,
-                         std::vector<int> &rows) {
-    ptr.assign((size_t)nlev + 1, 0);
-    for (int v : lev) ptr[(size_t)v + 1]++;
-    for (int l = 0; l < nlev; l++) ptr[(size_t)l + 1] += ptr[(size_t)l];
-    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
-    rows.assign(lev.size(), 0);
-    for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
+// Host worker threads for the analysis: OMP_NUM_THREADS (the box's share of
+// its cores; the machine may have many more) or the hardware count, <= 64.
+static int host_threads() {
+    int t = env_int("OMP_NUM_THREADS", 0);
+    if (t <= 0) t = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 64));
 }
 
+// f(r0, r1) over contiguous row blocks of [0, n) on host_threads() threads.
+template <typename F>
+static void parallel_rows(int n, F f) {
+    const int nt = n < 8192 ? 1 : host_threads();
+    if (nt == 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+        th.emplace_back(f, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
+    for (std::thread &x : th) x.join();
+}
 
+// f(lo, hi) over [0, n) in at most host_threads() contiguous blocks of at
+// least `grain` (the calling thread takes the first block).
+template <typename F>
+static void pfor(long long n, long long grain, F f) {
+    const int nt = (int)std::max<long long>(1, std::min<long long>(host_threads(), n / std::max(grain, 1LL)));
+    if (nt <= 1) {
+        if (n > 0) f(0LL, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt - 1);
+    for (int t = 1; t < nt; t++) th.emplace_back(f, n * t / nt, n * (t + 1) / nt);
+    f(0LL, n / nt);
+    for (std::thread &x : th) x.join();
+}
 
+// f(j) for j in [0, n), items handed out dynamically (uneven item costs:
+// levels, segments, chunks); `work` estimates the total cost to size the team.
+template <typename F>
+static void pfor_dyn(int n, long long work, long long grain, F f) {
+    const int nt = (int)std::max<long long>(1, std::min<long long>({(long long)host_threads(), (long long)n,
+                                                                     work / std::max(grain, 1LL)}));
+    if (nt <= 1) {
+        for (int j = 0; j < n; j++) f(j);
+        return;
+    }
+    std::atomic<int> next(0);
+    auto body = [&]() {
+        for (int j; (j = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(j);
+    };
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt - 1);
+    for (int t = 1; t < nt; t++) th.emplace_back(body);
+    body();
+    for (std::thread &x : th) x.join();
+}
+
+// rows grouped by level (stable: ascending row within a level): a counting
+// sort over contiguous row blocks, one level histogram per block
+static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int> &ptr,
+                         std::vector<int> &rows) {
+    const long long n = (long long)lev.size();
+    const int nb = (int)std::max<long long>(1, std::min<long long>(host_threads(), n / (1 << 15)));
+    std::vector<std::vector<int>> hist((size_t)nb);
+    auto blk = [&](int t) { return std::make_pair(n * t / nb, n * (t + 1) / nb); };
+    pfor_dyn(nb, n, 1, [&](int t) {
+        std::vector<int> &h = hist[(size_t)t];
+        h.assign((size_t)nlev, 0);
+        for (long long i = blk(t).first; i < blk(t).second; i++) h[(size_t)lev[(size_t)i]]++;
+    });
+    ptr.assign((size_t)nlev + 1, 0);
+    for (int l = 0; l < nlev; l++) {  // block t's first slot in level l
+        int at = ptr[(size_t)l];
+        for (int t = 0; t < nb; t++) {
+            const int c = hist[(size_t)t][(size_t)l];
+            hist[(size_t)t][(size_t)l] = at;
+            at += c;
+        }
+        ptr[(size_t)l + 1] = at;
+    }
+    rows.resize((size_t)n);
+    pfor_dyn(nb, n, 1, [&](int t) {
+        std::vector<int> &h = hist[(size_t)t];
+        for (long long i = blk(t).first; i < blk(t).second; i++) rows[(size_t)h[(size_t)lev[(size_t)i]]++] = (int)i;
+    });
+}
 
 // fma-chain batch for a mean chain length of total / count
 static int chain_batch(long long total, long long count) {
@@ -66,29 +142,28 @@ static int chain_batch(long long total, long long count) {
 // run, so its store is visible after the chunk's full barrier).
 
 // row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
-template <typename RowTerms>
+// Built in parallel phases (rows, levels and chunks as work items, prefix
+// sums over level order in between); row_count(i) = the number of terms
+// row_terms(i) emits.
+template <typename RowCount, typename RowTerms>
 static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
                              int thin_rows, int group, const std::vector<int> &diag,
-                             RowTerms row_terms, SolvePlan &sp) {
+                             RowCount row_count, RowTerms row_terms, SolvePlan &sp) {
     const int nlev = (int)ptr.size() - 1;
+    const long long nx = (long long)rows.size();
+    constexpr long long kGrain = 1 << 14;
     std::vector<int> order(rows);
-    // segments: runs of thin levels / fat levels. A thin level's rows have
-    // their terms padded to whole groups of `group` (at least one group):
-    // pads are (position -1, source kPadSrc), i.e. a zero value times the zero
-    // slot of the LDS y buffer — an exact no-op fma — so the thin kernel reads
-    // a row as whole groups with vector loads and no length tests.
-    // terms per row, counted once
     std::vector<int> nt_row((size_t)n, 0);
-    for (int i = 0; i < n; i++) {
-        int cnt = 0;
-        row_terms(i, [&](int, int) { cnt++; });
-        nt_row[(size_t)i] = cnt;
-    }
-    auto nterms = [&](int i) { return nt_row[(size_t)i]; };
+    pfor(n, kGrain, [&](long long a, long long b) {
+        for (long long i = a; i < b; i++) nt_row[(size_t)i] = row_count((int)i);
+    });
     auto padded = [&](int cnt) { return std::max(1, (cnt + group - 1) / group) * group; };
     std::vector<int> lpad((size_t)std::max(nlev, 1), 0);
-    for (int l = 0; l < nlev; l++)
-        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) lpad[(size_t)l] += padded(nterms(order[(size_t)x]));
+    pfor_dyn(nlev, nx, kGrain, [&](int l) {
+        int t = 0;
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) t += padded(nt_row[(size_t)order[(size_t)x]]);
+        lpad[(size_t)l] = t;
+    });
     sp.segs.clear();
     for (int l = 0; l < nlev; l++) {
         const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
@@ -102,64 +177,66 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     std::vector<char> thin_lev((size_t)std::max(nlev, 1), 0);
     for (const rsp::LevelSeg &sg : sp.segs)
         for (int l = sg.lb; l < sg.le; l++) thin_lev[(size_t)l] = (char)sg.thin;
-    // within each level: short rows first (a thread each), longer rows after
-    // them (a wave each). Short: <= kLongTerms terms in a thin run (LDS
-    // operands); <= kFatLongTerms in a fat level, where a thread pays one
-    // global round trip per batch of terms and a wave one per 64 terms.
-    // A fat level's rows of > kHubTerms terms come last, a workgroup each.
+    // within each level (stable): short rows, then wave rows, then (fat
+    // levels) hub rows
     const int fat_long = env_int("RSP_ILU_FAT_LONG", rsp::kFatLongTerms);
     const int hub = env_int("RSP_ILU_HUB", rsp::kHubTerms);
     sp.nshort.assign((size_t)std::max(nlev, 1), 0);
     sp.nwave.assign((size_t)std::max(nlev, 1), 0);
-    for (int l = 0; l < nlev; l++) {
+    pfor_dyn(nlev, nx, kGrain, [&](int l) {
         const int lim = thin_lev[(size_t)l] ? rsp::kLongTerms : fat_long;
-        auto b = order.begin() + ptr[(size_t)l], e = order.begin() + ptr[(size_t)l + 1];
-        auto mid = std::stable_partition(b, e, [&](int i) { return nterms(i) <= lim; });
-        sp.nshort[(size_t)l] = (int)(mid - b);
-        auto hb = thin_lev[(size_t)l] ? e : std::stable_partition(mid, e, [&](int i) { return nterms(i) <= hub; });
-        sp.nwave[(size_t)l] = (int)(hb - b);
-    }
-    std::vector<int> col;
-    sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
-    sp.tpos.clear();
-    {  // flat terms incl. pads: reserve once
-        size_t total = 0;
-        for (int l = 0; l < nlev; l++) total += (size_t)lpad[(size_t)l];
-        total += (size_t)rows.size() * rsp::kFatLongTerms;
-        sp.tpos.reserve(total);
-        col.reserve(total);
-    }
-    // fat levels: each short row owns kFatLongTerms flat terms (its terms,
-    // then pads), so trsv_level finds a row's terms at sbase + r * 8 without
-    // reading its task first; t1 stays at the row's last real term
+        const int b = ptr[(size_t)l], e = ptr[(size_t)l + 1];
+        int c[3] = {0, 0, 0};
+        auto cls = [&](int i) {
+            const int t = nt_row[(size_t)i];
+            return t <= lim ? 0 : (thin_lev[(size_t)l] || t <= hub ? 1 : 2);
+        };
+        for (int x = b; x < e; x++) c[cls(order[(size_t)x])]++;
+        sp.nshort[(size_t)l] = c[0];
+        sp.nwave[(size_t)l] = c[0] + c[1];
+        if (c[0] == e - b || c[1] == e - b || c[2] == e - b) return;  // one class: order unchanged
+        std::vector<int> tmp(order.begin() + b, order.begin() + e);
+        int w[3] = {b, b + c[0], b + c[0] + c[1]};
+        for (int i : tmp) order[(size_t)w[cls(i)]++] = i;
+    });
+    // flat term ranges in level order: a thin row's terms padded to whole
+    // groups; a padded fat level's short rows own kFatLongTerms terms each
     const bool pad_fat = fat_long == rsp::kFatLongTerms && env_int("RSP_ILU_FAT_PAD", 1) != 0;
     sp.sbase.assign((size_t)std::max(nlev, 1), -1);
-    for (int l = 0; l < nlev; l++) {
+    sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
+    std::vector<int> len((size_t)std::max(nx, 1LL), 0);
+    pfor_dyn(nlev, nx, kGrain, [&](int l) {
         const bool padl = pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0;
-        if (padl) sp.sbase[(size_t)l] = (int)sp.tpos.size();
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-            const int i = order[(size_t)x];
-            rsp::RowTask &t = sp.tasks[(size_t)x];
-            t.i = i;
-            t.t0 = (int)sp.tpos.size();
-            row_terms(i, [&](int tp, int c) {
-                sp.tpos.push_back(tp);
-                col.push_back(c);
-            });
-            if (thin_lev[(size_t)l])
-                while ((int)sp.tpos.size() - t.t0 < padded((int)sp.tpos.size() - t.t0)) {
-                    sp.tpos.push_back(-1);
-                    col.push_back(-1);
-                }
-            t.t1 = (int)sp.tpos.size();
-            if (padl && x - ptr[(size_t)l] < sp.nshort[(size_t)l])
-                while ((int)sp.tpos.size() - t.t0 < rsp::kFatLongTerms) {
-                    sp.tpos.push_back(-1);
-                    col.push_back(-1);
-                }
-            t.d = diag.empty() ? -1 : diag[(size_t)i];
+            const int i = order[(size_t)x], t = nt_row[(size_t)i];
+            const int t1 = thin_lev[(size_t)l] ? padded(t) : t;
+            len[(size_t)x] = padl && x - ptr[(size_t)l] < sp.nshort[(size_t)l] ? std::max(t1, rsp::kFatLongTerms) : t1;
+            sp.tasks[(size_t)x].t1 = t1;  // length for now
         }
+    });
+    long long total = 0;
+    for (long long x = 0; x < nx; x++) {
+        sp.tasks[(size_t)x].t0 = (int)total;
+        total += len[(size_t)x];
     }
+    for (int l = 0; l < nlev; l++)
+        if (pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0) sp.sbase[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l]].t0;
+    sp.tpos.assign((size_t)total, -1);
+    std::vector<int> col((size_t)total, -1);
+    pfor(nx, kGrain, [&](long long a, long long b) {
+        for (long long x = a; x < b; x++) {
+            rsp::RowTask &t = sp.tasks[(size_t)x];
+            const int i = order[(size_t)x];
+            t.i = i;
+            t.t1 += t.t0;
+            t.d = diag.empty() ? -1 : diag[(size_t)i];
+            int k = t.t0;
+            row_terms(i, [&](int tp, int c) {
+                sp.tpos[(size_t)k] = tp;
+                col[(size_t)k++] = c;
+            });
+        }
+    });
     // flow segments: fat segments of two or more levels run as one persistent
     // launch (trsv_flow) over work items in level order — a level's short rows
     // in groups of 64 (a lane each), then its wave and hub rows (a wave each).
@@ -194,20 +271,25 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
         fprintf(stderr, "rsp_ilu0 plan n=%d levels=%d group=%d thin %d segs / %d levels, fat %d / %d, flow %d / %d (%zu items)\n",
                 n, nlev, group, nthin, lthin, nfat, lfat, nflow, lflow, sp.fitems.size());
     }
-    if (sp.fitems.empty()) sp.fitems.push_back({0, 0, -1, -1});  // keep the device array non-empty
+    if (sp.fitems.empty()) sp.fitems.push_back({0, 0, -1, -1});
     std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
     for (int l = 0; l < nlev; l++)
         if (ptr[(size_t)l + 1] > ptr[(size_t)l])
             lterms[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l + 1] - 1].t1 - sp.tasks[(size_t)ptr[(size_t)l]].t0;
-    sp.src = col;
-    for (size_t k = 0; k < col.size(); k++)
-        if (col[k] < 0) sp.src[k] = rsp::kPadSrc;
+    sp.src.resize((size_t)total);
+    pfor(total, kGrain, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) sp.src[(size_t)k] = col[(size_t)k] < 0 ? rsp::kPadSrc : col[(size_t)k];
+    });
     for (rsp::LevelSeg &sg : sp.segs)
         if (sg.thin) sg.nth = rsp::kThinThreads;
-    // chunks of the thin runs + term sources
     std::vector<int> slot_of((size_t)n, -1);
-    for (size_t x = 0; x < order.size(); x++) slot_of[(size_t)order[x]] = (int)x;
+    pfor(nx, kGrain, [&](long long a, long long b) {
+        for (long long x = a; x < b; x++) slot_of[(size_t)order[(size_t)x]] = (int)x;
+    });
+    // chunks of the thin runs (greedy over levels), then the y sources of
+    // their terms (per level)
     sp.chunks.clear();
+    std::vector<int> thin_base((size_t)std::max(nlev, 1), -1);  // per thin level: its run's first slot
     for (rsp::LevelSeg &sg : sp.segs) {
         if (!sg.thin) continue;
         sg.c0 = (int)sp.chunks.size();
@@ -224,70 +306,78 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
             }
             crow += cnt;
             cterm += lterms[(size_t)l];
+            thin_base[(size_t)l] = ptr[(size_t)sg.lb];
         }
         sg.c1 = (int)sp.chunks.size();
-        const int base = ptr[(size_t)sg.lb];
-        for (int l = sg.lb; l < sg.le; l++) {
-            const int r_end = ptr[(size_t)l + 1] - base;
-            for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++)
-                for (int k = sp.tasks[(size_t)x].t0; k < sp.tasks[(size_t)x].t1; k++) {
-                    if (col[(size_t)k] < 0) continue;  // pad
-                    const int sj = slot_of[(size_t)col[(size_t)k]];
-                    if (sj < base || sj >= ptr[(size_t)l]) continue;  // before the run
-                    const int rj = sj - base;
-                    if (r_end - rj <= rsp::kYWin) sp.src[(size_t)k] = -((rj & (rsp::kYWin - 1)) + 1);
-                }
-        }
     }
-    if (sp.tpos.empty()) {  // keep the device arrays non-empty
+    pfor_dyn(nlev, nx, kGrain, [&](int l) {
+        const int base = thin_base[(size_t)l];
+        if (base < 0) return;
+        const int r_end = ptr[(size_t)l + 1] - base;
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++)
+            for (int k = sp.tasks[(size_t)x].t0; k < sp.tasks[(size_t)x].t1; k++) {
+                if (col[(size_t)k] < 0) continue;  // pad
+                const int sj = slot_of[(size_t)col[(size_t)k]];
+                if (sj < base || sj >= ptr[(size_t)l]) continue;  // before the run
+                const int rj = sj - base;
+                if (r_end - rj <= rsp::kYWin) sp.src[(size_t)k] = -((rj & (rsp::kYWin - 1)) + 1);
+            }
+    });
+    if (sp.tpos.empty()) {
         sp.tpos.push_back(0);
         sp.src.push_back(0);
     }
-    // per chunk: slot and term ranges, the static row records (first group,
-    // y window slot), each term's y index in the LDS y buffer (window slot,
-    // the zero slot for pads, or its staged slot) and the staged terms
+    // per chunk: ranges, static row records, term y indices, staged terms
+    // (counted per chunk, then filled at their prefix offsets)
     sp.trow.assign(std::max<size_t>(rows.size(), 1), rsp::ThinRowPlan{0, 0, 0, -1});
     sp.sid.assign(sp.tpos.size(), rsp::kYWin);
-    sp.stg.clear();
-    for (const rsp::LevelSeg &sg : sp.segs) {
-        if (!sg.thin) continue;
-        const int base = ptr[(size_t)sg.lb];
-        for (int c = sg.c0; c < sg.c1; c++) {
-            rsp::LevelChunk &ch = sp.chunks[(size_t)c];
-            ch.x0 = ptr[(size_t)ch.l0];
-            ch.x1 = ptr[(size_t)ch.l1];
-            ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
-            ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
-            ch.st0 = (int)sp.stg.size();
-            for (int x = ch.x0; x < ch.x1; x++) {
-                const rsp::RowTask &t = sp.tasks[(size_t)x];
-                sp.trow[(size_t)x] = {(t.t0 - ch.k0) / group | ((t.t1 - t.t0) / group) << 16,
-                                      (x - base) & (rsp::kYWin - 1), t.i, t.d};
-                for (int k = t.t0; k < t.t1; k++) {
-                    const int sc = sp.src[(size_t)k];
-                    if (sc < 0) {
-                        sp.sid[(size_t)k] = -sc - 1;  // window slot, or the zero slot for a pad
-                    } else {
-                        sp.sid[(size_t)k] = rsp::kYWin + 1 + (k - ch.k0);
-                        sp.stg.push_back({k - ch.k0, sc});
-                    }
+    const int nch = (int)sp.chunks.size();
+    std::vector<int> chunk_base((size_t)std::max(nch, 1), 0);
+    for (const rsp::LevelSeg &sg : sp.segs)
+        if (sg.thin)
+            for (int c = sg.c0; c < sg.c1; c++) chunk_base[(size_t)c] = ptr[(size_t)sg.lb];
+    std::vector<int> nst((size_t)std::max(nch, 1), 0);
+    pfor_dyn(nch, nx, kGrain, [&](int c) {
+        rsp::LevelChunk &ch = sp.chunks[(size_t)c];
+        ch.x0 = ptr[(size_t)ch.l0];
+        ch.x1 = ptr[(size_t)ch.l1];
+        ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
+        ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
+        int m = 0;
+        for (int x = ch.x0; x < ch.x1; x++)
+            for (int k = sp.tasks[(size_t)x].t0; k < sp.tasks[(size_t)x].t1; k++) m += sp.src[(size_t)k] >= 0;
+        nst[(size_t)c] = m;
+    });
+    long long nstg = 0;
+    for (int c = 0; c < nch; c++) {
+        sp.chunks[(size_t)c].st0 = (int)nstg;
+        nstg += nst[(size_t)c];
+        sp.chunks[(size_t)c].st1 = (int)nstg;
+    }
+    sp.stg.assign((size_t)nstg, rsp::StagedTerm{0, 0});
+    pfor_dyn(nch, nx, kGrain, [&](int c) {
+        const rsp::LevelChunk &ch = sp.chunks[(size_t)c];
+        const int base = chunk_base[(size_t)c];
+        int st = ch.st0;
+        for (int x = ch.x0; x < ch.x1; x++) {
+            const rsp::RowTask &t = sp.tasks[(size_t)x];
+            sp.trow[(size_t)x] = {(t.t0 - ch.k0) / group | ((t.t1 - t.t0) / group) << 16,
+                                  (x - base) & (rsp::kYWin - 1), t.i, t.d};
+            for (int k = t.t0; k < t.t1; k++) {
+                const int sc = sp.src[(size_t)k];
+                if (sc < 0) {
+                    sp.sid[(size_t)k] = -sc - 1;
+                } else {
+                    sp.sid[(size_t)k] = rsp::kYWin + 1 + (k - ch.k0);
+                    sp.stg[(size_t)st++] = {k - ch.k0, sc};
                 }
             }
-            ch.st1 = (int)sp.stg.size();
         }
-    }
+    });
     if (sp.stg.empty()) sp.stg.push_back({0, 0});
     if (sp.chunks.empty()) sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
 }
 
-
-
-// Factor plan of the L DAG (see IluArgs): segments (a level is thin if it
-// has <= thin_rows rows and its positions / update pairs fit one chunk), the
-// LDS-staged chunks of every thin run, and per chunk its items (the positions
-// of its rows: lower ones in intra-row stage order, then upper ones) and update
-// pairs with their sources: a chunk-local item when the producing row is in
-// the chunk, else the position (its final value is staged at the chunk start).
 // Factor plan of the L DAG (see IluArgs): segments (fat levels: one launch
 // each; thin levels: one single-workgroup launch per run) and, for the thin
 // runs, ROUNDS: a level's positions ("items") grouped so that a round's items
@@ -301,6 +391,20 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
 // chunk's slots, the previous chunk's slots (kept in the other LDS buffer),
 // values staged from vals at the chunk start (producers two or more chunks
 // back, or before the run), or the zero slot (a missing u_kk).
+//
+// Built in parallel. A thin segment is cut at level boundaries into pieces
+// of about RSP_ILU_PIECE_ITEMS positions (default kRndPieceItems); each
+// piece is planned on its own (greedily, as above) and the pieces are joined
+// in order with an EMPTY chunk between two pieces of a segment: ilu0_rounds issues a chunk's gathers at
+// the previous chunk's switch, so the empty chunk's switch is where the
+// earlier piece's last stores are complete before the next piece stages them
+// (a piece sees every value before it as staged). Per position, where[] holds
+// the chunk key (piece + 1, chunk within the piece) and slot it was placed at:
+// keys are unique over the whole plan, so a piece reading a position another
+// piece is writing concurrently (never its own chunk or the one before) only
+// ever gets "not here" — the relaxed atomics make those reads well defined.
+// The staged positions of the current chunk sit in a piece-private hash.
+static constexpr int kRndPieceItems = 1 << 17;
 
 static void build_factor_plan(int n, const std::vector<int> &rp, const std::vector<int> &ci,
                               const std::vector<int> &dpos, const std::vector<int> &hasdiag,
@@ -309,74 +413,114 @@ static void build_factor_plan(int n, const std::vector<int> &rp, const std::vect
     const int nlev = (int)ptr.size() - 1;
     const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
     const int thin_items = env_int("RSP_ILU_THIN_FACTOR_ITEMS", rsp::kRndLevelItems);
-    auto npairs = [&](int p) { return sym.upd_ptr[(size_t)p + 1] - sym.upd_ptr[(size_t)p]; };
-    fp.segs.clear();
-    for (int l = 0; l < nlev; l++) {
-        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
+    const long long piece_items = std::max(1, env_int("RSP_ILU_PIECE_ITEMS", kRndPieceItems));
+    const int nnz = rp[(size_t)n];
+    // per level: positions and the largest update list
+    std::vector<long long> litems((size_t)std::max(nlev, 1), 0);
+    std::vector<int> lmaxp((size_t)std::max(nlev, 1), 0);
+    pfor_dyn(nlev, nnz, 1 << 15, [&](int l) {
         long long items = 0;
         int maxp = 0;
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
             const int i = rows[(size_t)x];
             items += rp[(size_t)i + 1] - rp[(size_t)i];
-            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) maxp = std::max(maxp, npairs(p));
+            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++)
+                maxp = std::max(maxp, sym.upd_ptr[(size_t)p + 1] - sym.upd_ptr[(size_t)p]);
         }
-        const int thin = (cnt <= thin_rows && items <= thin_items && maxp <= rsp::kRndItemPairs) ? 1 : 0;
+        litems[(size_t)l] = items;
+        lmaxp[(size_t)l] = maxp;
+    });
+    fp.segs.clear();
+    for (int l = 0; l < nlev; l++) {
+        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
+        const int thin = (cnt <= thin_rows && litems[(size_t)l] <= thin_items && lmaxp[(size_t)l] <= rsp::kRndItemPairs) ? 1 : 0;
         if (!fp.segs.empty() && fp.segs.back().thin == thin && fp.segs.back().le == l)
             fp.segs.back().le = l + 1;
         else
             fp.segs.push_back({l, l + 1, thin, 0, 0, rsp::kThinThreads});
     }
-    fp.chunks.clear();
-    fp.items.clear();
-    fp.pairs.clear();
-    fp.staged.clear();
-    fp.rounds.clear();
-    // where each position was placed: chunk and slot (-1: not in this run yet)
-    std::vector<int> pchunk((size_t)rp[(size_t)n], -1), pslot((size_t)rp[(size_t)n], 0);
-    std::vector<int> stg_of((size_t)rp[(size_t)n], -1);  // staged slot in the current chunk
-    std::vector<int> stg_list;                            // positions staged in the current chunk
-    struct RItem {
-        int round, pos, row;
+    struct Piece {
+        int seg, lb, le;
+        FacPlan out;  // chunk records relative to the piece's own arrays
     };
-    std::vector<RItem> ritems, rsorted;  // a level's items
-    std::vector<int> rcount;
-    for (rsp::LevelSeg &sg : fp.segs) {
+    std::vector<Piece> pieces;
+    for (int s = 0; s < (int)fp.segs.size(); s++) {
+        const rsp::LevelSeg &sg = fp.segs[(size_t)s];
         if (!sg.thin) continue;
-        sg.c0 = (int)fp.chunks.size();
+        long long acc = 0;
+        int lb = sg.lb;
+        for (int l = sg.lb; l < sg.le; l++) {
+            acc += litems[(size_t)l];
+            if (acc >= piece_items && l + 1 < sg.le) {
+                pieces.push_back({s, lb, l + 1, FacPlan()});
+                lb = l + 1;
+                acc = 0;
+            }
+        }
+        pieces.push_back({s, lb, sg.le, FacPlan()});
+    }
+    std::vector<unsigned long long> where((size_t)std::max(nnz, 1), 0ull);
+    auto wload = [&](int q) { return __atomic_load_n(&where[(size_t)q], __ATOMIC_RELAXED); };
+    pfor_dyn((int)pieces.size(), nnz, 1 << 15, [&](int pi) {
+        Piece &pc = pieces[(size_t)pi];
+        FacPlan &o = pc.out;
+        // staged positions of the current chunk: open addressing, epoch-stamped
+        constexpr int kH = 4 * rsp::kRndStaged;
+        std::vector<int> hkey(kH), hval(kH), hep(kH, 0);
+        int epoch = 0, nstg = 0;
+        auto hslot = [&](int q) { return (int)(((unsigned)q * 2654435761u) >> 18) & (kH - 1); };
+        auto hfind = [&](int q) {
+            for (int h = hslot(q);; h = (h + 1) & (kH - 1)) {
+                if (hep[(size_t)h] != epoch) return -1;
+                if (hkey[(size_t)h] == q) return hval[(size_t)h];
+            }
+        };
+        auto hput = [&](int q, int v) {
+            int h = hslot(q);
+            while (hep[(size_t)h] == epoch) h = (h + 1) & (kH - 1);
+            hep[(size_t)h] = epoch;
+            hkey[(size_t)h] = q;
+            hval[(size_t)h] = v;
+        };
+        const unsigned long long pkey = (unsigned long long)(pi + 1) << 28;
+        int c = -1;  // chunk within the piece
+        unsigned long long ckey = 0;
         rsp::RndChunk ch{};
-        int c = -1;  // current chunk id
         auto open_chunk = [&]() {
-            for (int q : stg_list) stg_of[(size_t)q] = -1;
-            stg_list.clear();
-            c = (int)fp.chunks.size();
-            ch = rsp::RndChunk{(int)fp.items.size(), (int)fp.items.size(), (int)fp.pairs.size(),
-                               (int)fp.pairs.size(), (int)fp.staged.size(), (int)fp.staged.size(),
-                               (int)fp.rounds.size(), (int)fp.rounds.size()};
-            fp.chunks.push_back(ch);
+            epoch++;
+            nstg = 0;
+            c = (int)o.chunks.size();
+            ckey = pkey | (unsigned long long)c;
+            ch = rsp::RndChunk{(int)o.items.size(), (int)o.items.size(), (int)o.pairs.size(), (int)o.pairs.size(),
+                               (int)o.staged.size(), (int)o.staged.size(), (int)o.rounds.size(), (int)o.rounds.size()};
+            o.chunks.push_back(ch);
         };
         auto close_chunk = [&]() {
-            ch.i1 = (int)fp.items.size();
-            ch.p1 = (int)fp.pairs.size();
-            ch.s1 = (int)fp.staged.size();
-            ch.r1 = (int)fp.rounds.size();
-            fp.chunks[(size_t)c] = ch;
+            ch.i1 = (int)o.items.size();
+            ch.p1 = (int)o.pairs.size();
+            ch.s1 = (int)o.staged.size();
+            ch.r1 = (int)o.rounds.size();
+            o.chunks[(size_t)c] = ch;
         };
-        // operand class index of position q for an item of chunk c (new staged
-        // values are appended to `fresh`; the caller commits or rolls back)
         auto ref = [&](int q, std::vector<int> &fresh) {
-            const int qc = pchunk[(size_t)q];
-            if (qc == c) return pslot[(size_t)q];
-            if (qc >= 0 && qc == c - 1) return K + pslot[(size_t)q];
-            if (stg_of[(size_t)q] >= 0) return 2 * K + stg_of[(size_t)q];
+            const unsigned long long w = wload(q), wk = w >> 12;
+            if (wk == ckey) return (int)(w & 0xfff);
+            if (c > 0 && wk == ckey - 1) return K + (int)(w & 0xfff);
+            const int st = hfind(q);
+            if (st >= 0) return 2 * K + st;
             for (size_t f = 0; f < fresh.size(); f++)
-                if (fresh[f] == q) return 2 * K + (int)(stg_list.size() + f);
+                if (fresh[f] == q) return 2 * K + (int)(nstg + f);
             fresh.push_back(q);
-            return 2 * K + (int)(stg_list.size() + fresh.size() - 1);
+            return 2 * K + (int)(nstg + fresh.size() - 1);
         };
+        struct RItem {
+            int round, pos, row;
+        };
+        std::vector<RItem> ritems, rsorted;
+        std::vector<int> rcount, fresh, ipairs;
         open_chunk();
-        long long last_round_key = -1;  // (level, round) of the chunk's last round
-        std::vector<int> fresh, ipairs;
-        for (int l = sg.lb; l < sg.le; l++) {
+        long long last_round_key = -1;
+        for (int l = pc.lb; l < pc.le; l++) {
             ritems.clear();
             for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
                 const int i = rows[(size_t)x], rs = rp[(size_t)i], di = dpos[(size_t)i];
@@ -399,7 +543,7 @@ static void build_factor_plan(int n, const std::vector<int> &rp, const std::vect
             }
             for (const RItem &ri : ritems) {
                 const int p = ri.pos, i = ri.row;
-                const long long key = (long long)(l - sg.lb) * 1000000007LL + ri.round;
+                const long long key = (long long)(l - pc.lb) * 1000000007LL + ri.round;
                 const bool lower = p < dpos[(size_t)i];
                 for (int attempt = 0; attempt < 2; attempt++) {
                     fresh.clear();
@@ -413,45 +557,73 @@ static void build_factor_plan(int n, const std::vector<int> &rp, const std::vect
                         const int k = ci[(size_t)p];
                         d = hasdiag[(size_t)k] ? ref(dpos[(size_t)k], fresh) : kZero;
                     }
-                    const int slot = (int)fp.items.size() - ch.i0;
+                    const int slot = (int)o.items.size() - ch.i0;
                     const bool new_round = key != last_round_key;
-                    const bool fits = slot < K && (int)(fp.pairs.size() - ch.p0 + ipairs.size()) <= rsp::kRndPairs &&
-                                      (int)(stg_list.size() + fresh.size()) <= S &&
-                                      (int)(fp.rounds.size() - ch.r0) + (new_round ? 1 : 0) <= rsp::kRndRounds;
-                    if (!fits && attempt == 0 && slot > 0) {  // next chunk (references re-resolved there)
+                    const bool fits = slot < K && (int)(o.pairs.size() - ch.p0 + ipairs.size()) <= rsp::kRndPairs &&
+                                      nstg + (int)fresh.size() <= S &&
+                                      (int)(o.rounds.size() - ch.r0) + (new_round ? 1 : 0) <= rsp::kRndRounds;
+                    if (!fits && attempt == 0 && slot > 0) {
                         close_chunk();
                         open_chunk();
                         last_round_key = -1;
                         continue;
                     }
-                    // commit the item
                     for (int q : fresh) {
-                        stg_of[(size_t)q] = (int)stg_list.size();
-                        stg_list.push_back(q);
-                        fp.staged.push_back(q);
+                        hput(q, nstg++);
+                        o.staged.push_back(q);
                     }
                     if (new_round) {
-                        fp.rounds.push_back(slot);
+                        o.rounds.push_back(slot);
                         last_round_key = key;
                     }
-                    const int pstart = (int)fp.pairs.size() - ch.p0;
-                    fp.pairs.insert(fp.pairs.end(), ipairs.begin(), ipairs.end());
+                    const int pstart = (int)o.pairs.size() - ch.p0;
+                    o.pairs.insert(o.pairs.end(), ipairs.begin(), ipairs.end());
                     const int zr = (!lower && p == dpos[(size_t)i] && hasdiag[(size_t)i]) ? i : -1;
-                    fp.items.push_back({p, pstart | (int)ipairs.size() << 16, d, zr});
-                    pchunk[(size_t)p] = c;
-                    pslot[(size_t)p] = slot;
+                    o.items.push_back({p, pstart | (int)ipairs.size() << 16, d, zr});
+                    __atomic_store_n(&where[(size_t)p], ckey << 12 | (unsigned long long)slot, __ATOMIC_RELAXED);
                     break;
                 }
             }
         }
         close_chunk();
-        sg.c1 = (int)fp.chunks.size();
-        for (int x = ptr[(size_t)sg.lb]; x < ptr[(size_t)sg.le]; x++) {  // positions leave the run
-            const int i = rows[(size_t)x];
-            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) pchunk[(size_t)p] = -1;
+    });
+    // join: pieces in order, an empty chunk between two pieces of a segment
+    fp.chunks.clear();
+    fp.items.clear();
+    fp.pairs.clear();
+    fp.staged.clear();
+    fp.rounds.clear();
+    size_t ni = 0, np = 0, ns = 0, nr = 0, nc = 0;
+    for (const Piece &pc : pieces) {
+        ni += pc.out.items.size();
+        np += pc.out.pairs.size();
+        ns += pc.out.staged.size();
+        nr += pc.out.rounds.size();
+        nc += pc.out.chunks.size() + 1;
+    }
+    fp.items.reserve(ni);
+    fp.pairs.reserve(np);
+    fp.staged.reserve(ns);
+    fp.rounds.reserve(nr);
+    fp.chunks.reserve(nc);
+    for (size_t q = 0; q < pieces.size(); q++) {
+        const Piece &pc = pieces[q];
+        rsp::LevelSeg &sg = fp.segs[(size_t)pc.seg];
+        const int bi = (int)fp.items.size(), bp = (int)fp.pairs.size(), bs = (int)fp.staged.size(),
+                  br = (int)fp.rounds.size();
+        if (q == 0 || pieces[q - 1].seg != pc.seg)
+            sg.c0 = (int)fp.chunks.size();
+        else
+            fp.chunks.push_back(rsp::RndChunk{bi, bi, bp, bp, bs, bs, br, br});  // the separator
+        for (rsp::RndChunk r : pc.out.chunks) {
+            r.i0 += bi, r.i1 += bi, r.p0 += bp, r.p1 += bp, r.s0 += bs, r.s1 += bs, r.r0 += br, r.r1 += br;
+            fp.chunks.push_back(r);
         }
-        for (int q : stg_list) stg_of[(size_t)q] = -1;
-        stg_list.clear();
+        fp.items.insert(fp.items.end(), pc.out.items.begin(), pc.out.items.end());
+        fp.pairs.insert(fp.pairs.end(), pc.out.pairs.begin(), pc.out.pairs.end());
+        fp.staged.insert(fp.staged.end(), pc.out.staged.begin(), pc.out.staged.end());
+        fp.rounds.insert(fp.rounds.end(), pc.out.rounds.begin(), pc.out.rounds.end());
+        sg.c1 = (int)fp.chunks.size();
     }
     if (fp.items.empty()) fp.items.push_back({0, 0, -1, -1});
     for (std::vector<int> *v : {&fp.pairs, &fp.staged, &fp.rounds})
@@ -459,33 +631,10 @@ static void build_factor_plan(int n, const std::vector<int> &rp, const std::vect
     if (fp.chunks.empty()) fp.chunks.push_back(rsp::RndChunk{});
 }
 
-
 // Symbolic ILU(0): the update list of every position (see IluArgs) and the
 // intra-row stages of the lower positions. Row i is scattered into a dense
 // column -> position map, then each lower k (ascending) walks row k's upper
 // part; a hit at column j appends (pos l_ik, pos u_kj) to position (i, j).
-
-// Host worker threads for the analysis: OMP_NUM_THREADS (the box's share of
-// its cores; the machine may have many more) or the hardware count, <= 64.
-static int host_threads() {
-    int t = env_int("OMP_NUM_THREADS", 0);
-    if (t <= 0) t = (int)std::thread::hardware_concurrency();
-    return std::max(1, std::min(t, 64));
-}
-
-// f(r0, r1) over contiguous row blocks of [0, n) on host_threads() threads.
-template <typename F>
-static void parallel_rows(int n, F f) {
-    const int nt = n < 8192 ? 1 : host_threads();
-    if (nt == 1) {
-        f(0, n);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; t++)
-        th.emplace_back(f, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
-    for (std::thread &x : th) x.join();
-}
 
 static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<int> &ci,
                          const std::vector<int> &dpos, const std::vector<int> &hasdiag,
@@ -637,7 +786,9 @@ void plan_u(const int *rp, const int *ci, IluHostPlan &hp) {
     std::vector<int> udiag((size_t)n);
     for (int i = 0; i < n; i++) udiag[(size_t)i] = hasdiag[(size_t)i] ? dpos[(size_t)i] : -1;
     const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
-    build_solve_plan(n, hp.U.ptr, hp.U.rows, thin_solve, hp.U.group, udiag, [&](int i, auto emit) {
+    build_solve_plan(n, hp.U.ptr, hp.U.rows, thin_solve, hp.U.group, udiag,
+                     [&](int i) { return rp[(size_t)i + 1] - dpos[(size_t)i] - hasdiag[(size_t)i]; },
+                     [&](int i, auto emit) {
         for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++) emit(p, ci[(size_t)p]);
     }, hp.U.sp);
     hp.U.planned = true;
@@ -710,23 +861,37 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
         nl = std::max(nl, l + 1);
     }
     // transposed strict lower: row k lists (j, pos) for l_jk, j descending
+    // (each worker owns a range of columns k and scans the whole strict
+    // lower part for them: j descending, so its lists come out in order)
     std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
     ltp.assign((size_t)n + 1, 0);
-    for (int j = 0; j < n; j++)
-        for (int p = rp[j]; p < dpos[(size_t)j]; p++) ltp[(size_t)ci[p] + 1]++;
+    long long nlo = 0;
+    for (int j = 0; j < n; j++) nlo += dpos[(size_t)j] - rp[j];
+    const int nb = (int)std::max<long long>(1, std::min<long long>(host_threads(), nlo / (1 << 16)));
+    auto kr = [&](int t) { return std::make_pair((int)((long long)n * t / nb), (int)((long long)n * (t + 1) / nb)); };
+    pfor_dyn(nb, nlo, 1, [&](int t) {
+        const int ka = kr(t).first, kb = kr(t).second;
+        for (int j = 0; j < n; j++)
+            for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
+                const int k = ci[p];
+                if (k >= ka && k < kb) ltp[(size_t)k + 1]++;
+            }
+    });
     for (int k = 0; k < n; k++) ltp[(size_t)k + 1] += ltp[(size_t)k];
-    lts.assign((size_t)ltp[(size_t)n], 0);
-    ltc.assign((size_t)ltp[(size_t)n], 0);
-    {
-        std::vector<int> fill(ltp.begin(), ltp.end() - 1);
+    lts.resize((size_t)ltp[(size_t)n]);
+    ltc.resize((size_t)ltp[(size_t)n]);
+    pfor_dyn(nb, nlo, 1, [&](int t) {
+        const int ka = kr(t).first, kb = kr(t).second;
+        std::vector<int> fill(ltp.begin() + ka, ltp.begin() + kb);
         for (int j = n - 1; j >= 0; j--)
             for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
                 const int k = ci[p];
-                const int slot = fill[(size_t)k]++;
+                if (k < ka || k >= kb) continue;
+                const int slot = fill[(size_t)(k - ka)]++;
                 lts[(size_t)slot] = p;
                 ltc[(size_t)slot] = j;
             }
-    }
+    });
     // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
     std::vector<int> lvt((size_t)n, 0);
     int nlt = n > 0 ? 1 : 0;
@@ -792,6 +957,7 @@ void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, 
         th.emplace_back([&] {
             timed("L", [&] {
                 build_solve_plan(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, std::vector<int>(),
+                                 [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; },
                                  [&](int i, auto emit) {
                                      for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
                                  }, hp.L.sp);
@@ -800,6 +966,7 @@ void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, 
         th.emplace_back([&] {
             timed("LT", [&] {
                 build_solve_plan(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, std::vector<int>(),
+                                 [&](int i) { return ltp[(size_t)i + 1] - ltp[(size_t)i]; },
                                  [&](int i, auto emit) {
                                      for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++)
                                          emit(lts[(size_t)q], ltc[(size_t)q]);
@@ -811,45 +978,61 @@ void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, 
     }
     hp.L.planned = hp.LT.planned = true;
     const std::vector<int> &rows_l = hp.L.rows;
+    const long long nx = (long long)rows_l.size();
     hp.frow.assign(std::max<size_t>(rows_l.size(), 1), rsp::FacRow{});
-    for (size_t x = 0; x < rows_l.size(); x++) {
-        const int i = rows_l[x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
-        hp.frow[x] = rsp::FacRow{i, rs, dpos[(size_t)i], re, sym.upd_ptr[(size_t)rs], sym.upd_ptr[(size_t)re],
-                                 hasdiag[(size_t)i], 0};
-    }
+    pfor(nx, 1 << 14, [&](long long a, long long b) {
+        for (long long x = a; x < b; x++) {
+            const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
+            hp.frow[(size_t)x] = rsp::FacRow{i, rs, dpos[(size_t)i], re, sym.upd_ptr[(size_t)rs],
+                                             sym.upd_ptr[(size_t)re], hasdiag[(size_t)i], 0};
+        }
+    });
     // fat factor levels in the slot layout (rsp::FacSlotLevel): each row's
     // structure at a fixed stride, so ilu0_level_slot reads it in one round
     // trip. A level whose padded slots would take more than twice its rows'
     // own structure (one large row among many small ones), or past the
-    // budget, keeps the FacRow path.
+    // budget, keeps the FacRow path. Per level (parallel): the largest
+    // LDS-path row and pair count, the rows' own structure size, whether
+    // every row fits the LDS path (flow runs); then the offsets in order.
     const std::vector<int> &lp = hp.L.ptr;
     const int nlev = (int)lp.size() - 1;
     hp.fslev.assign((size_t)std::max(nlev, 0), rsp::FacSlotLevel{0, 0, 0, 0, 0});
+    struct LevStat {
+        int rm, qm, all_lds, fat;
+        long long own;
+    };
+    std::vector<LevStat> ls((size_t)std::max(nlev, 1), LevStat{0, 0, 0, 0, 0});
+    for (const rsp::LevelSeg &sg : hp.fplan.segs)
+        if (!sg.thin)
+            for (int l = sg.lb; l < sg.le; l++) ls[(size_t)l].fat = 1;
+    pfor_dyn(nlev, nx, 1 << 14, [&](int l) {
+        LevStat &st = ls[(size_t)l];
+        if (!st.fat) return;
+        st.all_lds = 1;
+        for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
+            const rsp::FacRow &fr = hp.frow[(size_t)x];
+            const int nr = fr.re - fr.rs, nq = fr.q1 - fr.q0;
+            if (nr <= rsp::kFacRow && nq <= rsp::kFacPairs) {
+                st.rm = std::max(st.rm, nr);
+                st.qm = std::max(st.qm, nq);
+            } else {
+                st.all_lds = 0;
+            }
+            st.own += (rsp::fac_pairs_at(std::min(nr, rsp::kFacRow)) + 2 * std::min(nq, rsp::kFacPairs) + 3) & ~3;
+        }
+    });
     long long total = 0;
     std::vector<int> slot_levels;
-    for (const rsp::LevelSeg &sg : hp.fplan.segs) {
-        if (sg.thin) continue;
-        for (int l = sg.lb; l < sg.le; l++) {
-            int rm = 0, qm = 0;
-            long long own = 0;
-            for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
-                const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
-                const int nq = sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs];
-                if (re - rs <= rsp::kFacRow && nq <= rsp::kFacPairs) {
-                    rm = std::max(rm, re - rs);
-                    qm = std::max(qm, nq);
-                }
-                own += (rsp::fac_pairs_at(std::min(re - rs, rsp::kFacRow)) + 2 * std::min(nq, rsp::kFacPairs) + 3) & ~3;
-            }
-            if (rm == 0 || qm == 0) continue;
-            const int stride = (rsp::fac_pairs_at(rm) + 2 * qm + 3) & ~3;
-            const long long cnt = lp[(size_t)l + 1] - lp[(size_t)l];
-            if (cnt * stride > 2 * own) continue;  // padding would dominate
-            if (total + cnt * stride > slot_cap) continue;
-            hp.fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, rm, qm, 0};
-            total += cnt * stride;
-            slot_levels.push_back(l);
-        }
+    for (int l = 0; l < nlev; l++) {
+        const LevStat &st = ls[(size_t)l];
+        if (!st.fat || st.rm == 0 || st.qm == 0) continue;
+        const int stride = (rsp::fac_pairs_at(st.rm) + 2 * st.qm + 3) & ~3;
+        const long long cnt = lp[(size_t)l + 1] - lp[(size_t)l];
+        if (cnt * stride > 2 * st.own) continue;  // padding would dominate
+        if (total + cnt * stride > slot_cap) continue;
+        hp.fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, st.rm, st.qm, 0};
+        total += cnt * stride;
+        slot_levels.push_back(l);
     }
     hp.slot_total = total;
     // flow runs: maximal runs of >= 2 slot-layout fat levels without
@@ -858,16 +1041,7 @@ void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, 
     hp.ffitems.clear();
     if (env_int("RSP_ILU_FLOW_PLAN", 1) != 0) {
         const int gate_d = env_int("RSP_ILU_FLOW_GATE", 3);
-        auto flowable = [&](int l) {
-            const rsp::FacSlotLevel &sl = hp.fslev[(size_t)l];
-            if (sl.stride <= 0) return false;
-            for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
-                const int i = rows_l[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
-                if (re - rs > rsp::kFacRow || sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs] > rsp::kFacPairs)
-                    return false;
-            }
-            return true;
-        };
+        auto flowable = [&](int l) { return hp.fslev[(size_t)l].stride > 0 && ls[(size_t)l].all_lds; };
         for (const rsp::LevelSeg &sg : hp.fplan.segs) {
             if (sg.thin) continue;
             for (int l = sg.lb; l < sg.le;) {
@@ -878,31 +1052,40 @@ void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, 
                 int e = l + 1;
                 while (e < sg.le && flowable(e)) e++;
                 if (e - l >= 2) {
-                    rsp::FacFlowRun r{l, e, (int)hp.ffitems.size(), 0};
-                    for (int v = l; v < e; v++) {
-                        const rsp::FacSlotLevel &sl = hp.fslev[(size_t)v];
-                        const int lg = v - gate_d;
-                        const int gate = gate_d > 0 && lg >= l && lp[(size_t)lg + 1] > lp[(size_t)lg]
-                                             ? rows_l[(size_t)lp[(size_t)lg + 1] - 1] : -1;
-                        for (int x = lp[(size_t)v]; x < lp[(size_t)v + 1]; x++)
-                            hp.ffitems.push_back({sl.off + (long long)(x - lp[(size_t)v]) * sl.stride,
-                                                  sl.rm | sl.qm << 16, gate});
-                    }
-                    r.c1 = (int)hp.ffitems.size();
-                    hp.fruns.push_back(r);
+                    const int c0 = hp.fruns.empty() ? 0 : hp.fruns.back().c1;
+                    hp.fruns.push_back(rsp::FacFlowRun{l, e, c0, c0 + lp[(size_t)e] - lp[(size_t)l]});
                 }
                 l = e;
             }
         }
+        hp.ffitems.resize(hp.fruns.empty() ? 0 : (size_t)hp.fruns.back().c1);
+        for (const rsp::FacFlowRun &r : hp.fruns)
+            pfor_dyn(r.le - r.lb, lp[(size_t)r.le] - lp[(size_t)r.lb], 1 << 14, [&](int j) {
+                const int v = r.lb + j;
+                const rsp::FacSlotLevel &sl = hp.fslev[(size_t)v];
+                const int lg = v - gate_d;
+                const int gate = gate_d > 0 && lg >= r.lb && lp[(size_t)lg + 1] > lp[(size_t)lg]
+                                     ? rows_l[(size_t)lp[(size_t)lg + 1] - 1] : -1;
+                for (int x = lp[(size_t)v]; x < lp[(size_t)v + 1]; x++)
+                    hp.ffitems[(size_t)(r.c0 + x - lp[(size_t)r.lb])] =
+                        rsp::FacFlowItem{sl.off + (long long)(x - lp[(size_t)v]) * sl.stride, sl.rm | sl.qm << 16, gate};
+            });
     }
     if (hp.ffitems.empty()) hp.ffitems.push_back({0, 0, -1});  // keep the device array non-empty
-    for (int l : slot_levels) {
+    std::vector<long long> sd0(slot_levels.size() + 1, 0);
+    for (size_t j = 0; j < slot_levels.size(); j++)
+        sd0[j + 1] = sd0[j] + lp[(size_t)slot_levels[j] + 1] - lp[(size_t)slot_levels[j]];
+    hp.slot_desc.resize((size_t)sd0.back());
+    hp.slot_offs.resize((size_t)sd0.back());
+    pfor_dyn((int)slot_levels.size(), sd0.back(), 1 << 14, [&](int j) {
+        const int l = slot_levels[(size_t)j];
         const rsp::FacSlotLevel &sl = hp.fslev[(size_t)l];
         for (int x = lp[(size_t)l]; x < lp[(size_t)l + 1]; x++) {
-            hp.slot_desc.push_back(int4{x, sl.rm, sl.qm, 0});
-            hp.slot_offs.push_back(sl.off + (long long)(x - lp[(size_t)l]) * sl.stride);
+            const size_t o = (size_t)(sd0[(size_t)j] + x - lp[(size_t)l]);
+            hp.slot_desc[o] = int4{x, sl.rm, sl.qm, 0};
+            hp.slot_offs[o] = sl.off + (long long)(x - lp[(size_t)l]) * sl.stride;
         }
-    }
+    });
 }
 
 

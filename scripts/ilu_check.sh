@@ -1,18 +1,22 @@
 #!/bin/bash
-# ILU GPU tests + one config-3 timing run (+ optional trace of named matrices).
-#   bash scripts/ilu_check.sh <tag> [trace-matrices]
+# ILU pass on the GPU box: ILU GPU tests, analysis phase times
+# (RSP_ILU_TIMING=2) over config 3, config-3 factor / solve timing.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${1:-ilu}
-O=gpurun_out/$TAG
-mkdir -p "$O"
+OUT="$ROOT/gpurun_out/$TAG"
+mkdir -p "$OUT"
+cd "$ROOT"
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests/test_gpu_ilu0.py tests/test_gpu_drivers.py -q -x -rf > "$O/pytest.log" 2>&1
-rc=$?; tail -3 "$O/pytest.log"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python scripts/bench_ilu0.py --json "$O/ilu.json" > "$O/ilu.txt" 2> "$O/ilu.err" || { tail -20 "$O/ilu.err"; exit 1; }
-cat "$O/ilu.txt"
-if [ -n "${2:-}" ]; then
-    timeout -k 10 300 python scripts/ilu_trace.py "$2" > "$O/trace.txt" 2>&1 && \
-    RSP_ILU_TRACE_CLK=1 timeout -k 10 300 python scripts/ilu_trace.py "$2" >> "$O/trace.txt" 2>&1
-    grep -v amdgpu.ids "$O/trace.txt"
-fi
+step() {  # name, limit, command...
+    local name=$1 lim=$2; shift 2
+    echo "== $name"
+    timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+    local rc=$?
+    echo "$name rc=$rc"; tail -3 "$OUT/$name.out"
+    if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.err"; exit $rc; fi
+}
+M=2cubes_sphere,ASIC_320ks,Baumann,cfd2,crashbasis,ct20stif,dc1,Dubcova3,ecology2,FEM_3D_thermal2,G2_circuit,Goodwin_095,matrix-new_3,offshore,para-10,parabolic_fem,ss1,stomach,thermomech_TK,tmt_unsym,xenon2
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_ilu 600 python -u -m pytest tests/test_gpu_ilu0.py tests/test_gpu_drivers.py -x -q --timeout 300 --timeout-method thread
+RSP_ILU_TIMING=2 step an_timing 300 python scripts/ilu_analysis_timing.py $M
+step ilu 300 python scripts/bench_ilu0.py --json "$OUT/ilu.json"

@@ -188,6 +188,19 @@ def test_schedule_variants(handle, monkeypatch, thin_solve, thin_factor, name, s
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
+@pytest.mark.parametrize("piece", [1, 700, 1 << 30])
+@pytest.mark.parametrize("name,scale", [("dc1", 0.2), ("parabolic_fem", 0.05), ("crashbasis", 0.05)])
+def test_factor_plan_pieces(handle, monkeypatch, piece, name, scale):
+    """The thin factor runs planned in pieces (in parallel on the host) and
+    joined by an empty chunk — one piece per level (1), pieces of ~700
+    positions, one piece per run — give the same bits."""
+    monkeypatch.setenv("RSP_ILU_PIECE_ITEMS", str(piece))
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float64, handle, x=x)
+    compare(A, torch.float32, handle, x=x)
+
+
 @pytest.mark.parametrize("slot,lds,pad,wlds", [(0, 1, 0, 0), (0, 0, 1, 1), (1, 1, 1, 1), (1, 1, 1, 0)])
 @pytest.mark.parametrize("name,scale", [("FEM_3D_thermal2", 0.1), ("Goodwin_095", 0.1), ("crashbasis", 0.1),
                                         ("ASIC_320ks", 0.1)])

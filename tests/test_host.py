@@ -261,6 +261,25 @@ def test_ilu_analysis_host_levels_and_digest(name, scale):
     assert all(v >= 0 for v in ph)
 
 
+@pytest.mark.parametrize("name,scale", [("dc1", 0.3), ("parabolic_fem", 0.3), ("tmt_unsym", 0.05)])
+def test_ilu_analysis_plan_thread_independent(monkeypatch, name, scale):
+    """The plans are built by parallel phases (rows, levels, chunks and factor
+    pieces as work items): the same plan on 1, 3 and 8 host threads, and with
+    the thin factor runs cut into many small pieces the plan still differs
+    from the one-piece plan only by construction (digests differ, both stable)."""
+    A = csr.surrogate(name, scale)
+    dg = set()
+    for t in ("1", "3", "8"):
+        monkeypatch.setenv("OMP_NUM_THREADS", t)
+        st, _, _, d, _ = _analysis_host(A)
+        assert st == 0
+        dg.add(d)
+    assert len(dg) == 1
+    monkeypatch.setenv("RSP_ILU_PIECE_ITEMS", "500")
+    small = {_analysis_host(A)[3] for t in ("1", "8") if not monkeypatch.setenv("OMP_NUM_THREADS", t)}
+    assert len(small) == 1 and small != dg
+
+
 def test_ilu_analysis_host_rejects_malformed():
     for rp, ci in (([0, 2, 4], [1, 0, 0, 1]), ([0, 2, 4], [0, 0, 0, 1]), ([0, 1, 2], [0, 5])):
         A = csr.CsrMatrix(0, 2, 2, len(ci), np.array(rp, np.int32), np.array(ci, np.int32), np.ones(len(ci)))
