@@ -621,6 +621,9 @@ def main():
                         "entry fp64); the kernel reads 16-bit column offsets where a tile spans < 65536 "
                         "columns, so it moves index_bytes_saved fewer: moved_* below",
                 "index_bytes_saved_per_launch": int(saved64 / per_step),
+                # share of stored entries read as 16-bit offsets (rank 0; halo layouts at N > 1
+                # lose it on boundary tiles whose columns span the receive region)
+                "entries_16bit_share_rank0": round(saved64 / 2 / max(1, sum(s.nnz_local for s in slices)), 4),
                 "moved_achieved": round(moved_achieved, 1),
                 "moved_frac": round(moved_achieved / HBM_PEAK_GBS, 4),
             },

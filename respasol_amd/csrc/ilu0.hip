@@ -610,9 +610,14 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
     __shared__ int4 litem[K];               // pos, pairs (start | count << 16), divisor index, zr
     __shared__ int lpair[rsp::kRndPairs];   // operand indices l_ik | u_kj << 16
     __shared__ int lrnd[rsp::kRndRounds + 1];
+    __shared__ unsigned char lfirst[rsp::kRndRounds + 1];  // round opens a level (rsp::kRndLevelStart)
+    __shared__ int lds_rdone;  // multi-wave narrow runs: absolute rounds completed
     const int tid = threadIdx.x, lane = tid & 63;
     T *vals = (T *)a.vals;
-    if (tid == 0) V[kZero] = T(0);
+    if (tid == 0) {
+        V[kZero] = T(0);
+        lds_rdone = INT_MIN;  // ordered before any use by the first chunk's barriers
+    }
     typedef const __attribute__((address_space(4))) int *ChunkPtr;  // scalar loads
     const ChunkPtr chunks = (ChunkPtr)a.rchunks;
     auto chunk = [&](int c) {
@@ -676,8 +681,14 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 lpair[tid + j * NTH] = idx(P.pr[j] & 0xffff, par) | idx(P.pr[j] >> 16, par) << 16;
 #pragma unroll
         for (int j = 0; j < RPT; ++j)
-            if (tid + j * NTH < nr) lrnd[tid + j * NTH] = P.rs[j];
-        if (tid == 0) lrnd[nr] = ni;
+            if (tid + j * NTH < nr) {
+                lrnd[tid + j * NTH] = P.rs[j] & (rsp::kRndLevelStart - 1);
+                lfirst[tid + j * NTH] = (P.rs[j] & rsp::kRndLevelStart) != 0;
+            }
+        if (tid == 0) {
+            lrnd[nr] = ni;
+            lfirst[nr] = 1;
+        }
         lds_barrier();
     };
     // An item: its value in the chunk's LDS slot and (wide rounds, STORE) in
@@ -731,6 +742,114 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
             if (m) return b + __builtin_ctzll(m);
         }
     };
+    // Narrow run on KW waves (a.narrow_waves, deferred stores only): the run's
+    // rounds are cut into segments at the rounds that open a level (a level's
+    // rounds depend on each other through its rows' l_ik: one wave runs a
+    // segment in order, its in-order LDS accesses ordering them, as in the
+    // one-wave run), and wave w takes segments w, w + KW, ... Before waiting,
+    // a wave loads what no value of the run feeds — the first two rounds'
+    // item records, initial values a_ij and first four pair indices; then it
+    // waits until the segment before its own is complete (an LDS counter of
+    // absolute rounds done, advanced by each segment's wave after its value
+    // stores, in-order LDS), and only then reads operands (divisors, l_ik,
+    // u_kj) and runs the fma chains and divisions. While one wave is on its
+    // chain, the others have prepared their next levels. Same items, same
+    // pairs in the same order, same divisions as the one-wave run: same bits.
+    struct ItemPre {
+        int4 r;
+        T v;
+        int pr[4];
+    };
+    auto item_pre = [&](int it, int cb) {
+        ItemPre p;
+        p.r = litem[it];
+        p.v = V[cb + it];
+        const int u0 = p.r.y & 0xffff, u1 = u0 + (p.r.y >> 16);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) p.pr[b] = lpair[min(u0 + b, max(u1 - 1, 0))];
+        return p;
+    };
+    auto item_post = [&](int it, int cb, const ItemPre &p) {
+        const int4 r = p.r;
+        T v = p.v;
+        const T dv = V[r.z >= 0 ? r.z : kZero];
+        const int u0 = r.y & 0xffff, u1 = u0 + (r.y >> 16);
+        if (u1 > u0) {
+            T l[4], w[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                l[b] = V[p.pr[b] & 0xffff];
+                w[b] = V[p.pr[b] >> 16];
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (u0 + b < u1) v = fma_t(-l[b], w[b], v);
+            for (int u = u0 + 4; u < u1; u += 4) {  // items of more than four pairs (rare)
+                int pr[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) pr[b] = lpair[min(u + b, u1 - 1)];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    l[b] = V[pr[b] & 0xffff];
+                    w[b] = V[pr[b] >> 16];
+                }
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (u + b < u1) v = fma_t(-l[b], w[b], v);
+            }
+        }
+        if (r.z >= 0) v = v / dv;
+        V[cb + it] = v;
+    };
+    auto wave_order = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    };
+    auto run_mw = [&](const rsp::RndChunk &ch, int q, int qe, int cb, int KW) {
+        const int w = tid >> 6;
+        auto seg_end = [&](int s) {  // first round > s that opens a level, or qe (wave-uniform)
+            for (int b = s + 1;; b += 64) {
+                const int qq = b + lane;
+                const unsigned long long m = __ballot(qq >= qe || lfirst[qq]);
+                if (m) return min(b + (int)__builtin_ctzll(m), qe);
+            }
+        };
+        int k = 0;
+        for (int s0 = q; s0 < qe; ++k) {
+            const int s1 = seg_end(s0);
+            if (k % KW == w) {
+                const int b0 = lrnd[s0], n0 = lrnd[s0 + 1] - b0;
+                const bool has1 = s0 + 1 < s1;
+                const int b1 = has1 ? lrnd[s0 + 1] : b0, n1 = has1 ? lrnd[s0 + 2] - b1 : 0;
+                const ItemPre p0 = item_pre(b0 + min(lane, n0 - 1), cb);
+                const ItemPre p1 = item_pre(b1 + min(lane, max(n1 - 1, 0)), cb);
+                if (s0 > q) {  // bounded: a plan bug gives wrong bits in the tests, never a hung GPU
+                    const int want = ch.r0 + s0;
+                    for (int i = 0; i < (1 << 26) &&
+                                    __hip_atomic_load(&lds_rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want;
+                         ++i) {
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                }
+                if (lane < n0) item_post(b0 + lane, cb, p0);
+                wave_order();
+                if (has1) {
+                    if (lane < n1) item_post(b1 + lane, cb, p1);
+                    wave_order();
+                    for (int qq = s0 + 2; qq < s1; ++qq) {  // levels of more than two rounds
+                        const int bq = lrnd[qq];
+                        if (bq + lane < lrnd[qq + 1]) process(bq + lane, cb, std::false_type());
+                        wave_order();
+                    }
+                }
+                asm volatile("" ::: "memory");  // value stores before the counter (in-order LDS)
+                if (lane == 0)
+                    __hip_atomic_store(&lds_rdone, ch.r0 + s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            s0 = s1;
+        }
+    };
     auto rounds = [&](int c, const rsp::RndChunk &ch) {
         const int nr = ch.r1 - ch.r0, cb = (c & 1) * K;
         for (int q = 0; q < nr;) {
@@ -748,7 +867,10 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
                     }
                 };
-                if (tid < 64) {  // (a software-pipelined form of this loop measured slower)
+                const int KW = min(a.narrow_waves, NTH / 64);
+                if (defer && KW > 1) {
+                    if (tid < 64 * KW) run_mw(ch, q, qe, cb, KW);
+                } else if (tid < 64) {  // (a software-pipelined form of this loop measured slower)
                     if (defer)
                         run(std::false_type());
                     else

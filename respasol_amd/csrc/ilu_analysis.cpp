@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <mutex>
 #include <thread>
 
@@ -164,11 +165,13 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) t += padded(nt_row[(size_t)order[(size_t)x]]);
         lpad[(size_t)l] = t;
     });
+    // RSP_ILU_THIN_TERMS: tuning knob (a thin level's padded terms, <= kChunkTerms)
+    const int thin_terms = std::min(env_int("RSP_ILU_THIN_TERMS", rsp::kThinSolveTerms), rsp::kChunkTerms);
     sp.segs.clear();
     for (int l = 0; l < nlev; l++) {
         const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
         const int thin = (cnt <= thin_rows && cnt <= rsp::kThinThreads && cnt <= rsp::kChunkRows &&
-                          lpad[(size_t)l] <= rsp::kChunkTerms) ? 1 : 0;
+                          lpad[(size_t)l] <= thin_terms) ? 1 : 0;
         if (!sp.segs.empty() && sp.segs.back().thin == thin && sp.segs.back().le == l)
             sp.segs.back().le = l + 1;
         else
@@ -406,7 +409,7 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
 // The staged positions of the current chunk sit in a piece-private hash.
 static constexpr int kRndPieceItems = 1 << 17;
 
-static void build_factor_plan(int n, const std::vector<int> &rp, const std::vector<int> &ci,
+static void build_factor_plan(int n, const int *rp, const int *ci,
                               const std::vector<int> &dpos, const std::vector<int> &hasdiag,
                               const IluSymbolic &sym, const std::vector<int> &ptr,
                               const std::vector<int> &rows, int thin_rows, FacPlan &fp) {
@@ -520,6 +523,7 @@ static void build_factor_plan(int n, const std::vector<int> &rp, const std::vect
         std::vector<int> rcount, fresh, ipairs;
         open_chunk();
         long long last_round_key = -1;
+        int last_round_level = -1;  // level of the chunk's last round (-1: none yet)
         for (int l = pc.lb; l < pc.le; l++) {
             ritems.clear();
             for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
@@ -566,15 +570,17 @@ static void build_factor_plan(int n, const std::vector<int> &rp, const std::vect
                         close_chunk();
                         open_chunk();
                         last_round_key = -1;
+                        last_round_level = -1;
                         continue;
                     }
                     for (int q : fresh) {
                         hput(q, nstg++);
                         o.staged.push_back(q);
                     }
-                    if (new_round) {
-                        o.rounds.push_back(slot);
+                    if (new_round) {  // flagged where it opens a level in this chunk
+                        o.rounds.push_back(slot | (l != last_round_level ? rsp::kRndLevelStart : 0));
                         last_round_key = key;
+                        last_round_level = l;
                     }
                     const int pstart = (int)o.pairs.size() - ch.p0;
                     o.pairs.insert(o.pairs.end(), ipairs.begin(), ipairs.end());
@@ -861,36 +867,38 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
         nl = std::max(nl, l + 1);
     }
     // transposed strict lower: row k lists (j, pos) for l_jk, j descending
-    // (each worker owns a range of columns k and scans the whole strict
-    // lower part for them: j descending, so its lists come out in order)
+    // (counts and slots by relaxed atomics over row blocks, then each
+    // column's entries sorted to j descending)
     std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
     ltp.assign((size_t)n + 1, 0);
-    long long nlo = 0;
-    for (int j = 0; j < n; j++) nlo += dpos[(size_t)j] - rp[j];
-    const int nb = (int)std::max<long long>(1, std::min<long long>(host_threads(), nlo / (1 << 16)));
-    auto kr = [&](int t) { return std::make_pair((int)((long long)n * t / nb), (int)((long long)n * (t + 1) / nb)); };
-    pfor_dyn(nb, nlo, 1, [&](int t) {
-        const int ka = kr(t).first, kb = kr(t).second;
-        for (int j = 0; j < n; j++)
-            for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
-                const int k = ci[p];
-                if (k >= ka && k < kb) ltp[(size_t)k + 1]++;
-            }
+    pfor(n, 1 << 14, [&](long long a, long long b) {
+        for (long long j = a; j < b; j++)
+            for (int p = rp[j]; p < dpos[(size_t)j]; p++) __atomic_fetch_add(&ltp[(size_t)ci[p] + 1], 1, __ATOMIC_RELAXED);
     });
     for (int k = 0; k < n; k++) ltp[(size_t)k + 1] += ltp[(size_t)k];
-    lts.resize((size_t)ltp[(size_t)n]);
-    ltc.resize((size_t)ltp[(size_t)n]);
-    pfor_dyn(nb, nlo, 1, [&](int t) {
-        const int ka = kr(t).first, kb = kr(t).second;
-        std::vector<int> fill(ltp.begin() + ka, ltp.begin() + kb);
-        for (int j = n - 1; j >= 0; j--)
-            for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
-                const int k = ci[p];
-                if (k < ka || k >= kb) continue;
-                const int slot = fill[(size_t)(k - ka)]++;
-                lts[(size_t)slot] = p;
-                ltc[(size_t)slot] = j;
+    const size_t nlo = (size_t)ltp[(size_t)n];
+    std::vector<unsigned long long> key(nlo);  // (n - 1 - j) << 32 | position
+    {
+        std::vector<int> fill(ltp.begin(), ltp.end() - 1);
+        pfor(n, 1 << 14, [&](long long a, long long b) {
+            for (long long j = a; j < b; j++)
+                for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
+                    const int slot = __atomic_fetch_add(&fill[(size_t)ci[p]], 1, __ATOMIC_RELAXED);
+                    key[(size_t)slot] = (unsigned long long)(n - 1 - j) << 32 | (unsigned)p;
+                }
+        });
+    }
+    lts.resize(nlo);
+    ltc.resize(nlo);
+    pfor(n, 1 << 14, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) {
+            const size_t q0 = (size_t)ltp[(size_t)k], q1 = (size_t)ltp[(size_t)k + 1];
+            if (q1 - q0 > 1) std::sort(key.begin() + (long)q0, key.begin() + (long)q1);
+            for (size_t q = q0; q < q1; q++) {
+                lts[q] = (int)(key[q] & 0xffffffffu);
+                ltc[q] = n - 1 - (int)(key[q] >> 32);
             }
+        }
     });
     // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
     std::vector<int> lvt((size_t)n, 0);
@@ -922,61 +930,60 @@ rsp_status_t plan_symbolic(const int *rpp, const int *cip, IluHostPlan &hp) {
     return RSP_STATUS_SUCCESS;
 }
 
-void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, IluHostPlan &hp) {
-    const int n = hp.n, nnz_s = hp.nnz_s;
-    const std::vector<int> rp(rpp, rpp + (size_t)n + 1), ci(cip, cip + (size_t)nnz_s);
-    const std::vector<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
+static void timed_plan(int n, const char *what, const std::function<void()> &fn) {
+    const double t0 = now_ms();
+    fn();
+    if (env_int("RSP_ILU_TIMING", 0) >= 2)  // diagnostics: per-plan wall time
+        fprintf(stderr, "rsp_ilu0_analysis n=%d   plan %-10s %8.2f ms\n", n, what, now_ms() - t0);
+}
+
+// RSP_ILU_THIN_SOLVE / RSP_ILU_THIN_FACTOR: tuning knobs (0 = no thin runs)
+static int thin_solve_rows() {
+    return std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
+}
+
+void plan_solves(const int *rp, const int *ci, IluHostPlan &hp) {
+    const int n = hp.n;
+    const std::vector<int> &dpos = hp.dpos;
     const std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
-    // RSP_ILU_THIN_SOLVE / RSP_ILU_THIN_FACTOR: tuning knobs (0 = no thin runs)
-    const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
+    const int thin_solve = thin_solve_rows();
+    long long nlo = 0;
+    for (int i = 0; i < n; i++) nlo += dpos[(size_t)i] - rp[(size_t)i];
+    hp.L.batch = hp.LT.batch = chain_batch(nlo, n);
+    for (DagHost *d : {&hp.L, &hp.LT})  // thin-run term groups
+        d->group = env_int("RSP_ILU_GROUP", d->batch == 2 ? 2 : 4) == 2 ? 2 : 4;
+    // the two DAGs' plans (flat terms in level order, thin-run chunks, y
+    // sources) are independent: built concurrently
+    std::thread tl([&] {
+        timed_plan(n, "L", [&] {
+            build_solve_plan(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, std::vector<int>(),
+                             [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; },
+                             [&](int i, auto emit) {
+                                 for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
+                             }, hp.L.sp);
+        });
+    });
+    timed_plan(n, "LT", [&] {
+        build_solve_plan(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, std::vector<int>(),
+                         [&](int i) { return ltp[(size_t)i + 1] - ltp[(size_t)i]; },
+                         [&](int i, auto emit) {
+                             for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++)
+                                 emit(lts[(size_t)q], ltc[(size_t)q]);
+                         }, hp.LT.sp);
+    });
+    tl.join();
+    hp.L.planned = hp.LT.planned = true;
+}
+
+void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &hp) {
+    const int n = hp.n, nnz_s = hp.nnz_s;
+    const std::vector<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
     const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
     IluSymbolic &sym = hp.sym;
-    {
-        long long nlo = 0;
-        for (int i = 0; i < n; i++) nlo += dpos[(size_t)i] - rp[(size_t)i];
-        hp.L.batch = hp.LT.batch = chain_batch(nlo, n);
-        for (DagHost *d : {&hp.L, &hp.LT})  // thin-run term groups
-            d->group = env_int("RSP_ILU_GROUP", d->batch == 2 ? 2 : 4) == 2 ? 2 : 4;
-        hp.fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
-    }
-    // the factor plan and the solve plans (flat terms in level order, thin-run
-    // chunks, y sources) are independent: built concurrently
-    {
-        std::vector<std::thread> th;
-        const bool tm = env_int("RSP_ILU_TIMING", 0) >= 2;  // diagnostics: per-plan wall time
-        auto timed = [tm, n](const char *what, auto fn) {
-            const double t0 = now_ms();
-            fn();
-            if (tm) fprintf(stderr, "rsp_ilu0_analysis n=%d   plan %-10s %8.2f ms\n", n, what, now_ms() - t0);
-        };
-        th.emplace_back([&] {
-            timed("factor", [&] {
-                build_factor_plan(n, rp, ci, dpos, hasdiag, sym, hp.L.ptr, hp.L.rows, thin_factor, hp.fplan);
-            });
-        });
-        th.emplace_back([&] {
-            timed("L", [&] {
-                build_solve_plan(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, std::vector<int>(),
-                                 [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; },
-                                 [&](int i, auto emit) {
-                                     for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
-                                 }, hp.L.sp);
-            });
-        });
-        th.emplace_back([&] {
-            timed("LT", [&] {
-                build_solve_plan(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, std::vector<int>(),
-                                 [&](int i) { return ltp[(size_t)i + 1] - ltp[(size_t)i]; },
-                                 [&](int i, auto emit) {
-                                     for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++)
-                                         emit(lts[(size_t)q], ltc[(size_t)q]);
-                                 }, hp.LT.sp);
-            });
-        });
-        if (want_u) th.emplace_back([&] { plan_u(rp.data(), ci.data(), hp); });
-        for (std::thread &x : th) x.join();
-    }
-    hp.L.planned = hp.LT.planned = true;
+    hp.fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
+    timed_plan(n, "factor", [&] {
+        build_factor_plan(n, rp, ci, dpos, hasdiag, sym, hp.L.ptr, hp.L.rows, thin_factor, hp.fplan);
+    });
     const std::vector<int> &rows_l = hp.L.rows;
     const long long nx = (long long)rows_l.size();
     hp.frow.assign(std::max<size_t>(rows_l.size(), 1), rsp::FacRow{});
@@ -1088,6 +1095,15 @@ void plan_rest(const int *rpp, const int *cip, long long slot_cap, bool want_u, 
     });
 }
 
+
+void plan_rest(const int *rp, const int *ci, long long slot_cap, bool want_u, IluHostPlan &hp) {
+    std::thread ts([&] {
+        plan_solves(rp, ci, hp);
+        if (want_u) plan_u(rp, ci, hp);
+    });
+    plan_factor(rp, ci, slot_cap, hp);
+    ts.join();
+}
 
 rsp_status_t plan_host(int n, const int *rp, const int *ci, long long slot_cap, bool want_u, IluHostPlan &hp,
                        Phases &ph) {

@@ -99,11 +99,15 @@ constexpr int kPhases = 6;  // phase slots of Phases::ms (marks in call order)
 //   plan_validate: pattern checks, diagonal positions, structural zero;
 //   plan_levels:   level sets of L and L^T, the transposed L (sequential);
 //   plan_symbolic: update lists, stages, stage order, divisor positions;
-//   plan_rest:     factor and solve plans, FacRow records, slot layout
-//                  (needs sym.upd_ptr / upd_l / upd_u / stage).
+//   plan_solves:   the L and L^T solve plans (needs the levels only);
+//   plan_factor:   the factor plan, FacRow records, slot layout, flow runs
+//                  (needs sym.upd_ptr / upd_l / upd_u / stage);
+//   plan_rest:     both (the solves on a second thread).
 rsp_status_t plan_validate(int n, const int *rp, const int *ci, IluHostPlan &hp);
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp);
 rsp_status_t plan_symbolic(const int *rp, const int *ci, IluHostPlan &hp);
+void plan_solves(const int *rp, const int *ci, IluHostPlan &hp);
+void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &hp);
 void plan_rest(const int *rp, const int *ci, long long slot_cap, bool want_u, IluHostPlan &hp);
 // The symbolic factor of the given rows on the host (the device analysis'
 // long rows): counts when cnt != nullptr, else pairs at ptr + stages, stage

@@ -19,6 +19,7 @@
 #include <new>
 #include <chrono>
 #include <mutex>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -1104,9 +1105,18 @@ static long long slot_cap_ints() {
 static constexpr int kAnDevRow = 1024;
 static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const int *d_rp, const int *d_ci,
                                         const std::vector<int> &rp, std::vector<int> &ci, rsp_an::IluHostPlan &hp,
-                                        rsp_an::Phases &ph) {
+                                        rsp_an::Phases &ph, const std::function<void()> &after_levels) {
     const int n = hp.n, nnz_s = hp.nnz_s;
     hipStream_t s = h->stream;
+    const bool tm3 = env_int("RSP_ILU_TIMING", 0) >= 3;  // diagnostics: sub-phase wall times
+    auto t_last = std::chrono::steady_clock::now();
+    auto sub = [&](const char *what) {
+        if (!tm3) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "rsp_ilu0_analysis n=%d     %-22s %8.2f ms\n", n, what,
+                std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     std::vector<int> dev_rows, long_rows;
     for (int i = 0; i < n; i++) (rp[(size_t)i + 1] - rp[(size_t)i] <= kAnDevRow ? dev_rows : long_rows).push_back(i);
     size_t scan_bytes = 0;
@@ -1126,6 +1136,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     ar.space((void **)&d_scratch, (size_t)std::max(nnz_s, 1) * 4);
     ar.space(&d_scan, std::max<size_t>(scan_bytes, 16));
     ar.up(&d_rows, dev_rows);
+    sub("arena");
     RSP_CHECK_HIP(ar.commit(&f->d_arena_sym, s));
     const int flags0[2] = {0, INT_MAX};
     int flags[2] = {0, INT_MAX};
@@ -1134,6 +1145,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     RSP_CHECK_HIP(hipMemcpyAsync(flags, d_flags, sizeof(flags), hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
     if (flags[0]) return RSP_STATUS_INVALID_VALUE;  // a column out of range or a row not increasing
+    sub("rows kernel + flags");
     hp.structural_zero = flags[1] == INT_MAX ? -1 : flags[1];
     const int n_c[3] = {(int)dev_rows.size(), 0, 0};
     const int *rows_c[3] = {d_rows, nullptr, nullptr};
@@ -1146,6 +1158,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     }
     if (nnz_s > 0) RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), d_ci, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
+    sub("count kernel + D2H pattern");
     // the long rows' counts on the host
     std::vector<int> hcnt(long_rows.empty() ? 0 : (size_t)nnz_s);
     rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), hcnt.data(),
@@ -1153,12 +1166,14 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     for (int i : long_rows)
         RSP_CHECK_HIP(hipMemcpyAsync(d_cnt + rp[(size_t)i], hcnt.data() + rp[(size_t)i],
                                      (size_t)(rp[(size_t)i + 1] - rp[(size_t)i]) * 4, hipMemcpyHostToDevice, s));
+    sub("long-row counts");
     RSP_CHECK_HIP(hipMemsetAsync(d_cnt + nnz_s, 0, 4, s));
     RSP_CHECK_HIP(rsp_k::ilu_an_scan(d_cnt, f->d_upd_ptr, nnz_s + 1, d_scan, &scan_bytes, s));
     hp.sym.upd_ptr.resize((size_t)nnz_s + 1);
     RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_ptr.data(), f->d_upd_ptr, ((size_t)nnz_s + 1) * 4,
                                  hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
+    sub("scan + D2H upd_ptr");
     ph.mark("device rows");
     // a pair count past int would overflow the plans' indices
     const int total = hp.sym.upd_ptr[(size_t)nnz_s];
@@ -1167,6 +1182,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     ap.space((void **)&f->d_upd_l, (size_t)std::max(total, 1) * 4);
     ap.space((void **)&f->d_upd_u, (size_t)std::max(total, 1) * 4);
     RSP_CHECK_HIP(ap.commit(&f->d_arena_pairs, s));
+    sub("pairs arena");
     RSP_CHECK_HIP(rsp_k::ilu_an_fill(rows_c, n_c, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, d_scratch,
                                      f->d_upd_l, f->d_upd_u, s));
     RSP_CHECK_HIP(rsp_k::ilu_an_stages(n, kAnDevRow, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, f->d_upd_l,
@@ -1174,6 +1190,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     // the level sets on the host while the device fills the update lists
     rsp_an::plan_levels(rp.data(), ci.data(), hp);
     ph.mark("levels");
+    after_levels();  // the solve plans need nothing more: started here
     hp.sym.upd_l.resize((size_t)total);
     hp.sym.upd_u.resize((size_t)total);
     hp.sym.stage.resize((size_t)nnz_s);
@@ -1184,6 +1201,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     if (nnz_s > 0)
         RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.stage.data(), d_stage, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
+    sub("D2H pairs + stages");
     if (!long_rows.empty()) {  // the long rows' lists, stages, stage order, divisors on the host
         std::vector<int> lord((size_t)nnz_s), lend((size_t)nnz_s), udiv((size_t)nnz_s);
         rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), nullptr,
@@ -1202,6 +1220,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
         }
         RSP_CHECK_HIP(hipStreamSynchronize(s));
     }
+    sub("long rows");
     ph.mark("device symbolic");
     return RSP_STATUS_SUCCESS;
 }
@@ -1239,13 +1258,19 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     if (!hp) return RSP_STATUS_ALLOC_FAILED;
     hp->n = n;
     hp->nnz_s = nnz_s;
-    rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph);
+    // the solve plans are built on a second thread from the moment the levels
+    // exist, under the symbolic factor's transfers and the factor plan
+    std::thread solves;
+    rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph, [&] {
+        solves = std::thread([&] { rsp_an::plan_solves(rp.data(), ci.data(), *hp); });
+    });
+    if (st == RSP_STATUS_SUCCESS) rsp_an::plan_factor(rp.data(), ci.data(), slot_cap_ints(), *hp);
+    if (solves.joinable()) solves.join();
     if (st != RSP_STATUS_SUCCESS) {
         ilu_free_device(f);
         return st;
     }
     // the U DAG (--true-lu extension) is planned on its first use
-    rsp_an::plan_rest(rp.data(), ci.data(), slot_cap_ints(), false, *hp);
     ph.mark("plans");
     f->structural_zero = hp->structural_zero;
     f->n_updates = (long long)hp->sym.upd_l.size();
@@ -1484,6 +1509,7 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.fat_slots = f->d_fslots && env_int("RSP_ILU_FAT_SLOT", 1) != 0;
     a.fat_lds = env_int("RSP_ILU_FAT_LDS", 1) != 0;
     a.defer_rounds = env_int("RSP_ILU_DEFER", 8);  // A/B knob (thin factor runs)
+    a.narrow_waves = std::min(std::max(env_int("RSP_ILU_FNARROW_WAVES", 4), 1), rsp::kThinThreads / 64);
     a.rchunks = f->d_rchunks;
     a.ritems = f->d_ritems;
     a.rpairs = f->d_rpairs;

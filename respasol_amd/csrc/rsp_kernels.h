@@ -203,7 +203,8 @@ constexpr int kPadSrc = -(kYWin + 1); // source of a pad term: the zero slot aft
 constexpr int kIluWaves = 4;         // rows per 256-thread workgroup (fat factor levels, global path)
 constexpr int kFacRow = 256;         // fat factor levels: rows staged in LDS up to this many entries
 constexpr int kFacPairs = 1024;      // ... and this many update pairs (else the global path)
-constexpr int kThinSolveRows = 1024; // solve levels this small (and <= kChunkTerms terms) run thin
+constexpr int kThinSolveRows = 512;  // solve levels this small (and <= kThinSolveTerms terms) run thin
+constexpr int kThinSolveTerms = 2048; // (padded terms; wider levels run on all CUs: flow segments)
 constexpr int kThinFactorRows = 1024; // factor levels this small (and within kRndLevelItems) run thin
 // LDS-staged factor chunks (ilu0_chunked): a chunk is a run of levels whose
 // rows' positions ("items") and update pairs fit these budgets.
@@ -216,6 +217,7 @@ constexpr int kRndStaged = 4096;
 constexpr int kRndRounds = 2048;
 constexpr int kRndLevelItems = 2048;
 constexpr int kRndItemPairs = 1024;
+constexpr int kRndLevelStart = 1 << 15;  // rounds[]: this round opens a level (or a chunk)
 struct alignas(16) RndChunk {  // flat ranges of a chunk's items, pairs, staged values, rounds
     int i0, i1, p0, p1, s0, s1, r0, r1;
 };
@@ -299,6 +301,7 @@ struct IluArgs {
     unsigned long long *trace;  // diagnostics (RSP_ILU_FTRACE): 4 words per thin-run chunk, or null
     int trace_cap;
     int defer_rounds;  // narrow runs of at least this many rounds flush their items after the run
+    int narrow_waves;  // ... and run on this many waves, levels round-robin (RSP_ILU_FNARROW_WAVES)
     // flow runs (ilu0_flow)
     const FacFlowItem *fitems;  // device
     const FacFlowRun *fruns;    // host

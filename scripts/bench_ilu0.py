@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--set", default="moderate")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--json", default="")
+    ap.add_argument("--fp64-only", action="store_true", help="A/B runs: fp64 only (fp32 columns repeat it)")
     args = ap.parse_args()
     names = csr.surrogate_names(0 if args.set == "moderate" else 1) if args.set in ("moderate", "big") \
         else args.set.split(",")
@@ -96,8 +97,8 @@ def main():
     for name in names:
         A = csr.surrogate(name)
         r64 = run_one(h, A, torch.float64, False, args.reps)
-        r32p = run_one(h, A, torch.float32, False, args.reps)
-        r32 = run_one(h, A, torch.float32, True, args.reps)
+        r32p = r64 if args.fp64_only else run_one(h, A, torch.float32, False, args.reps)
+        r32 = r64 if args.fp64_only else run_one(h, A, torch.float32, True, args.reps)
         row = {"matrix": name, "n": A.m, "nnz_s": A.nnz_stored, "fp64": r64, "fp32": r32p, "fp32_ftz": r32}
         out.append(row)
         print(f"{name:16s} {A.m:8d} {A.nnz_stored:9d} {r64['levels_L']:5d} {r64['levels_LT']:5d} | "

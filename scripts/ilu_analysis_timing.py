@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    os.environ["RSP_ILU_TIMING"] = "1"
+    os.environ.setdefault("RSP_ILU_TIMING", "1")
     import torch
     from respasol_amd import csr
     from respasol_amd.sparse import Handle, Ilu0, upload_csr

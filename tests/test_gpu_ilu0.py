@@ -188,6 +188,18 @@ def test_schedule_variants(handle, monkeypatch, thin_solve, thin_factor, name, s
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
+@pytest.mark.parametrize("waves", [1, 2, 4, 16])
+@pytest.mark.parametrize("name,scale", [("dc1", 0.3), ("matrix-new_3", 0.2), ("G2_circuit", 0.3),
+                                        ("thermomech_TK", 0.2)])
+def test_factor_narrow_waves(handle, monkeypatch, waves, name, scale):
+    """Narrow factor runs shared by 1, 2, 4 or 16 waves (a level's rounds on
+    one wave, levels round-robin, an LDS counter between them): same bits."""
+    monkeypatch.setenv("RSP_ILU_FNARROW_WAVES", str(waves))
+    A = csr.surrogate(name, scale)
+    compare(A, torch.float64, handle)
+    compare(A, torch.float32, handle)
+
+
 @pytest.mark.parametrize("piece", [1, 700, 1 << 30])
 @pytest.mark.parametrize("name,scale", [("dc1", 0.2), ("parabolic_fem", 0.05), ("crashbasis", 0.05)])
 def test_factor_plan_pieces(handle, monkeypatch, piece, name, scale):
