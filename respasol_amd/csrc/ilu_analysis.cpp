@@ -415,28 +415,40 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
                               const std::vector<int> &rows, int thin_rows, FacPlan &fp) {
     const int nlev = (int)ptr.size() - 1;
     const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
+    // a level runs thin up to kRndFlowItems positions; up to kRndLevelItems
+    // when it could not run in a flow launch anyway (a row past the slot
+    // layout's kFacRow entries / kFacPairs pairs: circuit hubs). Wider levels
+    // are fat: in a flow run they spread over all CUs, where a thin run
+    // stages every position through one (A/B knobs RSP_ILU_THIN_FACTOR_ITEMS /
+    // RSP_ILU_THIN_FACTOR_FLOW)
     const int thin_items = env_int("RSP_ILU_THIN_FACTOR_ITEMS", rsp::kRndLevelItems);
+    const int thin_flow = env_int("RSP_ILU_THIN_FACTOR_FLOW", rsp::kRndFlowItems);
     const long long piece_items = std::max(1, env_int("RSP_ILU_PIECE_ITEMS", kRndPieceItems));
     const int nnz = rp[(size_t)n];
     // per level: positions and the largest update list
     std::vector<long long> litems((size_t)std::max(nlev, 1), 0);
     std::vector<int> lmaxp((size_t)std::max(nlev, 1), 0);
+    std::vector<char> lhub((size_t)std::max(nlev, 1), 0);
     pfor_dyn(nlev, nnz, 1 << 15, [&](int l) {
         long long items = 0;
         int maxp = 0;
+        bool hub = false;
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-            const int i = rows[(size_t)x];
-            items += rp[(size_t)i + 1] - rp[(size_t)i];
-            for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++)
+            const int i = rows[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
+            items += re - rs;
+            for (int p = rs; p < re; p++)
                 maxp = std::max(maxp, sym.upd_ptr[(size_t)p + 1] - sym.upd_ptr[(size_t)p]);
+            hub |= re - rs > rsp::kFacRow || sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs] > rsp::kFacPairs;
         }
         litems[(size_t)l] = items;
         lmaxp[(size_t)l] = maxp;
+        lhub[(size_t)l] = hub;
     });
     fp.segs.clear();
     for (int l = 0; l < nlev; l++) {
         const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
-        const int thin = (cnt <= thin_rows && litems[(size_t)l] <= thin_items && lmaxp[(size_t)l] <= rsp::kRndItemPairs) ? 1 : 0;
+        const long long lim = lhub[(size_t)l] ? thin_items : std::min(thin_items, thin_flow);
+        const int thin = (cnt <= thin_rows && litems[(size_t)l] <= lim && lmaxp[(size_t)l] <= rsp::kRndItemPairs) ? 1 : 0;
         if (!fp.segs.empty() && fp.segs.back().thin == thin && fp.segs.back().le == l)
             fp.segs.back().le = l + 1;
         else
@@ -1032,12 +1044,15 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
     std::vector<int> slot_levels;
     for (int l = 0; l < nlev; l++) {
         const LevStat &st = ls[(size_t)l];
-        if (!st.fat || st.rm == 0 || st.qm == 0) continue;
-        const int stride = (rsp::fac_pairs_at(st.rm) + 2 * st.qm + 3) & ~3;
+        if (!st.fat || st.rm == 0) continue;
+        // a level without update pairs keeps one (padding) pair slot per row:
+        // the kernels' pair loads are clamped to the level's qm - 1
+        const int qm = std::max(st.qm, 1);
+        const int stride = (rsp::fac_pairs_at(st.rm) + 2 * qm + 3) & ~3;
         const long long cnt = lp[(size_t)l + 1] - lp[(size_t)l];
         if (cnt * stride > 2 * st.own) continue;  // padding would dominate
         if (total + cnt * stride > slot_cap) continue;
-        hp.fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, st.rm, st.qm, 0};
+        hp.fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, st.rm, qm, 0};
         total += cnt * stride;
         slot_levels.push_back(l);
     }
@@ -1115,7 +1130,16 @@ rsp_status_t plan_host(int n, const int *rp, const int *ci, long long slot_cap, 
     st = plan_symbolic(rp, ci, hp);
     if (st != RSP_STATUS_SUCCESS) return st;
     ph.mark("symbolic");
+    // the plans see what they see after the device analysis: no host copy of
+    // the stage order, stage ends or divisor positions (kept for the digest)
+    std::vector<int> lord, lend, udiv;
+    lord.swap(hp.sym.lord);
+    lend.swap(hp.sym.lend);
+    udiv.swap(hp.udiv);
     plan_rest(rp, ci, slot_cap, want_u, hp);
+    lord.swap(hp.sym.lord);
+    lend.swap(hp.sym.lend);
+    udiv.swap(hp.udiv);
     ph.mark("plans");
     return RSP_STATUS_SUCCESS;
 }

@@ -216,6 +216,7 @@ constexpr int kRndPairs = 4096;
 constexpr int kRndStaged = 4096;
 constexpr int kRndRounds = 2048;
 constexpr int kRndLevelItems = 2048;
+constexpr int kRndFlowItems = 1024;  // ... kRndFlowItems if the level could run in a flow launch
 constexpr int kRndItemPairs = 1024;
 constexpr int kRndLevelStart = 1 << 15;  // rounds[]: this round opens a level (or a chunk)
 struct alignas(16) RndChunk {  // flat ranges of a chunk's items, pairs, staged values, rounds
