@@ -769,12 +769,25 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
         for (int b = 0; b < 4; ++b) p.pr[b] = lpair[min(u0 + b, max(u1 - 1, 0))];
         return p;
     };
-    auto item_post = [&](int it, int cb, const ItemPre &p) {
+    // short: no item of the wave's round has more than two pairs (wave-
+    // uniform), so only the first two pairs' operands are read and chained
+    auto item_post = [&](int it, int cb, const ItemPre &p, bool short2) {
         const int4 r = p.r;
         T v = p.v;
         const T dv = V[r.z >= 0 ? r.z : kZero];
         const int u0 = r.y & 0xffff, u1 = u0 + (r.y >> 16);
-        if (u1 > u0) {
+        if (short2) {
+            if (u1 > u0) {
+                T l[2], w[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    l[b] = V[p.pr[b] & 0xffff];
+                    w[b] = V[p.pr[b] >> 16];
+                }
+                v = fma_t(-l[0], w[0], v);
+                if (u1 > u0 + 1) v = fma_t(-l[1], w[1], v);
+            }
+        } else if (u1 > u0) {
             T l[4], w[4];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
@@ -824,6 +837,8 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 const int b1 = has1 ? lrnd[s0 + 1] : b0, n1 = has1 ? lrnd[s0 + 2] - b1 : 0;
                 const ItemPre p0 = item_pre(b0 + min(lane, n0 - 1), cb);
                 const ItemPre p1 = item_pre(b1 + min(lane, max(n1 - 1, 0)), cb);
+                const bool sh0 = !__ballot(lane < n0 && (p0.r.y >> 16) > 2);
+                const bool sh1 = !__ballot(lane < n1 && (p1.r.y >> 16) > 2);
                 if (s0 > q) {  // bounded: a plan bug gives wrong bits in the tests, never a hung GPU
                     const int want = ch.r0 + s0;
                     for (int i = 0; i < (1 << 26) &&
@@ -832,10 +847,10 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
                 }
-                if (lane < n0) item_post(b0 + lane, cb, p0);
+                if (lane < n0) item_post(b0 + lane, cb, p0, sh0);
                 wave_order();
                 if (has1) {
-                    if (lane < n1) item_post(b1 + lane, cb, p1);
+                    if (lane < n1) item_post(b1 + lane, cb, p1, sh1);
                     wave_order();
                     for (int qq = s0 + 2; qq < s1; ++qq) {  // levels of more than two rounds
                         const int bq = lrnd[qq];
