@@ -94,34 +94,15 @@ static void pfor_dyn(int n, long long work, long long grain, F f) {
     for (std::thread &x : th) x.join();
 }
 
-// rows grouped by level (stable: ascending row within a level): a counting
-// sort over contiguous row blocks, one level histogram per block
+// rows grouped by level (stable: ascending row within a level)
 static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int> &ptr,
                          std::vector<int> &rows) {
-    const long long n = (long long)lev.size();
-    const int nb = (int)std::max<long long>(1, std::min<long long>(host_threads(), n / (1 << 15)));
-    std::vector<std::vector<int>> hist((size_t)nb);
-    auto blk = [&](int t) { return std::make_pair(n * t / nb, n * (t + 1) / nb); };
-    pfor_dyn(nb, n, 1, [&](int t) {
-        std::vector<int> &h = hist[(size_t)t];
-        h.assign((size_t)nlev, 0);
-        for (long long i = blk(t).first; i < blk(t).second; i++) h[(size_t)lev[(size_t)i]]++;
-    });
     ptr.assign((size_t)nlev + 1, 0);
-    for (int l = 0; l < nlev; l++) {  // block t's first slot in level l
-        int at = ptr[(size_t)l];
-        for (int t = 0; t < nb; t++) {
-            const int c = hist[(size_t)t][(size_t)l];
-            hist[(size_t)t][(size_t)l] = at;
-            at += c;
-        }
-        ptr[(size_t)l + 1] = at;
-    }
-    rows.resize((size_t)n);
-    pfor_dyn(nb, n, 1, [&](int t) {
-        std::vector<int> &h = hist[(size_t)t];
-        for (long long i = blk(t).first; i < blk(t).second; i++) rows[(size_t)h[(size_t)lev[(size_t)i]]++] = (int)i;
-    });
+    for (int v : lev) ptr[(size_t)v + 1]++;
+    for (int l = 0; l < nlev; l++) ptr[(size_t)l + 1] += ptr[(size_t)l];
+    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+    rows.resize(lev.size());
+    for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
 }
 
 // fma-chain batch for a mean chain length of total / count
@@ -868,62 +849,55 @@ rsp_status_t plan_validate(int n, const int *rpp, const int *cip, IluHostPlan &h
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     const int n = hp.n;
     const std::vector<int> &dpos = hp.dpos;
+    // three independent sequential passes over the strict lower part, run
+    // concurrently (each is memory-latency bound; splitting one over threads
+    // measured slower on the box): the L levels, the transposed lower part,
+    // the L^T levels; each level set then grouped (counting sort).
     // levels of the lower DAG (factor + L solve): the longest path ending at
-    // each row — a sequential O(nnz) pass (each row needs its producers')
-    std::vector<int> lv((size_t)n, 0);
-    int nl = n > 0 ? 1 : 0;
-    for (int i = 0; i < n; i++) {
-        int l = 0;
-        for (int p = rp[i]; p < dpos[(size_t)i]; p++) l = std::max(l, lv[(size_t)ci[p]] + 1);
-        lv[(size_t)i] = l;
-        nl = std::max(nl, l + 1);
-    }
-    // transposed strict lower: row k lists (j, pos) for l_jk, j descending
-    // (counts and slots by relaxed atomics over row blocks, then each
-    // column's entries sorted to j descending)
-    std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
-    ltp.assign((size_t)n + 1, 0);
-    pfor(n, 1 << 14, [&](long long a, long long b) {
-        for (long long j = a; j < b; j++)
-            for (int p = rp[j]; p < dpos[(size_t)j]; p++) __atomic_fetch_add(&ltp[(size_t)ci[p] + 1], 1, __ATOMIC_RELAXED);
-    });
-    for (int k = 0; k < n; k++) ltp[(size_t)k + 1] += ltp[(size_t)k];
-    const size_t nlo = (size_t)ltp[(size_t)n];
-    std::vector<unsigned long long> key(nlo);  // (n - 1 - j) << 32 | position
-    {
-        std::vector<int> fill(ltp.begin(), ltp.end() - 1);
-        pfor(n, 1 << 14, [&](long long a, long long b) {
-            for (long long j = a; j < b; j++)
-                for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
-                    const int slot = __atomic_fetch_add(&fill[(size_t)ci[p]], 1, __ATOMIC_RELAXED);
-                    key[(size_t)slot] = (unsigned long long)(n - 1 - j) << 32 | (unsigned)p;
-                }
-        });
-    }
-    lts.resize(nlo);
-    ltc.resize(nlo);
-    pfor(n, 1 << 14, [&](long long a, long long b) {
-        for (long long k = a; k < b; k++) {
-            const size_t q0 = (size_t)ltp[(size_t)k], q1 = (size_t)ltp[(size_t)k + 1];
-            if (q1 - q0 > 1) std::sort(key.begin() + (long)q0, key.begin() + (long)q1);
-            for (size_t q = q0; q < q1; q++) {
-                lts[q] = (int)(key[q] & 0xffffffffu);
-                ltc[q] = n - 1 - (int)(key[q] >> 32);
-            }
+    // each row (each row needs its producers')
+    std::thread tl([&] {
+        std::vector<int> lv((size_t)n, 0);
+        int nl = n > 0 ? 1 : 0;
+        for (int i = 0; i < n; i++) {
+            int l = 0;
+            for (int p = rp[i]; p < dpos[(size_t)i]; p++) l = std::max(l, lv[(size_t)ci[p]] + 1);
+            lv[(size_t)i] = l;
+            nl = std::max(nl, l + 1);
         }
+        group_levels(lv, nl, hp.L.ptr, hp.L.rows);
     });
     // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
-    std::vector<int> lvt((size_t)n, 0);
-    int nlt = n > 0 ? 1 : 0;
-    for (int j = n - 1; j >= 0; j--) {
-        nlt = std::max(nlt, lvt[(size_t)j] + 1);
-        for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
-            const int k = ci[p];
-            lvt[(size_t)k] = std::max(lvt[(size_t)k], lvt[(size_t)j] + 1);
+    std::thread tt([&] {
+        std::vector<int> lvt((size_t)n, 0);
+        int nlt = n > 0 ? 1 : 0;
+        for (int j = n - 1; j >= 0; j--) {
+            nlt = std::max(nlt, lvt[(size_t)j] + 1);
+            for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
+                const int k = ci[p];
+                lvt[(size_t)k] = std::max(lvt[(size_t)k], lvt[(size_t)j] + 1);
+            }
         }
+        group_levels(lvt, nlt, hp.LT.ptr, hp.LT.rows);
+    });
+    // transposed strict lower: row k lists (j, pos) for l_jk, j descending
+    std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
+    ltp.assign((size_t)n + 1, 0);
+    for (int j = 0; j < n; j++)
+        for (int p = rp[j]; p < dpos[(size_t)j]; p++) ltp[(size_t)ci[p] + 1]++;
+    for (int k = 0; k < n; k++) ltp[(size_t)k + 1] += ltp[(size_t)k];
+    lts.resize((size_t)ltp[(size_t)n]);
+    ltc.resize((size_t)ltp[(size_t)n]);
+    {
+        std::vector<int> fill(ltp.begin(), ltp.end() - 1);
+        for (int j = n - 1; j >= 0; j--)
+            for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
+                const int slot = fill[(size_t)ci[p]]++;
+                lts[(size_t)slot] = p;
+                ltc[(size_t)slot] = j;
+            }
     }
-    group_levels(lv, nl, hp.L.ptr, hp.L.rows);
-    group_levels(lvt, nlt, hp.LT.ptr, hp.LT.rows);
+    tl.join();
+    tt.join();
 }
 
 rsp_status_t plan_symbolic(const int *rpp, const int *cip, IluHostPlan &hp) {
