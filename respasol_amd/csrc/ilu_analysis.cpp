@@ -362,6 +362,52 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     if (sp.chunks.empty()) sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
 }
 
+// Which levels of the L DAG the factor runs thin. A level runs thin up to
+// kRndFlowItems positions; up to kRndLevelItems when it could not run in a
+// flow launch anyway (a row past the slot layout's kFacRow entries /
+// kFacPairs pairs: circuit hubs); and never with a position of more than
+// kRndItemPairs update pairs. Wider levels are fat: in a flow run they
+// spread over all CUs, where a thin run stages every position through one
+// (A/B knobs RSP_ILU_THIN_FACTOR_ITEMS / RSP_ILU_THIN_FACTOR_FLOW).
+static std::vector<char> factor_thin_levels(const int *rp, const std::vector<int> &upd_ptr,
+                                            const std::vector<int> &ptr, const std::vector<int> &rows,
+                                            int thin_rows, std::vector<long long> *items_out) {
+    const int nlev = (int)ptr.size() - 1;
+    const int thin_items = env_int("RSP_ILU_THIN_FACTOR_ITEMS", rsp::kRndLevelItems);
+    const int thin_flow = env_int("RSP_ILU_THIN_FACTOR_FLOW", rsp::kRndFlowItems);
+    std::vector<long long> litems((size_t)std::max(nlev, 1), 0);
+    std::vector<char> thin((size_t)std::max(nlev, 1), 0);
+    pfor_dyn(nlev, (long long)rows.size(), 1 << 14, [&](int l) {
+        long long items = 0;
+        int maxp = 0;
+        bool hub = false;
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
+            const int i = rows[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
+            items += re - rs;
+            for (int p = rs; p < re; p++) maxp = std::max(maxp, upd_ptr[(size_t)p + 1] - upd_ptr[(size_t)p]);
+            hub |= re - rs > rsp::kFacRow || upd_ptr[(size_t)re] - upd_ptr[(size_t)rs] > rsp::kFacPairs;
+        }
+        litems[(size_t)l] = items;
+        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
+        const long long lim = hub ? thin_items : std::min(thin_items, thin_flow);
+        thin[(size_t)l] = (cnt <= thin_rows && items <= lim && maxp <= rsp::kRndItemPairs) ? 1 : 0;
+    });
+    if (items_out) items_out->swap(litems);
+    return thin;
+}
+
+static int thin_factor_rows() { return env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows); }
+
+std::vector<int> factor_thin_rows(const int *rp, const IluHostPlan &hp) {
+    const std::vector<char> thin = factor_thin_levels(rp, hp.sym.upd_ptr, hp.L.ptr, hp.L.rows, thin_factor_rows(),
+                                                      nullptr);
+    std::vector<int> out;
+    for (size_t l = 0; l + 1 < hp.L.ptr.size(); l++)
+        if (thin[l])
+            for (int x = hp.L.ptr[l]; x < hp.L.ptr[l + 1]; x++) out.push_back(hp.L.rows[(size_t)x]);
+    return out;
+}
+
 // Factor plan of the L DAG (see IluArgs): segments (fat levels: one launch
 // each; thin levels: one single-workgroup launch per run) and, for the thin
 // runs, ROUNDS: a level's positions ("items") grouped so that a round's items
@@ -396,40 +442,17 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
                               const std::vector<int> &rows, int thin_rows, FacPlan &fp) {
     const int nlev = (int)ptr.size() - 1;
     const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
-    // a level runs thin up to kRndFlowItems positions; up to kRndLevelItems
-    // when it could not run in a flow launch anyway (a row past the slot
-    // layout's kFacRow entries / kFacPairs pairs: circuit hubs). Wider levels
-    // are fat: in a flow run they spread over all CUs, where a thin run
-    // stages every position through one (A/B knobs RSP_ILU_THIN_FACTOR_ITEMS /
-    // RSP_ILU_THIN_FACTOR_FLOW)
-    const int thin_items = env_int("RSP_ILU_THIN_FACTOR_ITEMS", rsp::kRndLevelItems);
-    const int thin_flow = env_int("RSP_ILU_THIN_FACTOR_FLOW", rsp::kRndFlowItems);
     const long long piece_items = std::max(1, env_int("RSP_ILU_PIECE_ITEMS", kRndPieceItems));
     const int nnz = rp[(size_t)n];
-    // per level: positions and the largest update list
-    std::vector<long long> litems((size_t)std::max(nlev, 1), 0);
-    std::vector<int> lmaxp((size_t)std::max(nlev, 1), 0);
-    std::vector<char> lhub((size_t)std::max(nlev, 1), 0);
-    pfor_dyn(nlev, nnz, 1 << 15, [&](int l) {
-        long long items = 0;
-        int maxp = 0;
-        bool hub = false;
-        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-            const int i = rows[(size_t)x], rs = rp[(size_t)i], re = rp[(size_t)i + 1];
-            items += re - rs;
-            for (int p = rs; p < re; p++)
-                maxp = std::max(maxp, sym.upd_ptr[(size_t)p + 1] - sym.upd_ptr[(size_t)p]);
-            hub |= re - rs > rsp::kFacRow || sym.upd_ptr[(size_t)re] - sym.upd_ptr[(size_t)rs] > rsp::kFacPairs;
-        }
-        litems[(size_t)l] = items;
-        lmaxp[(size_t)l] = maxp;
-        lhub[(size_t)l] = hub;
-    });
+    std::vector<long long> litems;
+    const std::vector<char> lthin = factor_thin_levels(rp, sym.upd_ptr, ptr, rows, thin_rows, &litems);
+    // pairs of position p of thin row i (packed, see IluSymbolic::pair_base)
+    auto pair_off = [&](int i) {
+        return sym.pair_base.empty() ? 0 : sym.pair_base[(size_t)i] - sym.upd_ptr[(size_t)rp[(size_t)i]];
+    };
     fp.segs.clear();
     for (int l = 0; l < nlev; l++) {
-        const int cnt = ptr[(size_t)l + 1] - ptr[(size_t)l];
-        const long long lim = lhub[(size_t)l] ? thin_items : std::min(thin_items, thin_flow);
-        const int thin = (cnt <= thin_rows && litems[(size_t)l] <= lim && lmaxp[(size_t)l] <= rsp::kRndItemPairs) ? 1 : 0;
+        const int thin = lthin[(size_t)l];
         if (!fp.segs.empty() && fp.segs.back().thin == thin && fp.segs.back().le == l)
             fp.segs.back().le = l + 1;
         else
@@ -545,8 +568,9 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
                 for (int attempt = 0; attempt < 2; attempt++) {
                     fresh.clear();
                     ipairs.clear();
+                    const int po = pair_off(i);
                     for (int u = sym.upd_ptr[(size_t)p]; u < sym.upd_ptr[(size_t)p + 1]; u++) {
-                        const int lc = ref(sym.upd_l[(size_t)u], fresh), uc = ref(sym.upd_u[(size_t)u], fresh);
+                        const int lc = ref(sym.upd_l[(size_t)(u + po)], fresh), uc = ref(sym.upd_u[(size_t)(u + po)], fresh);
                         ipairs.push_back(lc | uc << 16);
                     }
                     int d = -1;
@@ -964,9 +988,9 @@ void plan_solves(const int *rp, const int *ci, IluHostPlan &hp) {
 void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &hp) {
     const int n = hp.n, nnz_s = hp.nnz_s;
     const std::vector<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
-    const int thin_factor = env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows);
+    const int thin_factor = thin_factor_rows();
     IluSymbolic &sym = hp.sym;
-    hp.fac_batch = chain_batch((long long)sym.upd_l.size(), nnz_s);
+    hp.fac_batch = chain_batch((long long)sym.upd_ptr[(size_t)nnz_s], nnz_s);
     timed_plan(n, "factor", [&] {
         build_factor_plan(n, rp, ci, dpos, hasdiag, sym, hp.L.ptr, hp.L.rows, thin_factor, hp.fplan);
     });
@@ -1110,10 +1134,34 @@ rsp_status_t plan_host(int n, const int *rp, const int *ci, long long slot_cap, 
     lord.swap(hp.sym.lord);
     lend.swap(hp.sym.lend);
     udiv.swap(hp.udiv);
+    // ... and, like it, only the thin rows' update pairs, packed (the full
+    // lists are kept for the digest)
+    std::vector<int> upd_l, upd_u;
+    if (env_int("RSP_ILU_PACK_PAIRS", 1)) {
+        const std::vector<int> trows = factor_thin_rows(rp, hp);
+        std::vector<int> pl, pu;
+        hp.sym.pair_base.assign((size_t)std::max(n, 1), 0);
+        for (int i : trows) {
+            hp.sym.pair_base[(size_t)i] = (int)pl.size();
+            for (int q = hp.sym.upd_ptr[(size_t)rp[i]]; q < hp.sym.upd_ptr[(size_t)rp[i + 1]]; q++) {
+                pl.push_back(hp.sym.upd_l[(size_t)q]);
+                pu.push_back(hp.sym.upd_u[(size_t)q]);
+            }
+        }
+        upd_l.swap(hp.sym.upd_l);
+        upd_u.swap(hp.sym.upd_u);
+        hp.sym.upd_l.swap(pl);
+        hp.sym.upd_u.swap(pu);
+    }
     plan_rest(rp, ci, slot_cap, want_u, hp);
     lord.swap(hp.sym.lord);
     lend.swap(hp.sym.lend);
     udiv.swap(hp.udiv);
+    if (!hp.sym.pair_base.empty()) {
+        hp.sym.pair_base.clear();
+        hp.sym.upd_l.swap(upd_l);
+        hp.sym.upd_u.swap(upd_u);
+    }
     ph.mark("plans");
     return RSP_STATUS_SUCCESS;
 }

@@ -42,6 +42,11 @@ struct SolvePlan {
 struct IluSymbolic {
     std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
     std::vector<int> stage;  // per lower position: its intra-row stage
+    // empty: upd_l / upd_u hold every pair (indexed as upd_ptr). Else only
+    // the pairs of the rows of the factor's thin levels, packed: row i's pair
+    // u at pair_base[i] + u - upd_ptr[rowptr[i]] (the device analysis
+    // downloads no more; the factor plan reads no other row's pairs).
+    std::vector<int> pair_base;
 };
 
 struct FacPlan {
@@ -104,6 +109,9 @@ constexpr int kPhases = 6;  // phase slots of Phases::ms (marks in call order)
 //                  (needs sym.upd_ptr / upd_l / upd_u / stage);
 //   plan_rest:     both (the solves on a second thread).
 rsp_status_t plan_validate(int n, const int *rp, const int *ci, IluHostPlan &hp);
+// The rows of the L DAG's levels the factor runs thin (needs the levels and
+// sym.upd_ptr): the only rows whose update pairs the factor plan reads.
+std::vector<int> factor_thin_rows(const int *rp, const IluHostPlan &hp);
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp);
 rsp_status_t plan_symbolic(const int *rp, const int *ci, IluHostPlan &hp);
 void plan_solves(const int *rp, const int *ci, IluHostPlan &hp);

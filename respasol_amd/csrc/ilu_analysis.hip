@@ -311,4 +311,27 @@ hipError_t ilu_an_stages(int n, int maxlen, const int *rp, const int *ci, const 
     return hipGetLastError();
 }
 
+// The update pairs of the listed rows, packed back to back (row r's pairs at
+// cbase[r]): the host factor plan reads only its thin rows' pairs.
+__global__ __launch_bounds__(256) void an_gather_pairs(const int *__restrict__ rows, int nrows,
+                                                       const int *__restrict__ rp, const int *__restrict__ ptr,
+                                                       const int *__restrict__ cbase, const int *__restrict__ upd_l,
+                                                       const int *__restrict__ upd_u, int *__restrict__ out_l,
+                                                       int *__restrict__ out_u) {
+    for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+        const int i = rows[r], q0 = ptr[rp[i]], q1 = ptr[rp[i + 1]], o = cbase[r] - q0;
+        for (int q = q0 + (int)threadIdx.x; q < q1; q += 256) {
+            out_l[o + q] = upd_l[q];
+            out_u[o + q] = upd_u[q];
+        }
+    }
+}
+
+hipError_t ilu_an_gather_pairs(const int *rows, int nrows, const int *rp, const int *ptr, const int *cbase,
+                               const int *upd_l, const int *upd_u, int *out_l, int *out_u, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    an_gather_pairs<<<std::min(nrows, 65536), 256, 0, s>>>(rows, nrows, rp, ptr, cbase, upd_l, upd_u, out_l, out_u);
+    return hipGetLastError();
+}
+
 }  // namespace rsp_k

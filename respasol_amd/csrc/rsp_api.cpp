@@ -1191,13 +1191,50 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     rsp_an::plan_levels(rp.data(), ci.data(), hp);
     ph.mark("levels");
     after_levels();  // the solve plans need nothing more: started here
-    hp.sym.upd_l.resize((size_t)total);
-    hp.sym.upd_u.resize((size_t)total);
-    hp.sym.stage.resize((size_t)nnz_s);
-    if (total > 0) {
-        RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_l.data(), f->d_upd_l, (size_t)total * 4, hipMemcpyDeviceToHost, s));
-        RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_u.data(), f->d_upd_u, (size_t)total * 4, hipMemcpyDeviceToHost, s));
+    // the host factor plan reads the update pairs of its thin rows only: those
+    // are packed on the device and downloaded (FEM matrices have tens of
+    // millions of pairs, nearly all in fat levels). Not with host-built hub
+    // rows (their lists are uploaded from full host arrays) or for the tests'
+    // plan digest (which covers the full arrays).
+    const bool pack = long_rows.empty() && !env_int("RSP_ILU_DIGEST", 0) && env_int("RSP_ILU_PACK_PAIRS", 1);
+    if (pack) {
+        const std::vector<int> trows = rsp_an::factor_thin_rows(rp.data(), hp);
+        std::vector<int> cbase(trows.size() + 1, 0);
+        for (size_t r = 0; r < trows.size(); r++) {
+            const int i = trows[r];
+            cbase[r + 1] = cbase[r] + hp.sym.upd_ptr[(size_t)rp[(size_t)i + 1]] - hp.sym.upd_ptr[(size_t)rp[(size_t)i]];
+        }
+        const int packed = cbase.back();
+        hp.sym.pair_base.assign((size_t)std::max(n, 1), 0);
+        for (size_t r = 0; r < trows.size(); r++) hp.sym.pair_base[(size_t)trows[r]] = cbase[r];
+        hp.sym.upd_l.resize((size_t)packed);
+        hp.sym.upd_u.resize((size_t)packed);
+        if (packed > 0) {
+            Arena ag;
+            int *d_trows = nullptr, *d_cbase = nullptr, *d_pl = nullptr, *d_pu = nullptr;
+            void *d_gather = nullptr;
+            ag.up(&d_trows, trows);
+            ag.up(&d_cbase, cbase);
+            ag.space((void **)&d_pl, (size_t)packed * 4);
+            ag.space((void **)&d_pu, (size_t)packed * 4);
+            RSP_CHECK_HIP(ag.commit(&d_gather, s));
+            hipError_t e = rsp_k::ilu_an_gather_pairs(d_trows, (int)trows.size(), d_rp, f->d_upd_ptr, d_cbase,
+                                                      f->d_upd_l, f->d_upd_u, d_pl, d_pu, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hp.sym.upd_l.data(), d_pl, (size_t)packed * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hp.sym.upd_u.data(), d_pu, (size_t)packed * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            (void)hipFree(d_gather);
+            RSP_CHECK_HIP(e);
+        }
+    } else {
+        hp.sym.upd_l.resize((size_t)total);
+        hp.sym.upd_u.resize((size_t)total);
+        if (total > 0) {
+            RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_l.data(), f->d_upd_l, (size_t)total * 4, hipMemcpyDeviceToHost, s));
+            RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_u.data(), f->d_upd_u, (size_t)total * 4, hipMemcpyDeviceToHost, s));
+        }
     }
+    hp.sym.stage.resize((size_t)nnz_s);
     if (nnz_s > 0)
         RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.stage.data(), d_stage, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
@@ -1273,7 +1310,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     // the U DAG (--true-lu extension) is planned on its first use
     ph.mark("plans");
     f->structural_zero = hp->structural_zero;
-    f->n_updates = (long long)hp->sym.upd_l.size();
+    f->n_updates = nnz_s > 0 ? (long long)hp->sym.upd_ptr[(size_t)nnz_s] : 0;
     f->fac_batch = hp->fac_batch;
     f->fac_segs = hp->fplan.segs;
     f->fslev = hp->fslev;

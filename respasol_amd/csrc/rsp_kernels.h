@@ -384,6 +384,8 @@ hipError_t ilu_an_rows(int n, const int *rp, const int *ci, int *dpos, int *hasd
 hipError_t ilu_an_count(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
                         const int *dpos, const int *hasdiag, int *cnt, int *gcur, hipStream_t s);
 hipError_t ilu_an_scan(const int *cnt, int *ptr, int count, void *temp, size_t *temp_bytes, hipStream_t s);
+hipError_t ilu_an_gather_pairs(const int *rows, int nrows, const int *rp, const int *ptr, const int *cbase,
+                               const int *upd_l, const int *upd_u, int *out_l, int *out_u, hipStream_t s);
 hipError_t ilu_an_fill(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
                        const int *dpos, const int *hasdiag, const int *ptr, int *gcur, int *upd_l, int *upd_u,
                        hipStream_t s);
