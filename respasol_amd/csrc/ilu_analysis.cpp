@@ -11,7 +11,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 
@@ -43,6 +46,82 @@ static int host_threads() {
     return std::max(1, std::min(t, 64));
 }
 
+// Persistent worker threads for the parallel loops below. A loop used to
+// spawn and join its team each time (~0.2-0.5 ms per loop at 16 threads, and
+// an analysis runs ~35 loops: tens of ms on a small matrix). A loop is a job
+// of `nb` blocks claimed through an atomic counter; the calling thread works
+// on its own job too, so a job always finishes even when every worker is busy
+// (nested or concurrent loops: the plans of L, L^T and the factor run at the
+// same time). Block boundaries are the same as before, so are the plans.
+// Workers are created on first use (as many as host_threads() - 1 asks for,
+// growing if a later call asks for more), detached, and live as long as the
+// process.
+class Pool {
+    struct Job {
+        std::function<void(int)> body;
+        int nb = 0;
+        std::atomic<int> next{0}, done{0};
+        std::mutex m;
+        std::condition_variable cv;
+        void work() {
+            for (int b; (b = next.fetch_add(1, std::memory_order_relaxed)) < nb;) {
+                body(b);
+                if (done.fetch_add(1, std::memory_order_acq_rel) + 1 == nb) {
+                    std::lock_guard<std::mutex> g(m);
+                    cv.notify_all();
+                }
+            }
+        }
+    };
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Job>> q_;
+    int workers_ = 0;
+
+    void worker() {
+        for (;;) {
+            std::shared_ptr<Job> j;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return !q_.empty(); });
+                j = std::move(q_.front());
+                q_.pop_front();
+            }
+            j->work();
+        }
+    }
+
+  public:
+    static Pool &get() {
+        static Pool *p = new Pool();  // never destroyed: its threads outlive static destructors
+        return *p;
+    }
+    // body(b) for b in [0, nb) on up to `team` threads (the caller included)
+    void run(int nb, int team, const std::function<void(int)> &body) {
+        if (nb <= 0) return;
+        team = std::max(1, std::min(team, nb));
+        if (team == 1) {
+            for (int b = 0; b < nb; b++) body(b);
+            return;
+        }
+        auto j = std::make_shared<Job>();
+        j->body = body;
+        j->nb = nb;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            for (; workers_ < team - 1; workers_++) std::thread([this] { worker(); }).detach();
+            for (int t = 1; t < team; t++) q_.push_back(j);
+        }
+        if (team == 2)
+            cv_.notify_one();
+        else
+            cv_.notify_all();
+        j->work();
+        std::unique_lock<std::mutex> g(j->m);
+        j->cv.wait(g, [&] { return j->done.load(std::memory_order_acquire) == nb; });
+    }
+};
+
 // f(r0, r1) over contiguous row blocks of [0, n) on host_threads() threads.
 template <typename F>
 static void parallel_rows(int n, F f) {
@@ -51,14 +130,11 @@ static void parallel_rows(int n, F f) {
         f(0, n);
         return;
     }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; t++)
-        th.emplace_back(f, (int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt));
-    for (std::thread &x : th) x.join();
+    Pool::get().run(nt, nt, [&](int t) { f((int)((long long)n * t / nt), (int)((long long)n * (t + 1) / nt)); });
 }
 
 // f(lo, hi) over [0, n) in at most host_threads() contiguous blocks of at
-// least `grain` (the calling thread takes the first block).
+// least `grain`.
 template <typename F>
 static void pfor(long long n, long long grain, F f) {
     const int nt = (int)std::max<long long>(1, std::min<long long>(host_threads(), n / std::max(grain, 1LL)));
@@ -66,11 +142,7 @@ static void pfor(long long n, long long grain, F f) {
         if (n > 0) f(0LL, n);
         return;
     }
-    std::vector<std::thread> th;
-    th.reserve((size_t)nt - 1);
-    for (int t = 1; t < nt; t++) th.emplace_back(f, n * t / nt, n * (t + 1) / nt);
-    f(0LL, n / nt);
-    for (std::thread &x : th) x.join();
+    Pool::get().run(nt, nt, [&](int t) { f(n * t / nt, n * (t + 1) / nt); });
 }
 
 // f(j) for j in [0, n), items handed out dynamically (uneven item costs:
@@ -83,15 +155,7 @@ static void pfor_dyn(int n, long long work, long long grain, F f) {
         for (int j = 0; j < n; j++) f(j);
         return;
     }
-    std::atomic<int> next(0);
-    auto body = [&]() {
-        for (int j; (j = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(j);
-    };
-    std::vector<std::thread> th;
-    th.reserve((size_t)nt - 1);
-    for (int t = 1; t < nt; t++) th.emplace_back(body);
-    body();
-    for (std::thread &x : th) x.join();
+    Pool::get().run(n, nt, [&](int j) { f(j); });
 }
 
 // rows grouped by level (stable: ascending row within a level)
@@ -123,14 +187,20 @@ static int chain_batch(long long total, long long count) {
 // the chunk start — the producer is then in an earlier chunk or before the
 // run, so its store is visible after the chunk's full barrier).
 
-// row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
-// Built in parallel phases (rows, levels and chunks as work items, prefix
-// sums over level order in between); row_count(i) = the number of terms
-// row_terms(i) emits.
-template <typename RowCount, typename RowTerms>
-static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
-                             int thin_rows, int group, const std::vector<int> &diag,
-                             RowCount row_count, RowTerms row_terms, SolvePlan &sp) {
+// Built in two parts, each in parallel phases (rows, levels and chunks as
+// work items, prefix sums over level order in between):
+//   solve_plan_rows  (host): segments, row classes and order, tasks, flow
+//                    items, the thin runs' chunks (levels, slots, terms) —
+//                    per-row and per-level decisions; row_count(i) = the
+//                    number of terms of row i;
+//   solve_plan_terms (host; the device analysis runs ilu_an_solve_terms
+//                    instead, the same arrays bit for bit): per flat term
+//                    its position and y source, the window remap, the thin
+//                    runs' row records, y indices and staged terms.
+template <typename RowCount>
+static void solve_plan_rows(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
+                            int thin_rows, int group, const std::vector<int> &diag,
+                            RowCount row_count, SolvePlan &sp) {
     const int nlev = (int)ptr.size() - 1;
     const long long nx = (long long)rows.size();
     constexpr long long kGrain = 1 << 14;
@@ -205,20 +275,13 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     }
     for (int l = 0; l < nlev; l++)
         if (pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0) sp.sbase[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l]].t0;
-    sp.tpos.assign((size_t)total, -1);
-    std::vector<int> col((size_t)total, -1);
+    sp.nterm = total;
     pfor(nx, kGrain, [&](long long a, long long b) {
         for (long long x = a; x < b; x++) {
             rsp::RowTask &t = sp.tasks[(size_t)x];
-            const int i = order[(size_t)x];
-            t.i = i;
+            t.i = order[(size_t)x];
             t.t1 += t.t0;
-            t.d = diag.empty() ? -1 : diag[(size_t)i];
-            int k = t.t0;
-            row_terms(i, [&](int tp, int c) {
-                sp.tpos[(size_t)k] = tp;
-                col[(size_t)k++] = c;
-            });
+            t.d = diag.empty() ? -1 : diag[(size_t)t.i];
         }
     });
     // flow segments: fat segments of two or more levels run as one persistent
@@ -260,20 +323,12 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     for (int l = 0; l < nlev; l++)
         if (ptr[(size_t)l + 1] > ptr[(size_t)l])
             lterms[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l + 1] - 1].t1 - sp.tasks[(size_t)ptr[(size_t)l]].t0;
-    sp.src.resize((size_t)total);
-    pfor(total, kGrain, [&](long long a, long long b) {
-        for (long long k = a; k < b; k++) sp.src[(size_t)k] = col[(size_t)k] < 0 ? rsp::kPadSrc : col[(size_t)k];
-    });
     for (rsp::LevelSeg &sg : sp.segs)
         if (sg.thin) sg.nth = rsp::kThinThreads;
-    std::vector<int> slot_of((size_t)n, -1);
-    pfor(nx, kGrain, [&](long long a, long long b) {
-        for (long long x = a; x < b; x++) slot_of[(size_t)order[(size_t)x]] = (int)x;
-    });
-    // chunks of the thin runs (greedy over levels), then the y sources of
-    // their terms (per level)
+    // chunks of the thin runs (greedy over levels): levels, slots, terms, and
+    // each chunk's run base (the run's first slot)
     sp.chunks.clear();
-    std::vector<int> thin_base((size_t)std::max(nlev, 1), -1);  // per thin level: its run's first slot
+    sp.cbase.clear();
     for (rsp::LevelSeg &sg : sp.segs) {
         if (!sg.thin) continue;
         sg.c0 = (int)sp.chunks.size();
@@ -283,6 +338,7 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
             if (sp.chunks.size() == (size_t)sg.c0 || crow + cnt > rsp::kChunkRows ||
                 cterm + lterms[(size_t)l] > rsp::kChunkTerms) {
                 sp.chunks.push_back({l, l + 1, 0, 0, 0, 0, 0, 0});
+                sp.cbase.push_back(ptr[(size_t)sg.lb]);
                 crow = 0;
                 cterm = 0;
             } else {
@@ -290,10 +346,53 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
             }
             crow += cnt;
             cterm += lterms[(size_t)l];
-            thin_base[(size_t)l] = ptr[(size_t)sg.lb];
         }
         sg.c1 = (int)sp.chunks.size();
     }
+    for (rsp::LevelChunk &ch : sp.chunks) {
+        ch.x0 = ptr[(size_t)ch.l0];
+        ch.x1 = ptr[(size_t)ch.l1];
+        ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
+        ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
+    }
+    if (sp.chunks.empty()) {
+        sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
+        sp.cbase.push_back(0);
+    }
+}
+
+// row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
+// (row_count(i) of them, as given to solve_plan_rows).
+template <typename RowTerms>
+static void solve_plan_terms(int n, const std::vector<int> &ptr, int group, RowTerms row_terms, SolvePlan &sp) {
+    constexpr long long kGrain = 1 << 14;
+    const int nlev = (int)ptr.size() - 1;
+    const long long nx = (long long)ptr[(size_t)nlev], total = sp.nterm;
+    sp.tpos.assign((size_t)total, -1);
+    std::vector<int> col((size_t)total, -1);
+    pfor(nx, kGrain, [&](long long a, long long b) {
+        for (long long x = a; x < b; x++) {
+            int k = sp.tasks[(size_t)x].t0;
+            row_terms(sp.tasks[(size_t)x].i, [&](int tp, int c) {
+                sp.tpos[(size_t)k] = tp;
+                col[(size_t)k++] = c;
+            });
+        }
+    });
+    sp.src.resize((size_t)total);
+    pfor(total, kGrain, [&](long long a, long long b) {
+        for (long long k = a; k < b; k++) sp.src[(size_t)k] = col[(size_t)k] < 0 ? rsp::kPadSrc : col[(size_t)k];
+    });
+    std::vector<int> slot_of((size_t)n, -1);
+    pfor(nx, kGrain, [&](long long a, long long b) {
+        for (long long x = a; x < b; x++) slot_of[(size_t)sp.tasks[(size_t)x].i] = (int)x;
+    });
+    std::vector<int> thin_base((size_t)std::max(nlev, 1), -1);  // per thin level: its run's first slot
+    for (const rsp::LevelSeg &sg : sp.segs)
+        if (sg.thin)
+            for (int l = sg.lb; l < sg.le; l++) thin_base[(size_t)l] = ptr[(size_t)sg.lb];
+    // y sources of the thin runs' terms: the LDS window slot when the
+    // producer is earlier in the run and still in the window
     pfor_dyn(nlev, nx, kGrain, [&](int l) {
         const int base = thin_base[(size_t)l];
         if (base < 0) return;
@@ -311,22 +410,14 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
         sp.tpos.push_back(0);
         sp.src.push_back(0);
     }
-    // per chunk: ranges, static row records, term y indices, staged terms
-    // (counted per chunk, then filled at their prefix offsets)
-    sp.trow.assign(std::max<size_t>(rows.size(), 1), rsp::ThinRowPlan{0, 0, 0, -1});
+    // per chunk: static row records, term y indices, staged terms (counted
+    // per chunk, then filled at their prefix offsets)
+    sp.trow.assign(std::max<size_t>((size_t)nx, 1), rsp::ThinRowPlan{0, 0, 0, -1});
     sp.sid.assign(sp.tpos.size(), rsp::kYWin);
     const int nch = (int)sp.chunks.size();
-    std::vector<int> chunk_base((size_t)std::max(nch, 1), 0);
-    for (const rsp::LevelSeg &sg : sp.segs)
-        if (sg.thin)
-            for (int c = sg.c0; c < sg.c1; c++) chunk_base[(size_t)c] = ptr[(size_t)sg.lb];
     std::vector<int> nst((size_t)std::max(nch, 1), 0);
     pfor_dyn(nch, nx, kGrain, [&](int c) {
-        rsp::LevelChunk &ch = sp.chunks[(size_t)c];
-        ch.x0 = ptr[(size_t)ch.l0];
-        ch.x1 = ptr[(size_t)ch.l1];
-        ch.k0 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x0].t0 : 0;
-        ch.k1 = ch.x1 > ch.x0 ? sp.tasks[(size_t)ch.x1 - 1].t1 : 0;
+        const rsp::LevelChunk &ch = sp.chunks[(size_t)c];
         int m = 0;
         for (int x = ch.x0; x < ch.x1; x++)
             for (int k = sp.tasks[(size_t)x].t0; k < sp.tasks[(size_t)x].t1; k++) m += sp.src[(size_t)k] >= 0;
@@ -341,7 +432,7 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
     sp.stg.assign((size_t)nstg, rsp::StagedTerm{0, 0});
     pfor_dyn(nch, nx, kGrain, [&](int c) {
         const rsp::LevelChunk &ch = sp.chunks[(size_t)c];
-        const int base = chunk_base[(size_t)c];
+        const int base = sp.cbase[(size_t)c];
         int st = ch.st0;
         for (int x = ch.x0; x < ch.x1; x++) {
             const rsp::RowTask &t = sp.tasks[(size_t)x];
@@ -359,7 +450,15 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
         }
     });
     if (sp.stg.empty()) sp.stg.push_back({0, 0});
-    if (sp.chunks.empty()) sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
+}
+
+// Both parts on the host.
+template <typename RowCount, typename RowTerms>
+static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
+                             int thin_rows, int group, const std::vector<int> &diag,
+                             RowCount row_count, RowTerms row_terms, SolvePlan &sp) {
+    solve_plan_rows(n, ptr, rows, thin_rows, group, diag, row_count, sp);
+    solve_plan_terms(n, ptr, group, row_terms, sp);
 }
 
 // Which levels of the L DAG the factor runs thin. A level runs thin up to

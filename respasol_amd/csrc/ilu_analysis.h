@@ -36,6 +36,8 @@ struct SolvePlan {
     std::vector<int> sid;
     std::vector<rsp::StagedTerm> stg;
     std::vector<rsp::FlowItem> fitems;  // flow segments' work items (LevelSeg c0 / c1 of a fat segment)
+    std::vector<int> cbase;  // per chunk: its thin run's first slot (not in the digest: derived)
+    int nterm = 0;           // flat terms (tpos.size() once the terms are built; >= 1 then)
 };
 
 // Symbolic ILU(0) data (built by ilu_symbolic below).
