@@ -1051,7 +1051,10 @@ static int thin_solve_rows() {
     return std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
 }
 
-void plan_solves(const int *rp, const int *ci, IluHostPlan &hp) {
+// The L and L^T solve plans; terms_on_host = false builds only the per-row
+// half (the device analysis builds the per-term half on the MI355X:
+// rsp_k::ilu_an_solve_terms).
+static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool terms_on_host) {
     const int n = hp.n;
     const std::vector<int> &dpos = hp.dpos;
     const std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
@@ -1061,28 +1064,32 @@ void plan_solves(const int *rp, const int *ci, IluHostPlan &hp) {
     hp.L.batch = hp.LT.batch = chain_batch(nlo, n);
     for (DagHost *d : {&hp.L, &hp.LT})  // thin-run term groups
         d->group = env_int("RSP_ILU_GROUP", d->batch == 2 ? 2 : 4) == 2 ? 2 : 4;
+    auto cnt_l = [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; };
+    auto cnt_lt = [&](int i) { return ltp[(size_t)i + 1] - ltp[(size_t)i]; };
     // the two DAGs' plans (flat terms in level order, thin-run chunks, y
     // sources) are independent: built concurrently
     std::thread tl([&] {
         timed_plan(n, "L", [&] {
-            build_solve_plan(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, std::vector<int>(),
-                             [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; },
-                             [&](int i, auto emit) {
-                                 for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
-                             }, hp.L.sp);
+            solve_plan_rows(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, std::vector<int>(), cnt_l, hp.L.sp);
+            if (terms_on_host)
+                solve_plan_terms(n, hp.L.ptr, hp.L.group, [&](int i, auto emit) {
+                    for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
+                }, hp.L.sp);
         });
     });
     timed_plan(n, "LT", [&] {
-        build_solve_plan(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, std::vector<int>(),
-                         [&](int i) { return ltp[(size_t)i + 1] - ltp[(size_t)i]; },
-                         [&](int i, auto emit) {
-                             for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++)
-                                 emit(lts[(size_t)q], ltc[(size_t)q]);
-                         }, hp.LT.sp);
+        solve_plan_rows(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, std::vector<int>(), cnt_lt, hp.LT.sp);
+        if (terms_on_host)
+            solve_plan_terms(n, hp.LT.ptr, hp.LT.group, [&](int i, auto emit) {
+                for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++) emit(lts[(size_t)q], ltc[(size_t)q]);
+            }, hp.LT.sp);
     });
     tl.join();
     hp.L.planned = hp.LT.planned = true;
 }
+
+void plan_solves(const int *rp, const int *ci, IluHostPlan &hp) { plan_solves_impl(rp, ci, hp, true); }
+void plan_solves_rows(const int *rp, const int *ci, IluHostPlan &hp) { plan_solves_impl(rp, ci, hp, false); }
 
 void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &hp) {
     const int n = hp.n, nnz_s = hp.nnz_s;

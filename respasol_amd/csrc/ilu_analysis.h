@@ -117,6 +117,9 @@ std::vector<int> factor_thin_rows(const int *rp, const IluHostPlan &hp);
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp);
 rsp_status_t plan_symbolic(const int *rp, const int *ci, IluHostPlan &hp);
 void plan_solves(const int *rp, const int *ci, IluHostPlan &hp);
+// ... their per-row half only (SolvePlan without tpos / src / trow / sid /
+// stg and the chunks' staged ranges: rsp_k::ilu_an_solve_terms builds those)
+void plan_solves_rows(const int *rp, const int *ci, IluHostPlan &hp);
 void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &hp);
 void plan_rest(const int *rp, const int *ci, long long slot_cap, bool want_u, IluHostPlan &hp);
 // The symbolic factor of the given rows on the host (the device analysis'

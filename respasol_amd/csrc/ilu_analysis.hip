@@ -334,4 +334,144 @@ hipError_t ilu_an_gather_pairs(const int *rows, int nrows, const int *rp, const 
     return hipGetLastError();
 }
 
+// ------------------------------------------------ solve plans: per-term half
+// (ilu_analysis.cpp solve_plan_terms restated; see SolveTermsArgs)
+namespace {
+
+// one wave per level-order slot x: its flat terms [t0, next t0) — the row's
+// terms in order, then pads (position -1, source the zero slot) — y index
+// "zero slot" (thin runs overwrite theirs), slot_of, default row record
+__global__ __launch_bounds__(256) void st_rows(rsp_k::SolveTermsArgs a) {
+    const int x = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (x >= a.nx) return;
+    const rsp::RowTask t = a.tasks[x];
+    const int i = t.i;
+    int j0, cnt;
+    if (a.kind == 0) {
+        j0 = a.rp[i];
+        cnt = a.dpos[i] - j0;
+    } else {
+        j0 = a.ltp[i];
+        cnt = a.ltp[i + 1] - j0;
+    }
+    const int tend = x + 1 < a.nx ? a.tasks[x + 1].t0 : a.total;
+    for (int o = lane; o < tend - t.t0; o += 64) {
+        const int k = t.t0 + o;
+        int tp = -1, c = rsp::kPadSrc;
+        if (o < cnt) {
+            const int j = j0 + o;
+            tp = a.kind == 0 ? j : a.lts[j];
+            c = a.kind == 0 ? a.ci[j] : a.ltc[j];
+        }
+        a.tpos[k] = tp;
+        a.src[k] = c;
+        a.sid[k] = rsp::kYWin;
+    }
+    if (lane == 0) {
+        a.slot_of[i] = x;
+        a.trow[x] = rsp::ThinRowPlan{0, 0, 0, -1};
+    }
+}
+
+__device__ __forceinline__ int block_sum(int v, int *lds) {
+    int tot;
+    block_excl_scan(v, lds, &tot);
+    return tot;
+}
+
+// one workgroup per chunk: the window remap of its terms (a producer earlier
+// in the run and at most kYWin slots before the end of the consumer's level
+// is read from the LDS window) and the count of its staged terms
+__global__ __launch_bounds__(256) void st_remap(rsp_k::SolveTermsArgs a) {
+    __shared__ int lds[256];
+    const int c = blockIdx.x;
+    const rsp::LevelChunk ch = a.chunks[c];
+    const int base = a.cbase[c];
+    int m = 0;
+    for (int k = ch.k0 + (int)threadIdx.x; k < ch.k1; k += 256) {
+        int sc = a.src[k];
+        if (sc >= 0) {
+            int lo = ch.x0, hi = ch.x1;  // the slot whose terms hold k (thin rows: t0 strictly increasing)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (a.tasks[mid].t0 <= k)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            int l0 = ch.l0, l1 = ch.l1;  // ... and its level
+            while (l1 - l0 > 1) {
+                const int mid = (l0 + l1) >> 1;
+                if (a.ptr[mid] <= lo)
+                    l0 = mid;
+                else
+                    l1 = mid;
+            }
+            const int sj = a.slot_of[sc];
+            if (sj >= base && sj < a.ptr[l0]) {
+                const int rj = sj - base;
+                if (a.ptr[l0 + 1] - base - rj <= rsp::kYWin) {
+                    sc = -((rj & (rsp::kYWin - 1)) + 1);
+                    a.src[k] = sc;
+                }
+            }
+        }
+        m += sc >= 0;
+    }
+    const int tot = block_sum(m, lds);
+    if (threadIdx.x == 0) a.nst[c] = tot;
+}
+
+// one workgroup per chunk: its staged range, row records, y indices and
+// staged terms (in term order: a block scan per 256 terms)
+__global__ __launch_bounds__(256) void st_fill(rsp_k::SolveTermsArgs a) {
+    __shared__ int lds[256];
+    const int c = blockIdx.x;
+    const rsp::LevelChunk ch = a.chunks[c];
+    const int base = a.cbase[c], st0 = a.nst_ptr[c];
+    if (threadIdx.x == 0) {
+        a.chunks[c].st0 = st0;
+        a.chunks[c].st1 = a.nst_ptr[c + 1];
+        if (c == 0 && a.nst_ptr[a.nch] == 0) a.stg[0] = rsp::StagedTerm{0, 0};  // the empty list's entry
+    }
+    const int G = a.group;
+    for (int x = ch.x0 + (int)threadIdx.x; x < ch.x1; x += 256) {
+        const rsp::RowTask t = a.tasks[x];
+        a.trow[x] = rsp::ThinRowPlan{(t.t0 - ch.k0) / G | ((t.t1 - t.t0) / G) << 16,
+                                     (x - base) & (rsp::kYWin - 1), t.i, t.d};
+    }
+    int run = st0;
+    for (int kb = ch.k0; kb < ch.k1; kb += 256) {
+        const int k = kb + (int)threadIdx.x;
+        const int sc = k < ch.k1 ? a.src[k] : -1;
+        int tot;
+        const int pos = block_excl_scan(sc >= 0 ? 1 : 0, lds, &tot);
+        if (k < ch.k1) {
+            if (sc < 0) {
+                a.sid[k] = -sc - 1;
+            } else {
+                a.sid[k] = rsp::kYWin + 1 + (k - ch.k0);
+                a.stg[run + pos] = rsp::StagedTerm{k - ch.k0, sc};
+            }
+        }
+        run += tot;
+    }
+}
+
+}  // namespace
+
+hipError_t ilu_an_solve_terms(const SolveTermsArgs &a, hipStream_t s) {
+    if (a.total <= 0 || a.nx <= 0 || a.nch <= 0) return hipErrorInvalidValue;  // the caller writes the empty plan
+    st_rows<<<(unsigned)((a.nx + 3) / 4), 256, 0, s>>>(a);
+    st_remap<<<a.nch, 256, 0, s>>>(a);
+    hipError_t e = hipMemsetAsync(a.nst + a.nch, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    size_t tb = 0;
+    ilu_an_scan(nullptr, nullptr, a.nch + 1, nullptr, &tb, s);
+    e = ilu_an_scan(a.nst, a.nst_ptr, a.nch + 1, a.scan, &tb, s);
+    if (e != hipSuccess) return e;
+    st_fill<<<a.nch, 256, 0, s>>>(a);
+    return hipGetLastError();
+}
+
 }  // namespace rsp_k

@@ -1078,6 +1078,88 @@ static void dag_upload(Arena &ar, rsp_ilu0_info::Dag &d, const rsp_an::DagHost &
     ar.up(&d.d_fitems, h.sp.fitems);
 }
 
+// Upload one DAG's per-row solve plan (L or L^T) into the arena and reserve
+// the per-term arrays, which rsp_k::ilu_an_solve_terms then builds on the
+// device (t: its arguments; pointers set at commit, the rest by the caller).
+static void dag_upload_rows(Arena &ar, rsp_ilu0_info::Dag &d, const rsp_an::DagHost &h, int n,
+                            rsp_k::SolveTermsArgs &t) {
+    d.ptr = h.ptr;
+    d.batch = h.batch;
+    d.group = h.group;
+    d.segs = h.sp.segs;
+    d.nshort = h.sp.nshort;
+    d.nwave = h.sp.nwave;
+    d.sbase = h.sp.sbase;
+    d.nterms = std::max(h.sp.nterm, 1);
+    const size_t nx = h.rows.size(), nch = h.sp.chunks.size();
+    long long thin_terms = 0;
+    for (const rsp::LevelChunk &ch : h.sp.chunks) thin_terms += ch.k1 - ch.k0;
+    ar.up(&d.d_rows, h.rows);
+    ar.up(&d.d_ptr, h.ptr);
+    ar.up(&d.d_tasks, h.sp.tasks);
+    ar.up(&d.d_nshort, h.sp.nshort);
+    ar.space((void **)&d.d_tpos, (size_t)d.nterms * 4);
+    ar.space((void **)&d.d_src, (size_t)d.nterms * 4);
+    ar.space((void **)&d.d_sid, (size_t)d.nterms * 4);
+    ar.up(&d.d_chunks, h.sp.chunks);  // staged ranges written on the device
+    ar.space((void **)&d.d_trow, std::max<size_t>(nx, 1) * sizeof(rsp::ThinRowPlan));
+    ar.space((void **)&d.d_stg, (size_t)std::max(thin_terms, 1LL) * sizeof(rsp::StagedTerm));
+    ar.up(&d.d_fitems, h.sp.fitems);
+    ar.up((int **)&t.cbase, h.sp.cbase);
+    ar.space((void **)&t.slot_of, (size_t)std::max(n, 1) * 4);
+    ar.space((void **)&t.nst, (nch + 1) * 4);
+    ar.space((void **)&t.nst_ptr, (nch + 1) * 4);
+    size_t tb = 0;
+    (void)rsp_k::ilu_an_scan(nullptr, nullptr, (int)nch + 1, nullptr, &tb, nullptr);
+    ar.space(&t.scan, std::max<size_t>(tb, 16));
+    t.n = n;
+    t.nx = (int)nx;
+    t.total = h.sp.nterm;
+    t.nch = (int)nch;
+    t.group = h.group;
+}
+
+// After the commit: the per-term arrays of a DAG uploaded by dag_upload_rows.
+static hipError_t dag_build_terms(rsp_ilu0_info::Dag &d, rsp_k::SolveTermsArgs &t, hipStream_t s) {
+    t.tasks = d.d_tasks;
+    t.ptr = d.d_ptr;
+    t.chunks = d.d_chunks;
+    t.tpos = d.d_tpos;
+    t.src = d.d_src;
+    t.sid = d.d_sid;
+    t.trow = d.d_trow;
+    t.stg = d.d_stg;
+    return rsp_k::ilu_an_solve_terms(t, s);
+}
+
+// Tests only (RSP_ILU_DIGEST): the device-built per-term arrays back into the
+// host plan, so the digest covers them.
+static hipError_t dag_download_terms(const rsp_ilu0_info::Dag &d, const rsp_k::SolveTermsArgs &t,
+                                     rsp_an::DagHost &h, hipStream_t s) {
+    rsp_an::SolvePlan &sp = h.sp;
+    int nstg = 0;
+    hipError_t e = hipMemcpyAsync(&nstg, t.nst_ptr + t.nch, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    sp.tpos.resize((size_t)d.nterms);
+    sp.src.resize((size_t)d.nterms);
+    sp.sid.resize((size_t)d.nterms);
+    sp.trow.resize(std::max<size_t>((size_t)t.nx, 1));
+    sp.stg.resize((size_t)std::max(nstg, 1));
+    e = hipMemcpyAsync(sp.tpos.data(), d.d_tpos, sp.tpos.size() * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(sp.src.data(), d.d_src, sp.src.size() * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(sp.sid.data(), d.d_sid, sp.sid.size() * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(sp.trow.data(), d.d_trow, sp.trow.size() * sizeof(rsp::ThinRowPlan), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(sp.stg.data(), d.d_stg, sp.stg.size() * sizeof(rsp::StagedTerm), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(sp.chunks.data(), d.d_chunks, sp.chunks.size() * sizeof(rsp::LevelChunk),
+                           hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e;
+}
+
 extern "C" {
 
 
@@ -1297,9 +1379,17 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     hp->nnz_s = nnz_s;
     // the solve plans are built on a second thread from the moment the levels
     // exist, under the symbolic factor's transfers and the factor plan
+    // their per-term half is built on the device after the upload
+    // (RSP_ILU_HOST_TERMS=1: on the host, as rsp_ilu0_analysis_host does; A/B)
+    const bool dev_terms = n > 0 && !env_int("RSP_ILU_HOST_TERMS", 0);
     std::thread solves;
     rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph, [&] {
-        solves = std::thread([&] { rsp_an::plan_solves(rp.data(), ci.data(), *hp); });
+        solves = std::thread([&] {
+            if (dev_terms)
+                rsp_an::plan_solves_rows(rp.data(), ci.data(), *hp);
+            else
+                rsp_an::plan_solves(rp.data(), ci.data(), *hp);
+        });
     });
     if (st == RSP_STATUS_SUCCESS) rsp_an::plan_factor(rp.data(), ci.data(), slot_cap_ints(), *hp);
     if (solves.joinable()) solves.join();
@@ -1327,7 +1417,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
                 e = hipMemcpyAsync(hp->udiv.data(), f->d_udiv, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, h->stream);
             if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         }
-        f->digest = e == hipSuccess ? rsp_an::digest(*hp) : 0;
+        f->digest = e == hipSuccess ? 1 : 0;  // computed once the solve terms exist (below)
     }
     // everything in one device allocation
     Arena ar;
@@ -1346,8 +1436,21 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         for (int x = hp->L.ptr[l]; x < hp->L.ptr[l + 1]; x++) lev[(size_t)hp->L.rows[(size_t)x]] = (int)l;
     ar.up(&f->d_lev, lev);
     ar.space((void **)&f->d_fdone, (size_t)std::max(n, 1) * sizeof(int));
-    dag_upload(ar, f->L, hp->L);
-    dag_upload(ar, f->LT, hp->LT);
+    rsp_k::SolveTermsArgs tl{}, tt{};
+    if (dev_terms) {
+        dag_upload_rows(ar, f->L, hp->L, n, tl);
+        dag_upload_rows(ar, f->LT, hp->LT, n, tt);
+        tl.kind = 0;
+        tl.rp = d_row_offsets;
+        tl.ci = d_col_ind;
+        tt.kind = 1;
+        ar.up((int **)&tt.ltp, hp->ltp);
+        ar.up((int **)&tt.lts, hp->lts);
+        ar.up((int **)&tt.ltc, hp->ltc);
+    } else {
+        dag_upload(ar, f->L, hp->L);
+        dag_upload(ar, f->LT, hp->LT);
+    }
     // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
     const size_t nt = (size_t)std::max({f->L.nterms, f->LT.nterms, 1});
     ar.space(&f->d_sval, nt * sizeof(double));
@@ -1361,6 +1464,18 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         ar.up(&d_offs, hp->slot_offs);
     }
     hipError_t e = ar.commit(&f->d_arena, h->stream);
+    if (e == hipSuccess && dev_terms) {
+        tl.dpos = f->d_dpos;
+        e = dag_build_terms(f->L, tl, h->stream);
+        if (e == hipSuccess) e = dag_build_terms(f->LT, tt, h->stream);
+    }
+    if (e == hipSuccess && env_int("RSP_ILU_DIGEST", 0)) {  // tests only
+        if (dev_terms) {
+            e = dag_download_terms(f->L, tl, hp->L, h->stream);
+            if (e == hipSuccess) e = dag_download_terms(f->LT, tt, hp->LT, h->stream);
+        }
+        f->digest = e == hipSuccess && f->digest ? rsp_an::digest(*hp) : 0;
+    }
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero + 1, 0, 1);
     if (e == hipSuccess) e = hipMemsetD32(f->d_fdone, 0, (size_t)std::max(n, 1));

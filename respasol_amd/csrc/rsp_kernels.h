@@ -392,4 +392,28 @@ hipError_t ilu_an_fill(const int *const rows_c[3], const int n_c[3], const int *
 hipError_t ilu_an_stages(int n, int maxlen, const int *rp, const int *ci, const int *dpos, const int *hasdiag,
                          const int *ptr, const int *upd_l, int *stage, int *lord, int *lend, int *udiv,
                          int *scratch, hipStream_t s);
+// The per-term half of a solve plan (ilu_analysis.cpp solve_plan_terms, same
+// arrays bit for bit) from its per-row half already on the device: flat term
+// positions and y sources, the thin runs' window remap, row records, y
+// indices, staged terms and the chunks' staged ranges. Row i's terms: kind 0
+// (L) positions [rp[i], dpos[i]) (column ci[p]); kind 1 (L^T) entries
+// [ltp[i], ltp[i+1]) of the transposed lower part (position lts[q], column
+// ltc[q]). stg holds room for every thin-run term (>= 1 entry); scratch:
+// slot_of (n ints), nst / nst_ptr (nch + 1 ints each), scan (temp bytes of
+// ilu_an_scan over nch + 1). nstg_out (device, may be null): staged terms.
+struct SolveTermsArgs {
+    int kind, n, nx, total, nch, group;
+    const rsp::RowTask *tasks;
+    const int *ptr;  // level pointers
+    const int *rp, *ci, *dpos;
+    const int *ltp, *lts, *ltc;
+    rsp::LevelChunk *chunks;
+    const int *cbase;  // per chunk: its thin run's first slot
+    int *tpos, *src, *sid;
+    rsp::ThinRowPlan *trow;
+    rsp::StagedTerm *stg;
+    int *slot_of, *nst, *nst_ptr;
+    void *scan;
+};
+hipError_t ilu_an_solve_terms(const SolveTermsArgs &a, hipStream_t s);
 }  // namespace rsp_k

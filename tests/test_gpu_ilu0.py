@@ -316,13 +316,17 @@ def test_unsorted_or_duplicate_rows_rejected(handle):
 
 
 @pytest.mark.parametrize("name,scale", [("ASIC_320ks", 1.0), ("dc1", 1.0), ("FEM_3D_thermal2", 0.2),
-                                        ("ecology2", 0.2), ("Goodwin_095", 0.2), ("G2_circuit", 0.3)])
+                                        ("ecology2", 0.2), ("Goodwin_095", 0.2), ("G2_circuit", 0.3),
+                                        ("matrix-new_3", 1.0), ("thermomech_TK", 1.0), ("tmt_unsym", 0.1),
+                                        ("crashbasis", 0.3), ("parabolic_fem", 0.2), ("para-10", 0.3)])
 def test_device_analysis_same_plan_as_host(handle, monkeypatch, name, scale):
     """rsp_ilu0_analysis validates the pattern, finds the diagonals and builds
     the symbolic factor (update lists, stages, stage order, divisor positions)
     with MI355X kernels; rsp_ilu0_analysis_host builds everything on the
     host. Every array of the plan must be identical (64-bit digest over all of
-    them), hub rows (ASIC_320ks: the long-row kernel classes) included."""
+    them), hub rows (ASIC_320ks: the long-row kernel classes) included — and
+    so the per-term half of the L and L^T solve plans, which the device
+    analysis builds with MI355X kernels (ilu_an_solve_terms)."""
     import ctypes as C
     from respasol_amd._lib import rsp
     monkeypatch.setenv("RSP_ILU_DIGEST", "1")
