@@ -5,6 +5,8 @@
 #include "ilu_analysis.h"
 
 #include <limits.h>
+#include <stdlib.h>
+#include <sys/mman.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -14,11 +16,70 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
+#include <unordered_map>
 #include <mutex>
 #include <thread>
 
 namespace rsp_an {
+
+// Block cache behind PoolAlloc (host_pool.h).
+namespace {
+constexpr size_t kHugePage = 2u << 20;
+struct BlockCache {
+    std::mutex m;
+    std::multimap<size_t, void *> free_blocks;    // size -> block
+    std::unordered_map<void *, size_t> live;      // block -> size
+    size_t cached = 0;
+    size_t cap = (size_t)std::max(0, env_int("RSP_HOST_POOL_MB", 1024)) << 20;
+};
+BlockCache &block_cache() {
+    static BlockCache *c = new BlockCache();  // never destroyed: blocks may be freed during exit
+    return *c;
+}
+}  // namespace
+
+void *pool_get(size_t bytes) {
+    const size_t r = (bytes + kHugePage - 1) & ~(kHugePage - 1);
+    BlockCache &c = block_cache();
+    {
+        std::lock_guard<std::mutex> g(c.m);
+        auto it = c.free_blocks.lower_bound(r);
+        if (it != c.free_blocks.end() && it->first <= r + r / 4 + kHugePage) {  // best fit, little slack
+            void *p = it->second;
+            const size_t s = it->first;
+            c.free_blocks.erase(it);
+            c.cached -= s;
+            c.live[p] = s;
+            return p;
+        }
+    }
+    void *p = nullptr;
+    if (posix_memalign(&p, kHugePage, r) != 0 || !p) throw std::bad_alloc();
+    (void)madvise(p, r, MADV_HUGEPAGE);  // a hint: without THP the block is just a block
+    std::lock_guard<std::mutex> g(c.m);
+    c.live[p] = r;
+    return p;
+}
+
+void pool_put(void *p, size_t) {
+    if (!p) return;
+    BlockCache &c = block_cache();
+    {
+        std::lock_guard<std::mutex> g(c.m);
+        auto it = c.live.find(p);
+        if (it == c.live.end()) return;  // not ours (cannot happen through PoolAlloc)
+        const size_t s = it->second;
+        c.live.erase(it);
+        if (c.cached + s <= c.cap) {
+            c.free_blocks.emplace(s, p);
+            c.cached += s;
+            return;
+        }
+    }
+    free(p);
+}
 
 static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
@@ -159,12 +220,12 @@ static void pfor_dyn(int n, long long work, long long grain, F f) {
 }
 
 // rows grouped by level (stable: ascending row within a level)
-static void group_levels(const std::vector<int> &lev, int nlev, std::vector<int> &ptr,
-                         std::vector<int> &rows) {
+static void group_levels(const hvec<int> &lev, int nlev, hvec<int> &ptr,
+                         hvec<int> &rows) {
     ptr.assign((size_t)nlev + 1, 0);
     for (int v : lev) ptr[(size_t)v + 1]++;
     for (int l = 0; l < nlev; l++) ptr[(size_t)l + 1] += ptr[(size_t)l];
-    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+    hvec<int> fill(ptr.begin(), ptr.end() - 1);
     rows.resize(lev.size());
     for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
 }
@@ -198,19 +259,19 @@ static int chain_batch(long long total, long long count) {
 //                    its position and y source, the window remap, the thin
 //                    runs' row records, y indices and staged terms.
 template <typename RowCount>
-static void solve_plan_rows(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
-                            int thin_rows, int group, const std::vector<int> &diag,
+static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
+                            int thin_rows, int group, const hvec<int> &diag,
                             RowCount row_count, SolvePlan &sp) {
     const int nlev = (int)ptr.size() - 1;
     const long long nx = (long long)rows.size();
     constexpr long long kGrain = 1 << 14;
-    std::vector<int> order(rows);
-    std::vector<int> nt_row((size_t)n, 0);
+    hvec<int> order(rows);
+    hvec<int> nt_row((size_t)n, 0);
     pfor(n, kGrain, [&](long long a, long long b) {
         for (long long i = a; i < b; i++) nt_row[(size_t)i] = row_count((int)i);
     });
     auto padded = [&](int cnt) { return std::max(1, (cnt + group - 1) / group) * group; };
-    std::vector<int> lpad((size_t)std::max(nlev, 1), 0);
+    hvec<int> lpad((size_t)std::max(nlev, 1), 0);
     pfor_dyn(nlev, nx, kGrain, [&](int l) {
         int t = 0;
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) t += padded(nt_row[(size_t)order[(size_t)x]]);
@@ -228,7 +289,7 @@ static void solve_plan_rows(int n, const std::vector<int> &ptr, const std::vecto
         else
             sp.segs.push_back({l, l + 1, thin, 0, 0, 0});
     }
-    std::vector<char> thin_lev((size_t)std::max(nlev, 1), 0);
+    hvec<char> thin_lev((size_t)std::max(nlev, 1), 0);
     for (const rsp::LevelSeg &sg : sp.segs)
         for (int l = sg.lb; l < sg.le; l++) thin_lev[(size_t)l] = (char)sg.thin;
     // within each level (stable): short rows, then wave rows, then (fat
@@ -249,7 +310,7 @@ static void solve_plan_rows(int n, const std::vector<int> &ptr, const std::vecto
         sp.nshort[(size_t)l] = c[0];
         sp.nwave[(size_t)l] = c[0] + c[1];
         if (c[0] == e - b || c[1] == e - b || c[2] == e - b) return;  // one class: order unchanged
-        std::vector<int> tmp(order.begin() + b, order.begin() + e);
+        hvec<int> tmp(order.begin() + b, order.begin() + e);
         int w[3] = {b, b + c[0], b + c[0] + c[1]};
         for (int i : tmp) order[(size_t)w[cls(i)]++] = i;
     });
@@ -258,7 +319,7 @@ static void solve_plan_rows(int n, const std::vector<int> &ptr, const std::vecto
     const bool pad_fat = fat_long == rsp::kFatLongTerms && env_int("RSP_ILU_FAT_PAD", 1) != 0;
     sp.sbase.assign((size_t)std::max(nlev, 1), -1);
     sp.tasks.assign(std::max<size_t>(rows.size(), 1), rsp::RowTask{0, 0, 0, -1});
-    std::vector<int> len((size_t)std::max(nx, 1LL), 0);
+    hvec<int> len((size_t)std::max(nx, 1LL), 0);
     pfor_dyn(nlev, nx, kGrain, [&](int l) {
         const bool padl = pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0;
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
@@ -319,7 +380,7 @@ static void solve_plan_rows(int n, const std::vector<int> &ptr, const std::vecto
                 n, nlev, group, nthin, lthin, nfat, lfat, nflow, lflow, sp.fitems.size());
     }
     if (sp.fitems.empty()) sp.fitems.push_back({0, 0, -1, -1});
-    std::vector<int> lterms((size_t)std::max(nlev, 1), 0);
+    hvec<int> lterms((size_t)std::max(nlev, 1), 0);
     for (int l = 0; l < nlev; l++)
         if (ptr[(size_t)l + 1] > ptr[(size_t)l])
             lterms[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l + 1] - 1].t1 - sp.tasks[(size_t)ptr[(size_t)l]].t0;
@@ -364,12 +425,12 @@ static void solve_plan_rows(int n, const std::vector<int> &ptr, const std::vecto
 // row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
 // (row_count(i) of them, as given to solve_plan_rows).
 template <typename RowTerms>
-static void solve_plan_terms(int n, const std::vector<int> &ptr, int group, RowTerms row_terms, SolvePlan &sp) {
+static void solve_plan_terms(int n, const hvec<int> &ptr, int group, RowTerms row_terms, SolvePlan &sp) {
     constexpr long long kGrain = 1 << 14;
     const int nlev = (int)ptr.size() - 1;
     const long long nx = (long long)ptr[(size_t)nlev], total = sp.nterm;
     sp.tpos.assign((size_t)total, -1);
-    std::vector<int> col((size_t)total, -1);
+    hvec<int> col((size_t)total, -1);
     pfor(nx, kGrain, [&](long long a, long long b) {
         for (long long x = a; x < b; x++) {
             int k = sp.tasks[(size_t)x].t0;
@@ -383,11 +444,11 @@ static void solve_plan_terms(int n, const std::vector<int> &ptr, int group, RowT
     pfor(total, kGrain, [&](long long a, long long b) {
         for (long long k = a; k < b; k++) sp.src[(size_t)k] = col[(size_t)k] < 0 ? rsp::kPadSrc : col[(size_t)k];
     });
-    std::vector<int> slot_of((size_t)n, -1);
+    hvec<int> slot_of((size_t)n, -1);
     pfor(nx, kGrain, [&](long long a, long long b) {
         for (long long x = a; x < b; x++) slot_of[(size_t)sp.tasks[(size_t)x].i] = (int)x;
     });
-    std::vector<int> thin_base((size_t)std::max(nlev, 1), -1);  // per thin level: its run's first slot
+    hvec<int> thin_base((size_t)std::max(nlev, 1), -1);  // per thin level: its run's first slot
     for (const rsp::LevelSeg &sg : sp.segs)
         if (sg.thin)
             for (int l = sg.lb; l < sg.le; l++) thin_base[(size_t)l] = ptr[(size_t)sg.lb];
@@ -415,7 +476,7 @@ static void solve_plan_terms(int n, const std::vector<int> &ptr, int group, RowT
     sp.trow.assign(std::max<size_t>((size_t)nx, 1), rsp::ThinRowPlan{0, 0, 0, -1});
     sp.sid.assign(sp.tpos.size(), rsp::kYWin);
     const int nch = (int)sp.chunks.size();
-    std::vector<int> nst((size_t)std::max(nch, 1), 0);
+    hvec<int> nst((size_t)std::max(nch, 1), 0);
     pfor_dyn(nch, nx, kGrain, [&](int c) {
         const rsp::LevelChunk &ch = sp.chunks[(size_t)c];
         int m = 0;
@@ -454,8 +515,8 @@ static void solve_plan_terms(int n, const std::vector<int> &ptr, int group, RowT
 
 // Both parts on the host.
 template <typename RowCount, typename RowTerms>
-static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vector<int> &rows,
-                             int thin_rows, int group, const std::vector<int> &diag,
+static void build_solve_plan(int n, const hvec<int> &ptr, const hvec<int> &rows,
+                             int thin_rows, int group, const hvec<int> &diag,
                              RowCount row_count, RowTerms row_terms, SolvePlan &sp) {
     solve_plan_rows(n, ptr, rows, thin_rows, group, diag, row_count, sp);
     solve_plan_terms(n, ptr, group, row_terms, sp);
@@ -468,14 +529,14 @@ static void build_solve_plan(int n, const std::vector<int> &ptr, const std::vect
 // kRndItemPairs update pairs. Wider levels are fat: in a flow run they
 // spread over all CUs, where a thin run stages every position through one
 // (A/B knobs RSP_ILU_THIN_FACTOR_ITEMS / RSP_ILU_THIN_FACTOR_FLOW).
-static std::vector<char> factor_thin_levels(const int *rp, const std::vector<int> &upd_ptr,
-                                            const std::vector<int> &ptr, const std::vector<int> &rows,
-                                            int thin_rows, std::vector<long long> *items_out) {
+static hvec<char> factor_thin_levels(const int *rp, const hvec<int> &upd_ptr,
+                                            const hvec<int> &ptr, const hvec<int> &rows,
+                                            int thin_rows, hvec<long long> *items_out) {
     const int nlev = (int)ptr.size() - 1;
     const int thin_items = env_int("RSP_ILU_THIN_FACTOR_ITEMS", rsp::kRndLevelItems);
     const int thin_flow = env_int("RSP_ILU_THIN_FACTOR_FLOW", rsp::kRndFlowItems);
-    std::vector<long long> litems((size_t)std::max(nlev, 1), 0);
-    std::vector<char> thin((size_t)std::max(nlev, 1), 0);
+    hvec<long long> litems((size_t)std::max(nlev, 1), 0);
+    hvec<char> thin((size_t)std::max(nlev, 1), 0);
     pfor_dyn(nlev, (long long)rows.size(), 1 << 14, [&](int l) {
         long long items = 0;
         int maxp = 0;
@@ -497,10 +558,10 @@ static std::vector<char> factor_thin_levels(const int *rp, const std::vector<int
 
 static int thin_factor_rows() { return env_int("RSP_ILU_THIN_FACTOR", rsp::kThinFactorRows); }
 
-std::vector<int> factor_thin_rows(const int *rp, const IluHostPlan &hp) {
-    const std::vector<char> thin = factor_thin_levels(rp, hp.sym.upd_ptr, hp.L.ptr, hp.L.rows, thin_factor_rows(),
+hvec<int> factor_thin_rows(const int *rp, const IluHostPlan &hp) {
+    const hvec<char> thin = factor_thin_levels(rp, hp.sym.upd_ptr, hp.L.ptr, hp.L.rows, thin_factor_rows(),
                                                       nullptr);
-    std::vector<int> out;
+    hvec<int> out;
     for (size_t l = 0; l + 1 < hp.L.ptr.size(); l++)
         if (thin[l])
             for (int x = hp.L.ptr[l]; x < hp.L.ptr[l + 1]; x++) out.push_back(hp.L.rows[(size_t)x]);
@@ -536,15 +597,15 @@ std::vector<int> factor_thin_rows(const int *rp, const IluHostPlan &hp) {
 static constexpr int kRndPieceItems = 1 << 17;
 
 static void build_factor_plan(int n, const int *rp, const int *ci,
-                              const std::vector<int> &dpos, const std::vector<int> &hasdiag,
-                              const IluSymbolic &sym, const std::vector<int> &ptr,
-                              const std::vector<int> &rows, int thin_rows, FacPlan &fp) {
+                              const hvec<int> &dpos, const hvec<int> &hasdiag,
+                              const IluSymbolic &sym, const hvec<int> &ptr,
+                              const hvec<int> &rows, int thin_rows, FacPlan &fp) {
     const int nlev = (int)ptr.size() - 1;
     const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
     const long long piece_items = std::max(1, env_int("RSP_ILU_PIECE_ITEMS", kRndPieceItems));
     const int nnz = rp[(size_t)n];
-    std::vector<long long> litems;
-    const std::vector<char> lthin = factor_thin_levels(rp, sym.upd_ptr, ptr, rows, thin_rows, &litems);
+    hvec<long long> litems;
+    const hvec<char> lthin = factor_thin_levels(rp, sym.upd_ptr, ptr, rows, thin_rows, &litems);
     // pairs of position p of thin row i (packed, see IluSymbolic::pair_base)
     auto pair_off = [&](int i) {
         return sym.pair_base.empty() ? 0 : sym.pair_base[(size_t)i] - sym.upd_ptr[(size_t)rp[(size_t)i]];
@@ -561,7 +622,7 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
         int seg, lb, le;
         FacPlan out;  // chunk records relative to the piece's own arrays
     };
-    std::vector<Piece> pieces;
+    hvec<Piece> pieces;
     for (int s = 0; s < (int)fp.segs.size(); s++) {
         const rsp::LevelSeg &sg = fp.segs[(size_t)s];
         if (!sg.thin) continue;
@@ -577,14 +638,14 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
         }
         pieces.push_back({s, lb, sg.le, FacPlan()});
     }
-    std::vector<unsigned long long> where((size_t)std::max(nnz, 1), 0ull);
+    hvec<unsigned long long> where((size_t)std::max(nnz, 1), 0ull);
     auto wload = [&](int q) { return __atomic_load_n(&where[(size_t)q], __ATOMIC_RELAXED); };
     pfor_dyn((int)pieces.size(), nnz, 1 << 15, [&](int pi) {
         Piece &pc = pieces[(size_t)pi];
         FacPlan &o = pc.out;
         // staged positions of the current chunk: open addressing, epoch-stamped
         constexpr int kH = 4 * rsp::kRndStaged;
-        std::vector<int> hkey(kH), hval(kH), hep(kH, 0);
+        hvec<int> hkey(kH), hval(kH), hep(kH, 0);
         int epoch = 0, nstg = 0;
         auto hslot = [&](int q) { return (int)(((unsigned)q * 2654435761u) >> 18) & (kH - 1); };
         auto hfind = [&](int q) {
@@ -620,7 +681,7 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
             ch.r1 = (int)o.rounds.size();
             o.chunks[(size_t)c] = ch;
         };
-        auto ref = [&](int q, std::vector<int> &fresh) {
+        auto ref = [&](int q, hvec<int> &fresh) {
             const unsigned long long w = wload(q), wk = w >> 12;
             if (wk == ckey) return (int)(w & 0xfff);
             if (c > 0 && wk == ckey - 1) return K + (int)(w & 0xfff);
@@ -634,8 +695,8 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
         struct RItem {
             int round, pos, row;
         };
-        std::vector<RItem> ritems, rsorted;
-        std::vector<int> rcount, fresh, ipairs;
+        hvec<RItem> ritems, rsorted;
+        hvec<int> rcount, fresh, ipairs;
         open_chunk();
         long long last_round_key = -1;
         int last_round_level = -1;  // level of the chunk's last round (-1: none yet)
@@ -748,7 +809,7 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
         sg.c1 = (int)fp.chunks.size();
     }
     if (fp.items.empty()) fp.items.push_back({0, 0, -1, -1});
-    for (std::vector<int> *v : {&fp.pairs, &fp.staged, &fp.rounds})
+    for (hvec<int> *v : {&fp.pairs, &fp.staged, &fp.rounds})
         if (v->empty()) v->push_back(0);
     if (fp.chunks.empty()) fp.chunks.push_back(rsp::RndChunk{});
 }
@@ -758,17 +819,17 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
 // column -> position map, then each lower k (ascending) walks row k's upper
 // part; a hit at column j appends (pos l_ik, pos u_kj) to position (i, j).
 
-static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<int> &ci,
-                         const std::vector<int> &dpos, const std::vector<int> &hasdiag,
+static bool ilu_symbolic(int n, const hvec<int> &rp, const hvec<int> &ci,
+                         const hvec<int> &dpos, const hvec<int> &hasdiag,
                          IluSymbolic &s) {
     const int nnz = rp[(size_t)n];
-    std::vector<int> cnt((size_t)nnz, 0);
+    hvec<int> cnt((size_t)nnz, 0);
     // pass 1: counts (rows are independent: a row writes only its own
     // positions' counts; each worker scatters its rows into its own map)
     std::mutex mu;
     long long total = 0;
     parallel_rows(n, [&](int r0, int r1) {
-        std::vector<int> map((size_t)n, -1);
+        hvec<int> map((size_t)n, -1);
         long long part = 0;
         for (int i = r0; i < r1; i++) {
             for (int p = rp[(size_t)i]; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
@@ -793,12 +854,12 @@ static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<in
     s.upd_l.resize((size_t)total);
     s.upd_u.resize((size_t)total);
     // pass 2: fill (k ascending per target, since p ascends) + stages
-    std::vector<int> &stage = s.stage;
+    hvec<int> &stage = s.stage;
     stage.assign((size_t)nnz, 0);
     s.lord.assign((size_t)nnz, 0);
     s.lend.assign((size_t)nnz, 0);
     parallel_rows(n, [&](int r0, int r1) {
-        std::vector<int> map((size_t)n, -1), order;
+        hvec<int> map((size_t)n, -1), order;
         for (int i = r0; i < r1; i++) {
             const int rs = rp[(size_t)i], di = dpos[(size_t)i];
             for (int p = rs; p < rp[(size_t)i + 1]; p++) map[(size_t)ci[(size_t)p]] = p;
@@ -838,11 +899,11 @@ static bool ilu_symbolic(int n, const std::vector<int> &rp, const std::vector<in
 // walks it in cache). cnt != nullptr: update-list counts of the rows'
 // positions; else the pairs at ptr, the stages, the stage order and the
 // divisor positions — every value exactly as ilu_symbolic / plan_symbolic.
-void symbolic_rows(const std::vector<int> &rows, int n, const int *rp, const int *ci, const int *dpos,
+void symbolic_rows(const hvec<int> &rows, int n, const int *rp, const int *ci, const int *dpos,
                    const int *hasdiag, int *cnt, const int *ptr, int *upd_l, int *upd_u, int *stage, int *lord,
                    int *lend, int *udiv) {
     if (rows.empty()) return;
-    std::vector<int> map((size_t)n, -1), cur, order;
+    hvec<int> map((size_t)n, -1), cur, order;
     for (int i : rows) {
         const int rs = rp[i], re = rp[i + 1], di = dpos[i];
         for (int p = rs; p < re; p++) map[(size_t)ci[p]] = p;
@@ -890,8 +951,8 @@ void symbolic_rows(const std::vector<int> &rows, int n, const int *rp, const int
 // for every j > i with u_ij != 0.
 void plan_u(const int *rp, const int *ci, IluHostPlan &hp) {
     const int n = hp.n;
-    const std::vector<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
-    std::vector<int> lvu((size_t)n, 0);
+    const hvec<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
+    hvec<int> lvu((size_t)n, 0);
     int nlu = n > 0 ? 1 : 0;
     for (int i = n - 1; i >= 0; i--) {
         int l = 0;
@@ -905,7 +966,7 @@ void plan_u(const int *rp, const int *ci, IluHostPlan &hp) {
     for (int i = 0; i < n; i++) nu += rp[(size_t)i + 1] - dpos[(size_t)i] - hasdiag[(size_t)i];
     hp.U.batch = chain_batch(nu, n);
     hp.U.group = env_int("RSP_ILU_GROUP", hp.U.batch == 2 ? 2 : 4) == 2 ? 2 : 4;
-    std::vector<int> udiag((size_t)n);
+    hvec<int> udiag((size_t)n);
     for (int i = 0; i < n; i++) udiag[(size_t)i] = hasdiag[(size_t)i] ? dpos[(size_t)i] : -1;
     const int thin_solve = std::min(env_int("RSP_ILU_THIN_SOLVE", rsp::kThinSolveRows), rsp::kThinThreads);
     build_solve_plan(n, hp.U.ptr, hp.U.rows, thin_solve, hp.U.group, udiag,
@@ -950,7 +1011,7 @@ rsp_status_t plan_validate(int n, const int *rpp, const int *cip, IluHostPlan &h
         });
     }
     if (bad) return RSP_STATUS_INVALID_VALUE;
-    std::vector<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
+    hvec<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
     dpos.assign((size_t)n, 0);
     hasdiag.assign((size_t)n, 0);
     parallel_rows(n, [&](int r0, int r1) {
@@ -971,7 +1032,7 @@ rsp_status_t plan_validate(int n, const int *rpp, const int *cip, IluHostPlan &h
 
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     const int n = hp.n;
-    const std::vector<int> &dpos = hp.dpos;
+    const hvec<int> &dpos = hp.dpos;
     // three independent sequential passes over the strict lower part, run
     // concurrently (each is memory-latency bound; splitting one over threads
     // measured slower on the box): the L levels, the transposed lower part,
@@ -979,7 +1040,7 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     // levels of the lower DAG (factor + L solve): the longest path ending at
     // each row (each row needs its producers')
     std::thread tl([&] {
-        std::vector<int> lv((size_t)n, 0);
+        hvec<int> lv((size_t)n, 0);
         int nl = n > 0 ? 1 : 0;
         for (int i = 0; i < n; i++) {
             int l = 0;
@@ -991,7 +1052,7 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     });
     // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
     std::thread tt([&] {
-        std::vector<int> lvt((size_t)n, 0);
+        hvec<int> lvt((size_t)n, 0);
         int nlt = n > 0 ? 1 : 0;
         for (int j = n - 1; j >= 0; j--) {
             nlt = std::max(nlt, lvt[(size_t)j] + 1);
@@ -1003,7 +1064,7 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
         group_levels(lvt, nlt, hp.LT.ptr, hp.LT.rows);
     });
     // transposed strict lower: row k lists (j, pos) for l_jk, j descending
-    std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
+    hvec<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
     ltp.assign((size_t)n + 1, 0);
     for (int j = 0; j < n; j++)
         for (int p = rp[j]; p < dpos[(size_t)j]; p++) ltp[(size_t)ci[p] + 1]++;
@@ -1011,7 +1072,7 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     lts.resize((size_t)ltp[(size_t)n]);
     ltc.resize((size_t)ltp[(size_t)n]);
     {
-        std::vector<int> fill(ltp.begin(), ltp.end() - 1);
+        hvec<int> fill(ltp.begin(), ltp.end() - 1);
         for (int j = n - 1; j >= 0; j--)
             for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
                 const int slot = fill[(size_t)ci[p]]++;
@@ -1025,7 +1086,7 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
 
 rsp_status_t plan_symbolic(const int *rpp, const int *cip, IluHostPlan &hp) {
     const int n = hp.n;
-    const std::vector<int> rp(rpp, rpp + (size_t)n + 1), ci(cip, cip + (size_t)hp.nnz_s);
+    const hvec<int> rp(rpp, rpp + (size_t)n + 1), ci(cip, cip + (size_t)hp.nnz_s);
     if (!ilu_symbolic(n, rp, ci, hp.dpos, hp.hasdiag, hp.sym)) return RSP_STATUS_ALLOC_FAILED;
     // per lower position (i, k): the position of its divisor u_kk (-1: none)
     hp.udiv.assign((size_t)hp.nnz_s, -1);
@@ -1056,8 +1117,8 @@ static int thin_solve_rows() {
 // rsp_k::ilu_an_solve_terms).
 static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool terms_on_host) {
     const int n = hp.n;
-    const std::vector<int> &dpos = hp.dpos;
-    const std::vector<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
+    const hvec<int> &dpos = hp.dpos;
+    const hvec<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
     const int thin_solve = thin_solve_rows();
     long long nlo = 0;
     for (int i = 0; i < n; i++) nlo += dpos[(size_t)i] - rp[(size_t)i];
@@ -1070,7 +1131,7 @@ static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool
     // sources) are independent: built concurrently
     std::thread tl([&] {
         timed_plan(n, "L", [&] {
-            solve_plan_rows(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, std::vector<int>(), cnt_l, hp.L.sp);
+            solve_plan_rows(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, hvec<int>(), cnt_l, hp.L.sp);
             if (terms_on_host)
                 solve_plan_terms(n, hp.L.ptr, hp.L.group, [&](int i, auto emit) {
                     for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
@@ -1078,7 +1139,7 @@ static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool
         });
     });
     timed_plan(n, "LT", [&] {
-        solve_plan_rows(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, std::vector<int>(), cnt_lt, hp.LT.sp);
+        solve_plan_rows(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, hvec<int>(), cnt_lt, hp.LT.sp);
         if (terms_on_host)
             solve_plan_terms(n, hp.LT.ptr, hp.LT.group, [&](int i, auto emit) {
                 for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++) emit(lts[(size_t)q], ltc[(size_t)q]);
@@ -1093,14 +1154,14 @@ void plan_solves_rows(const int *rp, const int *ci, IluHostPlan &hp) { plan_solv
 
 void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &hp) {
     const int n = hp.n, nnz_s = hp.nnz_s;
-    const std::vector<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
+    const hvec<int> &dpos = hp.dpos, &hasdiag = hp.hasdiag;
     const int thin_factor = thin_factor_rows();
     IluSymbolic &sym = hp.sym;
     hp.fac_batch = chain_batch((long long)sym.upd_ptr[(size_t)nnz_s], nnz_s);
     timed_plan(n, "factor", [&] {
         build_factor_plan(n, rp, ci, dpos, hasdiag, sym, hp.L.ptr, hp.L.rows, thin_factor, hp.fplan);
     });
-    const std::vector<int> &rows_l = hp.L.rows;
+    const hvec<int> &rows_l = hp.L.rows;
     const long long nx = (long long)rows_l.size();
     hp.frow.assign(std::max<size_t>(rows_l.size(), 1), rsp::FacRow{});
     pfor(nx, 1 << 14, [&](long long a, long long b) {
@@ -1117,14 +1178,14 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
     // budget, keeps the FacRow path. Per level (parallel): the largest
     // LDS-path row and pair count, the rows' own structure size, whether
     // every row fits the LDS path (flow runs); then the offsets in order.
-    const std::vector<int> &lp = hp.L.ptr;
+    const hvec<int> &lp = hp.L.ptr;
     const int nlev = (int)lp.size() - 1;
     hp.fslev.assign((size_t)std::max(nlev, 0), rsp::FacSlotLevel{0, 0, 0, 0, 0});
     struct LevStat {
         int rm, qm, all_lds, fat;
         long long own;
     };
-    std::vector<LevStat> ls((size_t)std::max(nlev, 1), LevStat{0, 0, 0, 0, 0});
+    hvec<LevStat> ls((size_t)std::max(nlev, 1), LevStat{0, 0, 0, 0, 0});
     for (const rsp::LevelSeg &sg : hp.fplan.segs)
         if (!sg.thin)
             for (int l = sg.lb; l < sg.le; l++) ls[(size_t)l].fat = 1;
@@ -1145,7 +1206,7 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
         }
     });
     long long total = 0;
-    std::vector<int> slot_levels;
+    hvec<int> slot_levels;
     for (int l = 0; l < nlev; l++) {
         const LevStat &st = ls[(size_t)l];
         if (!st.fat || st.rm == 0) continue;
@@ -1198,7 +1259,7 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
             });
     }
     if (hp.ffitems.empty()) hp.ffitems.push_back({0, 0, -1});  // keep the device array non-empty
-    std::vector<long long> sd0(slot_levels.size() + 1, 0);
+    hvec<long long> sd0(slot_levels.size() + 1, 0);
     for (size_t j = 0; j < slot_levels.size(); j++)
         sd0[j + 1] = sd0[j] + lp[(size_t)slot_levels[j] + 1] - lp[(size_t)slot_levels[j]];
     hp.slot_desc.resize((size_t)sd0.back());
@@ -1236,16 +1297,16 @@ rsp_status_t plan_host(int n, const int *rp, const int *ci, long long slot_cap, 
     ph.mark("symbolic");
     // the plans see what they see after the device analysis: no host copy of
     // the stage order, stage ends or divisor positions (kept for the digest)
-    std::vector<int> lord, lend, udiv;
+    hvec<int> lord, lend, udiv;
     lord.swap(hp.sym.lord);
     lend.swap(hp.sym.lend);
     udiv.swap(hp.udiv);
     // ... and, like it, only the thin rows' update pairs, packed (the full
     // lists are kept for the digest)
-    std::vector<int> upd_l, upd_u;
+    hvec<int> upd_l, upd_u;
     if (env_int("RSP_ILU_PACK_PAIRS", 1)) {
-        const std::vector<int> trows = factor_thin_rows(rp, hp);
-        std::vector<int> pl, pu;
+        const hvec<int> trows = factor_thin_rows(rp, hp);
+        hvec<int> pl, pu;
         hp.sym.pair_base.assign((size_t)std::max(n, 1), 0);
         for (int i : trows) {
             hp.sym.pair_base[(size_t)i] = (int)pl.size();
@@ -1286,7 +1347,7 @@ struct Fnv {  // FNV-1a over 8-byte words (bytes for the tail)
         for (; i < n; i++) h = (h ^ c[i]) * 1099511628211ULL;
     }
     template <typename V>
-    void vec(const std::vector<V> &v) {
+    void vec(const hvec<V> &v) {
         const uint64_t n = v.size();
         bytes(&n, sizeof(n));
         if (!v.empty()) bytes(v.data(), v.size() * sizeof(V));

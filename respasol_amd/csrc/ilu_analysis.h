@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "rsp.h"
+#include "host_pool.h"
 #include "rsp_kernels.h"
 
 namespace rsp_an {
@@ -25,42 +26,42 @@ inline int env_int(const char *name, int dflt) {
 }
 
 struct SolvePlan {
-    std::vector<int> sbase;   // per level: first flat term of its padded short rows, -1 = none
-    std::vector<int> nshort;  // per level
-    std::vector<int> nwave;   // per level: short + wave rows (the rest: hub rows)
-    std::vector<rsp::RowTask> tasks;
-    std::vector<int> tpos, src;
-    std::vector<rsp::LevelSeg> segs;
-    std::vector<rsp::LevelChunk> chunks;
-    std::vector<rsp::ThinRowPlan> trow;
-    std::vector<int> sid;
-    std::vector<rsp::StagedTerm> stg;
-    std::vector<rsp::FlowItem> fitems;  // flow segments' work items (LevelSeg c0 / c1 of a fat segment)
-    std::vector<int> cbase;  // per chunk: its thin run's first slot (not in the digest: derived)
+    hvec<int> sbase;   // per level: first flat term of its padded short rows, -1 = none
+    hvec<int> nshort;  // per level
+    hvec<int> nwave;   // per level: short + wave rows (the rest: hub rows)
+    hvec<rsp::RowTask> tasks;
+    hvec<int> tpos, src;
+    hvec<rsp::LevelSeg> segs;
+    hvec<rsp::LevelChunk> chunks;
+    hvec<rsp::ThinRowPlan> trow;
+    hvec<int> sid;
+    hvec<rsp::StagedTerm> stg;
+    hvec<rsp::FlowItem> fitems;  // flow segments' work items (LevelSeg c0 / c1 of a fat segment)
+    hvec<int> cbase;  // per chunk: its thin run's first slot (not in the digest: derived)
     int nterm = 0;           // flat terms (tpos.size() once the terms are built; >= 1 then)
 };
 
 // Symbolic ILU(0) data (built by ilu_symbolic below).
 struct IluSymbolic {
-    std::vector<int> upd_ptr, upd_l, upd_u, lord, lend;
-    std::vector<int> stage;  // per lower position: its intra-row stage
+    hvec<int> upd_ptr, upd_l, upd_u, lord, lend;
+    hvec<int> stage;  // per lower position: its intra-row stage
     // empty: upd_l / upd_u hold every pair (indexed as upd_ptr). Else only
     // the pairs of the rows of the factor's thin levels, packed: row i's pair
     // u at pair_base[i] + u - upd_ptr[rowptr[i]] (the device analysis
     // downloads no more; the factor plan reads no other row's pairs).
-    std::vector<int> pair_base;
+    hvec<int> pair_base;
 };
 
 struct FacPlan {
-    std::vector<rsp::LevelSeg> segs;
-    std::vector<rsp::RndChunk> chunks;
-    std::vector<rsp::RndItem> items;
-    std::vector<int> pairs, staged, rounds;
+    hvec<rsp::LevelSeg> segs;
+    hvec<rsp::RndChunk> chunks;
+    hvec<rsp::RndItem> items;
+    hvec<int> pairs, staged, rounds;
 };
 
 // One DAG's levels and solve plan.
 struct DagHost {
-    std::vector<int> ptr, rows;  // level pointers, rows in level order
+    hvec<int> ptr, rows;  // level pointers, rows in level order
     SolvePlan sp;
     int batch = 8, group = 4;
     bool planned = false;
@@ -69,23 +70,23 @@ struct DagHost {
 // Everything the analysis computes on the host.
 struct IluHostPlan {
     int n = 0, nnz_s = 0, structural_zero = -1;
-    std::vector<int> dpos, hasdiag, udiv;
+    hvec<int> dpos, hasdiag, udiv;
     IluSymbolic sym;
     DagHost L, LT, U;
     // transposed strict lower part (row k: (position of l_jk, j), j descending)
-    std::vector<int> ltp, lts, ltc;
+    hvec<int> ltp, lts, ltc;
     FacPlan fplan;
     int fac_batch = 8;
-    std::vector<rsp::FacRow> frow;
+    hvec<rsp::FacRow> frow;
     // fat factor levels in the slot layout: per L level (stride 0: FacRow
     // path), the rows to write (desc) and their offsets, total ints
-    std::vector<rsp::FacSlotLevel> fslev;
-    std::vector<int4> slot_desc;
-    std::vector<long long> slot_offs;
+    hvec<rsp::FacSlotLevel> fslev;
+    hvec<int4> slot_desc;
+    hvec<long long> slot_offs;
     long long slot_total = 0;
     // flow runs of the factor (rsp::FacFlowRun / FacFlowItem)
-    std::vector<rsp::FacFlowRun> fruns;
-    std::vector<rsp::FacFlowItem> ffitems;
+    hvec<rsp::FacFlowRun> fruns;
+    hvec<rsp::FacFlowItem> ffitems;
 };
 
 // Phase timer (RSP_ILU_TIMING=1 prints; phase_ms collects when given).
@@ -113,7 +114,7 @@ constexpr int kPhases = 6;  // phase slots of Phases::ms (marks in call order)
 rsp_status_t plan_validate(int n, const int *rp, const int *ci, IluHostPlan &hp);
 // The rows of the L DAG's levels the factor runs thin (needs the levels and
 // sym.upd_ptr): the only rows whose update pairs the factor plan reads.
-std::vector<int> factor_thin_rows(const int *rp, const IluHostPlan &hp);
+hvec<int> factor_thin_rows(const int *rp, const IluHostPlan &hp);
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp);
 rsp_status_t plan_symbolic(const int *rp, const int *ci, IluHostPlan &hp);
 void plan_solves(const int *rp, const int *ci, IluHostPlan &hp);
@@ -125,7 +126,7 @@ void plan_rest(const int *rp, const int *ci, long long slot_cap, bool want_u, Il
 // The symbolic factor of the given rows on the host (the device analysis'
 // long rows): counts when cnt != nullptr, else pairs at ptr + stages, stage
 // order, divisor positions (arrays indexed by position).
-void symbolic_rows(const std::vector<int> &rows, int n, const int *rp, const int *ci, const int *dpos,
+void symbolic_rows(const hvec<int> &rows, int n, const int *rp, const int *ci, const int *dpos,
                    const int *hasdiag, int *cnt, const int *ptr, int *upd_l, int *upd_u, int *stage, int *lord,
                    int *lend, int *udiv);
 // All of it. rp / ci: base 0, rp[n] stored entries. slot_cap_ints:

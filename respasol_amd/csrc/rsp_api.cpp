@@ -90,7 +90,7 @@ struct rsp_ilu0_info {
     long long n_updates;
     // one level set per DAG: L (factor + L solve), L^T, U
     struct Dag {
-        std::vector<int> ptr;                  // host level pointers
+        rsp_an::hvec<int> ptr;                  // host level pointers
         int *d_rows = nullptr, *d_ptr = nullptr;
         rsp::RowTask *d_tasks = nullptr;       // solve: task per level-order slot
         int *d_tpos = nullptr, *d_src = nullptr;  // solve: flat terms
@@ -101,25 +101,25 @@ struct rsp_ilu0_info {
         rsp::FlowItem *d_fitems = nullptr;     // solve: flow segments' work items
         int nterms = 0;                        // solve: flat terms
         int *d_nshort = nullptr;               // solve: short rows per level (device)
-        std::vector<int> nshort;               // (host)
-        std::vector<int> nwave;                // solve: short + wave rows per level (host)
-        std::vector<int> sbase;                // solve: padded short rows' first term per level (host)
-        std::vector<rsp::LevelSeg> segs;       // thread-per-row solve plan
+        rsp_an::hvec<int> nshort;               // (host)
+        rsp_an::hvec<int> nwave;                // solve: short + wave rows per level (host)
+        rsp_an::hvec<int> sbase;                // solve: padded short rows' first term per level (host)
+        rsp_an::hvec<rsp::LevelSeg> segs;       // thread-per-row solve plan
         int batch = 8;                         // solve fma-chain batch
         int group = 4;                         // thin-run term groups (2 or 4)
     } L, LT, U;
-    std::vector<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
+    rsp_an::hvec<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
     void *d_sval = nullptr, *d_sx = nullptr, *d_sdg = nullptr;  // solve streams (trsv_stream)
     rsp::RndChunk *d_rchunks = nullptr;        // round-based factor chunks (thin runs)
     rsp::RndItem *d_ritems = nullptr;
     rsp::FacRow *d_frow = nullptr;
     int *d_fslots = nullptr;                   // fat factor levels, slot layout (ilu0_level_slot)
-    std::vector<rsp::FacFlowRun> fruns;        // factor flow runs (ilu0_flow)
+    rsp_an::hvec<rsp::FacFlowRun> fruns;        // factor flow runs (ilu0_flow)
     rsp::FacFlowItem *d_ffitems = nullptr;
     int *d_lev = nullptr;                      // L level of each row
     int *d_fdone = nullptr;                    // per row: generation of the factor call that finished it
     int fac_gen = 0;
-    std::vector<rsp::FacSlotLevel> fslev;      // per L level (stride 0: FacRow path)
+    rsp_an::hvec<rsp::FacSlotLevel> fslev;      // per L level (stride 0: FacRow path)
     int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
     int fac_batch;
     void *d_arena = nullptr;    // one allocation holding the analysis' arrays (Arena)
@@ -129,7 +129,7 @@ struct rsp_ilu0_info {
     void *d_usval = nullptr;    // U solve term values (trsv_stream), in d_arena_u
     unsigned long long digest = 0;  // rsp_an::digest of the host plan
     std::unique_ptr<rsp_an::IluHostPlan> host;  // kept for the U plan
-    std::vector<int> host_rp, host_ci;
+    rsp_an::hvec<int> host_rp, host_ci;
 };
 
 #define RSP_CHECK_HIP(call)                                                     \
@@ -358,8 +358,8 @@ rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void
 // Greedy row-block schedule over host row offsets (see spmv.hip header).
 // Rows longer than kSpmvLongRow get tiles of their own (one per `chunk`
 // entries); the others are packed into tiles of <= cap entries / maxrows rows.
-static int build_spmv_plan(const int *rp, int m, int cap, int chunk, std::vector<SpmvBlock> &blocks,
-                           std::vector<SpmvLongRow> &longrows, int *nslots,
+static int build_spmv_plan(const int *rp, int m, int cap, int chunk, rsp_an::hvec<SpmvBlock> &blocks,
+                           rsp_an::hvec<SpmvLongRow> &longrows, int *nslots,
                            int maxrows = rsp::kSpmvMaxRows, int row_align = 1) {
     blocks.clear();
     longrows.clear();
@@ -427,11 +427,11 @@ static int build_spmv_plan(const int *rp, int m, int cap, int chunk, std::vector
 // tiles (interior tiles first when local_cols >= 0), long rows, per-tile
 // column base and the 16-bit column offsets.
 struct TilePlan {
-    std::vector<SpmvBlock> blocks;
-    std::vector<SpmvLongRow> longrows;
+    rsp_an::hvec<SpmvBlock> blocks;
+    rsp_an::hvec<SpmvLongRow> longrows;
     int nslots = 0, nint = 0;
-    std::vector<int> cbase;
-    std::vector<uint16_t> c16;
+    rsp_an::hvec<int> cbase;
+    rsp_an::hvec<uint16_t> c16;
     int64_t nnz_c16 = 0;
 };
 
@@ -454,8 +454,8 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
         const int64_t nnz_s = rp[(size_t)m];
         int c = (int)std::max<int64_t>(64, std::min<int64_t>(cap, (nnz_s + spread - 1) / spread));
         for (int tries = 0; tries < 32 && c < cap; tries++) {
-            std::vector<SpmvBlock> b2;
-            std::vector<SpmvLongRow> l2;
+            rsp_an::hvec<SpmvBlock> b2;
+            rsp_an::hvec<SpmvLongRow> l2;
             int s2 = 0;
             build_spmv_plan(rp, m, c, chunk, b2, l2, &s2, maxrows, align);
             if ((int64_t)b2.size() <= spread && b2.size() <= bb.nblocks) {
@@ -507,8 +507,8 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
 
 // Row offsets and column indices of `mat` on the host, validated (base 0,
 // non-decreasing offsets, columns inside [0, cols)).
-static rsp_status_t download_pattern(rsp_handle_t h, rsp_spmat_t mat, std::vector<int> &rp,
-                                     std::vector<int> &ci) {
+static rsp_status_t download_pattern(rsp_handle_t h, rsp_spmat_t mat, rsp_an::hvec<int> &rp,
+                                     rsp_an::hvec<int> &ci) {
     const int m = (int)mat->rows;
     rp.assign((size_t)m + 1, 0);
     ci.clear();
@@ -546,7 +546,7 @@ static int64_t spmv_resident_tiles(rsp_handle_t h, rsp_datatype_t t) {
 // memory (host-blocking; see struct rsp_spmat).
 static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t compute_type) {
     const int m = (int)mat->rows;
-    std::vector<int> rp, ci;
+    rsp_an::hvec<int> rp, ci;
     rsp_status_t st = download_pattern(h, mat, rp, ci);
     if (st != RSP_STATUS_SUCCESS) return st;
     const int chunk = chunk_cap(compute_type);
@@ -561,11 +561,11 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     make_tile_plan(rp.data(), ci.data(), m, mat->nnz, compute_type,
                    (h->spmv_variant & 16) ? 0 : spmv_resident_tiles(h, compute_type),
                    mat->local_cols, !(h->spmv_variant & 32), p, spmv_row_align(h, compute_type));
-    const std::vector<SpmvBlock> &blocks = p.blocks;
-    const std::vector<SpmvLongRow> &longrows = p.longrows;
+    const rsp_an::hvec<SpmvBlock> &blocks = p.blocks;
+    const rsp_an::hvec<SpmvLongRow> &longrows = p.longrows;
     const int nslots = p.nslots, nint = p.nint;
-    const std::vector<int> &cbase = p.cbase;
-    const std::vector<uint16_t> &c16 = p.c16;
+    const rsp_an::hvec<int> &cbase = p.cbase;
+    const rsp_an::hvec<uint16_t> &c16 = p.c16;
     const int64_t nnz_c16 = p.nnz_c16;
     (void)chunk;
     // exact layout of this schedule in the matrix's device memory (grown,
@@ -723,9 +723,9 @@ rsp_status_t rsp_spmv_part(rsp_handle_t h, const void *alpha, rsp_spmat_t mat, c
 struct rsp_spmv_batch {
     rsp_datatype_t type;
     int part;
-    std::vector<rsp_spmat_t> mats;
-    std::vector<unsigned long long> plan_gen;  // schedules as copied (stale check)
-    std::vector<rsp::SpmvBatchArgs> launches;  // one per kSpmvBatchMax matrices
+    rsp_an::hvec<rsp_spmat_t> mats;
+    rsp_an::hvec<unsigned long long> plan_gen;  // schedules as copied (stale check)
+    rsp_an::hvec<rsp::SpmvBatchArgs> launches;  // one per kSpmvBatchMax matrices
     void *d_mem = nullptr;                      // entries, tiles, long rows of every launch
     int64_t tiles = 0, entries_16bit = 0;       // rsp_spmv_batch_info
     ~rsp_spmv_batch() {
@@ -769,11 +769,11 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
     // matrix, so the partials stay in d_buffers[j].
     const int64_t R = spmv_resident_tiles(h, compute_type);
     const bool spread_ok = !(h->spmv_variant & 16), c16_ok = !(h->spmv_variant & 32);
-    std::vector<TilePlan> plans((size_t)count);
+    rsp_an::hvec<TilePlan> plans((size_t)count);
     // layout: per launch [entries | tiles | tile column bases | long rows |
     // 16-bit column offsets of each matrix], each 16-B aligned
-    struct Span { int first, count; size_t off_e, off_t, off_c, off_l; std::vector<size_t> off_16; };
-    std::vector<Span> spans;
+    struct Span { int first, count; size_t off_e, off_t, off_c, off_l; rsp_an::hvec<size_t> off_16; };
+    rsp_an::hvec<Span> spans;
     size_t bytes = 0;
     auto tile_range = [part](const TilePlan &p, int *t0, int *t1) {
         *t0 = part == 2 ? p.nint : 0;
@@ -781,7 +781,7 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
     };
     for (int first = 0; first < count; first += rsp::kSpmvBatchMax) {
         Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, {}};
-        std::vector<std::vector<int>> rps((size_t)sp.count), cis((size_t)sp.count);
+        rsp_an::hvec<rsp_an::hvec<int>> rps((size_t)sp.count), cis((size_t)sp.count);
         int64_t nt_full = 0, nnz_all = 0;
         for (int q = 0; q < sp.count; q++) {
             rsp_spmat_t A = mats[first + q];
@@ -830,7 +830,7 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         spans.push_back(sp);
     }
     if (bytes > 0) RSP_CHECK_HIP(hipMalloc(&b->d_mem, bytes));
-    std::vector<unsigned char> host(bytes);
+    rsp_an::hvec<unsigned char> host(bytes);
     for (const Span &sp : spans) {
         rsp::SpmvBatchArgs a{};
         a.entries = (const rsp::SpmvBatchEntry *)((char *)b->d_mem + sp.off_e);
@@ -1010,7 +1010,7 @@ rsp_status_t rsp_ilu0_buffer_size(rsp_handle_t h, int n, int nnz, rsp_datatype_t
 
 // Device helpers of the ILU analysis upload.
 template <typename V>
-static hipError_t upload_vec(V **dst, const std::vector<V> &v) {
+static hipError_t upload_vec(V **dst, const rsp_an::hvec<V> &v) {
     size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(V);
     hipError_t e = hipMalloc((void **)dst, bytes);
     if (e != hipSuccess) return e;
@@ -1028,14 +1028,14 @@ struct Arena {
         const void *src;
         size_t bytes, copy, off;
     };
-    std::vector<Item> items;
+    rsp_an::hvec<Item> items;
     size_t total = 0;
     void add(void **dst, const void *src, size_t bytes, size_t copy) {
         items.push_back({dst, src, bytes, copy, total});
         total += (bytes + 255) & ~(size_t)255;
     }
     template <typename V>
-    void up(V **dst, const std::vector<V> &v) {
+    void up(V **dst, const rsp_an::hvec<V> &v) {
         add((void **)dst, v.empty() ? nullptr : v.data(), std::max<size_t>(v.size(), 1) * sizeof(V),
             v.size() * sizeof(V));
     }
@@ -1186,7 +1186,7 @@ static long long slot_cap_ints() {
 // included).
 static constexpr int kAnDevRow = 1024;
 static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const int *d_rp, const int *d_ci,
-                                        const std::vector<int> &rp, std::vector<int> &ci, rsp_an::IluHostPlan &hp,
+                                        const rsp_an::hvec<int> &rp, rsp_an::hvec<int> &ci, rsp_an::IluHostPlan &hp,
                                         rsp_an::Phases &ph, const std::function<void()> &after_levels) {
     const int n = hp.n, nnz_s = hp.nnz_s;
     hipStream_t s = h->stream;
@@ -1199,7 +1199,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
                 std::chrono::duration<double, std::milli>(t - t_last).count());
         t_last = t;
     };
-    std::vector<int> dev_rows, long_rows;
+    rsp_an::hvec<int> dev_rows, long_rows;
     for (int i = 0; i < n; i++) (rp[(size_t)i + 1] - rp[(size_t)i] <= kAnDevRow ? dev_rows : long_rows).push_back(i);
     size_t scan_bytes = 0;
     RSP_CHECK_HIP(rsp_k::ilu_an_scan(nullptr, nullptr, nnz_s + 1, nullptr, &scan_bytes, s));
@@ -1242,7 +1242,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     RSP_CHECK_HIP(hipStreamSynchronize(s));
     sub("count kernel + D2H pattern");
     // the long rows' counts on the host
-    std::vector<int> hcnt(long_rows.empty() ? 0 : (size_t)nnz_s);
+    rsp_an::hvec<int> hcnt(long_rows.empty() ? 0 : (size_t)nnz_s);
     rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), hcnt.data(),
                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     for (int i : long_rows)
@@ -1280,8 +1280,8 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     // plan digest (which covers the full arrays).
     const bool pack = long_rows.empty() && !env_int("RSP_ILU_DIGEST", 0) && env_int("RSP_ILU_PACK_PAIRS", 1);
     if (pack) {
-        const std::vector<int> trows = rsp_an::factor_thin_rows(rp.data(), hp);
-        std::vector<int> cbase(trows.size() + 1, 0);
+        const rsp_an::hvec<int> trows = rsp_an::factor_thin_rows(rp.data(), hp);
+        rsp_an::hvec<int> cbase(trows.size() + 1, 0);
         for (size_t r = 0; r < trows.size(); r++) {
             const int i = trows[r];
             cbase[r + 1] = cbase[r] + hp.sym.upd_ptr[(size_t)rp[(size_t)i + 1]] - hp.sym.upd_ptr[(size_t)rp[(size_t)i]];
@@ -1322,7 +1322,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     RSP_CHECK_HIP(hipStreamSynchronize(s));
     sub("D2H pairs + stages");
     if (!long_rows.empty()) {  // the long rows' lists, stages, stage order, divisors on the host
-        std::vector<int> lord((size_t)nnz_s), lend((size_t)nnz_s), udiv((size_t)nnz_s);
+        rsp_an::hvec<int> lord((size_t)nnz_s), lend((size_t)nnz_s), udiv((size_t)nnz_s);
         rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), nullptr,
                               hp.sym.upd_ptr.data(), hp.sym.upd_l.data(), hp.sym.upd_u.data(), hp.sym.stage.data(),
                               lord.data(), lend.data(), udiv.data());
@@ -1353,14 +1353,24 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     ph.n = n;
     ph.start();
     if (!f || n < 0 || nnz < 0 || (n > 0 && !d_row_offsets)) return RSP_STATUS_INVALID_VALUE;
+    const bool tm3 = env_int("RSP_ILU_TIMING", 0) >= 3;  // diagnostics: preamble sub-phases
+    auto t_pre = std::chrono::steady_clock::now();
+    auto pre = [&](const char *what) {
+        if (!tm3) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "rsp_ilu0_analysis n=%d     %-22s %8.2f ms\n", n, what,
+                std::chrono::duration<double, std::milli>(t - t_pre).count());
+        t_pre = t;
+    };
     ilu_free_device(f);
+    pre("free");
     f->analysed = 0;
     f->factored = 0;
     f->structural_zero = -1;
     f->host.reset();
     // the pattern to the host (row offsets first: the stored entries must lie
     // inside the declared arrays before colidx is read)
-    std::vector<int> rp((size_t)n + 1, 0);
+    rsp_an::hvec<int> rp((size_t)n + 1, 0);
     if (n > 0) {
         RSP_CHECK_HIP(hipMemcpyAsync(rp.data(), d_row_offsets, ((size_t)n + 1) * sizeof(int),
                                      hipMemcpyDeviceToHost, h->stream));
@@ -1372,7 +1382,8 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     const int nnz_s = rp[(size_t)n];
     if (nnz_s > 0 && !d_col_ind) return RSP_STATUS_INVALID_VALUE;
     if (nnz_s > nnz) return RSP_STATUS_INVALID_VALUE;  // entries past the declared arrays
-    std::vector<int> ci((size_t)nnz_s);
+    pre("D2H rowptr + checks");
+    rsp_an::hvec<int> ci((size_t)nnz_s);
     std::unique_ptr<rsp_an::IluHostPlan> hp(new (std::nothrow) rsp_an::IluHostPlan());
     if (!hp) return RSP_STATUS_ALLOC_FAILED;
     hp->n = n;
@@ -1431,7 +1442,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     f->fruns = hp->fruns;
     // the L level of each row (flow runs: which producers are inside the run;
     // kept alive until the commit below copies it)
-    std::vector<int> lev((size_t)std::max(n, 1), 0);
+    rsp_an::hvec<int> lev((size_t)std::max(n, 1), 0);
     for (size_t l = 0; l + 1 < hp->L.ptr.size(); l++)
         for (int x = hp->L.ptr[l]; x < hp->L.ptr[l + 1]; x++) lev[(size_t)hp->L.rows[(size_t)x]] = (int)l;
     ar.up(&f->d_lev, lev);
@@ -1606,7 +1617,7 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
     return RSP_STATUS_SUCCESS;
 }
 
-static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const std::vector<rsp::LevelSeg> &segs,
+static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const rsp_an::hvec<rsp::LevelSeg> &segs,
                                  int batch) {
     rsp::LevelPlan p;
     p.rows = d.d_rows;
@@ -1702,7 +1713,7 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     else
         e = h->ftz ? rsp_k_ftz::ilu0_factor_f32(a, h->stream) : rsp_k::ilu0_factor_f32(a, h->stream);
     if (trace_file && e == hipSuccess) {
-        std::vector<unsigned long long> t(trace_cap);
+        rsp_an::hvec<unsigned long long> t(trace_cap);
         RSP_CHECK_HIP(hipMemcpyAsync(t.data(), d_trace, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost,
                                      h->stream));
         RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
@@ -1784,7 +1795,7 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
         return RSP_STATUS_INVALID_VALUE;
     }
     if (trace_file && e == hipSuccess) {
-        std::vector<unsigned long long> t(trace_cap);
+        rsp_an::hvec<unsigned long long> t(trace_cap);
         RSP_CHECK_HIP(hipMemcpyAsync(t.data(), d_trace, t.size() * sizeof(t[0]), hipMemcpyDeviceToHost,
                                      h->stream));
         RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
