@@ -295,7 +295,7 @@ static int setup_stencil(gen_ctx *c, long long target_s, int dim) {
     long long key[MAXOFF];
     for (int k = 0; k < no; k++) {
         long long lin = (long long)c->ox[k] + (long long)c->nx * (c->oy[k] + (long long)c->ny * c->oz[k]);
-        key[k] = (lin << 20) | k; /* |lin| < 2^42 for every catalogued grid */
+        key[k] = lin * (1LL << 20) + k; /* = (lin << 20) | k without shifting a negative; |lin| < 2^42 */
     }
     qsort(key, (size_t)no, sizeof(long long), cmp_ll);
     int tx[MAXOFF], ty[MAXOFF], tz[MAXOFF];

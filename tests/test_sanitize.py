@@ -61,3 +61,38 @@ def test_host_code_clean_on_surrogate(asan_exe, tmp_path):
     assert p.returncode == 0, err
     row = out.read_text().strip().split(",")
     assert row[0] == "2" and row[1] == "dc1"
+
+
+AN_TSAN = os.path.join(ROOT, "respasol_amd", "build", "asan", "an_host_check_tsan")
+AN_ASAN = os.path.join(ROOT, "respasol_amd", "build", "asan", "an_host_check_asan")
+
+
+@pytest.fixture(scope="module")
+def an_exes():
+    """The ILU analysis' host half (worker pool, concurrent L / L^T / factor
+    plans, the factor pieces' shared position table, the block cache) under
+    ThreadSanitizer and under ASan + UBSan (respasol_amd/drivers/an_host_check.cpp)."""
+    if shutil.which("g++") is None or shutil.which("make") is None:
+        pytest.skip("g++/make not available")
+    r = subprocess.run(["make", "-s", "-C", CSRC, "tsan", "asan-an"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return AN_TSAN, AN_ASAN
+
+
+@pytest.mark.parametrize("name,scale", [("dc1", 0.3), ("ecology2", 0.05), ("ASIC_320ks", 0.1),
+                                        ("FEM_3D_thermal2", 0.05)])
+def test_analysis_host_clean_under_tsan_and_asan(an_exes, name, scale):
+    """Plans built twice per run must agree (digest) and no sanitizer may
+    report; small factor pieces (RSP_ILU_PIECE_ITEMS) so several pieces are
+    planned concurrently, 4 worker threads."""
+    env = dict(os.environ, OMP_NUM_THREADS="4", RSP_ILU_PIECE_ITEMS="4096",
+               TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    digests = set()
+    for exe in an_exes:
+        p = subprocess.run([exe, name, str(scale)], env=env, capture_output=True, text=True, timeout=300)
+        ok, err = _clean(p)
+        assert ok and "ThreadSanitizer" not in err, err
+        assert p.returncode == 0, err
+        digests.add(p.stdout.split()[-1])
+    assert len(digests) == 1  # the same plan from both builds
