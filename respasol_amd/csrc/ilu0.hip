@@ -194,6 +194,42 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Wait until the LDS counter *p >= want (wave-uniform value; bounded: a plan
+// bug gives wrong bits in the tests, never a hung GPU). RSP_POLL_MODE (A/B):
+// 0 (shipped) = read -> wait -> compare; 1 = two reads in flight, each step
+// waiting for the older one only; 2 = s_sleep(RSP_POLL_SLEEP) between reads.
+// Config 3, same box, interleaved x2: fp64 factor / solve 58.6-58.8 /
+// 43.5-43.7 ms (mode 0), 59.6-59.7 / 46.7 (mode 1), 59.8 / 45.8 (mode 2,
+// sleep 1), 60.2 / 47.3 (sleep 2).
+#ifndef RSP_POLL_MODE
+#define RSP_POLL_MODE 0
+#endif
+#ifndef RSP_POLL_SLEEP
+#define RSP_POLL_SLEEP 1
+#endif
+__device__ __forceinline__ void lds_wait_geq(int *p, int want) {
+#if RSP_POLL_MODE == 1
+    const unsigned addr = (unsigned)(size_t)(__attribute__((address_space(3))) int *)p;
+    int a, b;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(a) : "v"(addr) : "memory");
+    for (int it = 0; it < (1 << 25); ++it) {
+        asm volatile("ds_read_b32 %0, %2\n\ts_waitcnt lgkmcnt(1)" : "=&v"(b), "+v"(a) : "v"(addr) : "memory");
+        if (__builtin_amdgcn_readfirstlane(a) >= want) break;
+        asm volatile("ds_read_b32 %0, %2\n\ts_waitcnt lgkmcnt(1)" : "=&v"(a), "+v"(b) : "v"(addr) : "memory");
+        if (__builtin_amdgcn_readfirstlane(b) >= want) break;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+    for (int it = 0; it < (1 << 26) && __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want;
+         ++it) {
+#if RSP_POLL_MODE == 2
+        __builtin_amdgcn_s_sleep(RSP_POLL_SLEEP);
+#endif
+    }
+#endif
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // --------------------------------------------------------------- kernels
 
 // Fat level, global-memory path: one wave per row.
@@ -839,14 +875,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 const ItemPre p1 = item_pre(b1 + min(lane, max(n1 - 1, 0)), cb);
                 const bool sh0 = !__ballot(lane < n0 && (p0.r.y >> 16) > 2);
                 const bool sh1 = !__ballot(lane < n1 && (p1.r.y >> 16) > 2);
-                if (s0 > q) {  // bounded: a plan bug gives wrong bits in the tests, never a hung GPU
-                    const int want = ch.r0 + s0;
-                    for (int i = 0; i < (1 << 26) &&
-                                    __hip_atomic_load(&lds_rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want;
-                         ++i) {
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                }
+                if (s0 > q) lds_wait_geq(&lds_rdone, ch.r0 + s0);
                 if (lane < n0) item_post(b0 + lane, cb, p0, sh0);
                 wave_order();
                 if (has1) {
@@ -1536,15 +1565,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 v2 = lval[gi];
             }
             const int L = ch.l0 + q;
-            if (L > L0) {
-                // bounded (a missing producer would be a plan bug: wrong
-                // bits in the tests, never a hung GPU)
-                for (int it = 0; it < (1 << 26) &&
-                                 __hip_atomic_load(&lds_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < L;
-                     ++it) {
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-            }
+            if (L > L0) lds_wait_geq(&lds_done, L);
             T s = group_fma(R.x, v1, i1);
             if (two) {
                 s = group_fma(s, v2, i2);
