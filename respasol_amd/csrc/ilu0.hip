@@ -1799,6 +1799,11 @@ hipError_t ilu0_factor_f32(const IluArgs &a, hipStream_t s) { return factor_disp
 hipError_t trsv_lower_n_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 0>(a, s); }
 hipError_t trsv_lower_t_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 1>(a, s); }
 hipError_t trsv_upper_f32(const TrsvArgs &a, hipStream_t s) { return solve_dispatch<float, 2>(a, s); }
+
+void warm_ilu() {  // see rsp_kernels.h
+    int o = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, trsv_stream<float, 0>, 256, 0);
+}
 #ifndef RSP_FTZ_BUILD
 // Slot rows of the fat factor levels (analysis, once per pattern). Padding
 // is written too: divisor positions -1 and pairs (0, 0), so every value

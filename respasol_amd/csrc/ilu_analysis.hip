@@ -181,6 +181,11 @@ inline unsigned grid_of(long long count) { return (unsigned)((count + kAnThreads
 
 }  // namespace
 
+void warm_analysis() {  // see rsp_kernels.h
+    int o = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, an_rows, kAnThreads, 0);
+}
+
 hipError_t ilu_an_rows(int n, const int *rp, const int *ci, int *dpos, int *hasdiag, int *flags,
                        hipStream_t s) {
     if (n <= 0) return hipSuccess;

@@ -176,6 +176,14 @@ rsp_status_t rsp_create(rsp_handle_t *handle) {
     const char *v = getenv("RSP_SPMV_VARIANT");
     c->spmv_variant = v ? atoi(v) : 0;
     c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    // every kernel code object loaded now, as cusparseCreate sets itself up
+    // outside the reference's timed calls (a lazily loaded one cost the
+    // first timed SpMV of a --ref-sequence run 1.2-1.5 ms, measured)
+    rsp_k::warm_spmv();
+    rsp_k_ftz::warm_spmv();
+    rsp_k::warm_ilu();
+    rsp_k_ftz::warm_ilu();
+    rsp_k::warm_analysis();
     c->d_ftrace = nullptr;
     c->d_strace = nullptr;
     *handle = c;
@@ -542,6 +550,27 @@ static int64_t spmv_resident_tiles(rsp_handle_t h, rsp_datatype_t t) {
     return (int64_t)rsp_k::spmv_tiles_per_cu((int)elem_size(t)) * h->num_cus;
 }
 
+// Whether a matrix's gathers are scattered (circuit-like): a row longer than
+// a tile, or more than 2 % of the entries of a sample of rows (every
+// m / 65536-th) more than 32768 columns off the diagonal. Only those gain from
+// being spread over every resident slot: their tiles wait on random x reads
+// and more of them in flight hide that; a local (stencil / FEM) matrix's
+// small tiles only add workgroups. Per call, 20 back-to-back calls of one
+// matrix (profiles/r03_spread_ab.txt): thermomech_TK 7.1 -> 6.0 us, cfd2
+// 8.4 -> 7.3, parabolic_fem 9.9 -> 8.4 unspread; G2_circuit 15.2 -> 11.3,
+// matrix-new_3 15.8 -> 12.9, ss1 18.8 -> 15.3 spread.
+static bool spmv_scattered(const int *rp, const int *ci, int m, int tile_cap) {
+    const int step = std::max(1, m / 65536);
+    int64_t far = 0, seen = 0;
+    for (int i = 0; i < m; i++) {
+        if (rp[i + 1] - rp[i] > tile_cap) return true;
+        if (i % step) continue;
+        for (int q = rp[i]; q < rp[i + 1]; q++) far += std::llabs((long long)ci[q] - i) > 32768;
+        seen += rp[i + 1] - rp[i];
+    }
+    return far * 50 > seen;
+}
+
 // Build the schedule of `mat` for `compute_type` into the matrix's own device
 // memory (host-blocking; see struct rsp_spmat).
 static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t compute_type) {
@@ -550,16 +579,19 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     rsp_status_t st = download_pattern(h, mat, rp, ci);
     if (st != RSP_STATUS_SUCCESS) return st;
     const int chunk = chunk_cap(compute_type);
-    // A matrix with fewer tiles than the chip holds resident workgroups (R)
-    // leaves slots idle and runs each tile latency-bound: spread it over up
-    // to R smaller tiles (measured +2.7 % on the moderate set per matrix;
-    // plans of >= 2 waves are left alone, they lost 1 % this way). A batch
-    // re-plans its members itself (rsp_spmv_batch_create). Tiling never
-    // changes the result (canonical summation order). RSP_SPMV_VARIANT bit 4
-    // turns spreading off, bit 5 keeps every tile on the int32 indices.
+    // A scattered matrix (spmv_scattered) with fewer tiles than the chip
+    // holds resident workgroups (R) leaves slots idle and runs each tile
+    // latency-bound: spread it over up to R smaller tiles (plans of >= 2
+    // waves are left alone, they lost 1 % this way); a local one keeps full
+    // tiles. A batch re-plans its members itself (rsp_spmv_batch_create).
+    // Tiling never changes the result (canonical summation order).
+    // RSP_SPMV_VARIANT bit 4 turns spreading off, bit 9 spreads every small
+    // matrix (round-2 rule), bit 5 keeps every tile on the int32 indices.
+    const bool spread = !(h->spmv_variant & 16) &&
+                        ((h->spmv_variant & 512) || spmv_scattered(rp.data(), ci.data(), m, chunk));
     TilePlan p;
     make_tile_plan(rp.data(), ci.data(), m, mat->nnz, compute_type,
-                   (h->spmv_variant & 16) ? 0 : spmv_resident_tiles(h, compute_type),
+                   spread ? spmv_resident_tiles(h, compute_type) : 0,
                    mat->local_cols, !(h->spmv_variant & 32), p, spmv_row_align(h, compute_type));
     const rsp_an::hvec<SpmvBlock> &blocks = p.blocks;
     const rsp_an::hvec<SpmvLongRow> &longrows = p.longrows;
@@ -567,7 +599,6 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     const rsp_an::hvec<int> &cbase = p.cbase;
     const rsp_an::hvec<uint16_t> &c16 = p.c16;
     const int64_t nnz_c16 = p.nnz_c16;
-    (void)chunk;
     // exact layout of this schedule in the matrix's device memory (grown,
     // never shrunk, on a re-plan)
     SpmvBounds b{blocks.size(), longrows.size(), (size_t)nslots};

@@ -351,6 +351,8 @@ struct TrsvArgs {
     hipError_t trsv_lower_n_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
     hipError_t trsv_lower_t_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
     hipError_t trsv_upper_f32(const rsp::TrsvArgs &a, hipStream_t s);                           \
+    void warm_spmv();                                                                           \
+    void warm_ilu();                                                                            \
     }
 
 RSP_DECLARE_KERNEL_API(rsp_k)
@@ -364,6 +366,10 @@ hipError_t scatter(int elem_bytes, int64_t n, const int64_t *idx, const void *sr
 hipError_t spmv_f64(const rsp::SpmvArgs &a, hipStream_t s);
 hipError_t spmv_batch_f64(const rsp::SpmvBatchArgs &a, hipStream_t s);
 int spmv_tiles_per_cu(int elem_bytes);  // resident spmv_tiles workgroups per CU
+// warm_*: load the translation unit's code object on the current device now
+// (HIP loads a code object at the first use of one of its kernels; without
+// this, the first timed call of a run pays it: ~1.2-1.5 ms, measured).
+void warm_analysis();
 hipError_t ilu0_factor_f64(const rsp::IluArgs &a, hipStream_t s);
 hipError_t trsv_lower_n_f64(const rsp::TrsvArgs &a, hipStream_t s);
 hipError_t trsv_lower_t_f64(const rsp::TrsvArgs &a, hipStream_t s);

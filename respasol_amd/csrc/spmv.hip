@@ -629,6 +629,13 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
 }
 
 hipError_t spmv_f32(const SpmvArgs &a, hipStream_t s) { return launch_spmv<float>(a, s); }
+void warm_spmv() {
+    hipFuncAttributes at;
+    (void)hipFuncGetAttributes(&at, reinterpret_cast<const void *>(spmv_tiles<float, true, false>));
+    int o = 0;  // (the occupancy query is the use measured to load the code object)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, spmv_tiles<float, true, false>, kSpmvThreads, 0);
+}
+
 #ifndef RSP_FTZ_BUILD
 int spmv_tiles_per_cu(int elem_bytes) {
     int o = 0;

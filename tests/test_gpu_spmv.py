@@ -280,10 +280,11 @@ def test_column_offset_tiles(handle):
         check(A, x, dt, handle)
 
 
-@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33, 64, 128, 80, 256, 257])
+@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33, 64, 128, 80, 256, 257, 512])
 def test_kernel_variants_same_bits(monkeypatch, variant):
     """Every kernel / plan variant (RSP_SPMV_VARIANT: default-policy instead of
-    non-temporal loads; small plans not spread over the chip; int32 column
+    non-temporal loads; small plans not spread over the chip, or every small
+    plan spread (bit 9, the round-2 rule); int32 column
     indices only, no 16-bit offsets) gives the same
     bits as the canonical-order oracle, on matrices with short rows, rows
     just above the 256 threshold and chunked hub rows."""
