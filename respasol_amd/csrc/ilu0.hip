@@ -197,17 +197,23 @@ __device__ __forceinline__ void lds_barrier() {
 // Wait until the LDS counter *p >= want (wave-uniform value; bounded: a plan
 // bug gives wrong bits in the tests, never a hung GPU). RSP_POLL_MODE (A/B):
 // 0 (shipped) = read -> wait -> compare; 1 = two reads in flight, each step
-// waiting for the older one only; 2 = s_sleep(RSP_POLL_SLEEP) between reads.
-// Config 3, same box, interleaved x2: fp64 factor / solve 58.6-58.8 /
+// waiting for the older one only; 2 = s_sleep(RSP_POLL_SLEEP) between reads;
+// 3 = s_sleep only while the counter is below `near` (the wave is not next in
+// line). Config 3, same box, interleaved x2: fp64 factor / solve 58.5-58.8 /
 // 43.5-43.7 ms (mode 0), 59.6-59.7 / 46.7 (mode 1), 59.8 / 45.8 (mode 2,
-// sleep 1), 60.2 / 47.3 (sleep 2).
+// sleep 1), 60.2 / 47.3 (sleep 2), 59.0 / 47.3 (mode 3, sleep 1; dc1 solve
+// 4.88 -> 6.23 ms), 58.9 / 48.8 (sleep 3). Also measured slower: reading the
+// counter and the level's y values together in every poll, so a level pays
+// one LDS round trip after its producer instead of two (solve 43.5 -> 45.4
+// ms; dc1 4.86 -> 5.62). A narrow level is ~425 cycles (160 ns, dc1,
+// RSP_ILU_TRACE_CLK) and any extra LDS traffic or wake-up delay lands on it.
 #ifndef RSP_POLL_MODE
 #define RSP_POLL_MODE 0
 #endif
 #ifndef RSP_POLL_SLEEP
 #define RSP_POLL_SLEEP 1
 #endif
-__device__ __forceinline__ void lds_wait_geq(int *p, int want) {
+__device__ __forceinline__ void lds_wait_geq(int *p, int want, int near) {
 #if RSP_POLL_MODE == 1
     const unsigned addr = (unsigned)(size_t)(__attribute__((address_space(3))) int *)p;
     int a, b;
@@ -219,6 +225,13 @@ __device__ __forceinline__ void lds_wait_geq(int *p, int want) {
         if (__builtin_amdgcn_readfirstlane(b) >= want) break;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#elif RSP_POLL_MODE == 3
+    for (int it = 0; it < (1 << 26); ++it) {
+        const int c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (c >= want) break;
+        if (c < near) __builtin_amdgcn_s_sleep(RSP_POLL_SLEEP);  // not next in line: poll less
+    }
 #else
     for (int it = 0; it < (1 << 26) && __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want;
          ++it) {
@@ -864,7 +877,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 if (m) return min(b + (int)__builtin_ctzll(m), qe);
             }
         };
-        int k = 0;
+        int k = 0, sp = q;  // sp: the previous level's first round
         for (int s0 = q; s0 < qe; ++k) {
             const int s1 = seg_end(s0);
             if (k % KW == w) {
@@ -875,7 +888,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 const ItemPre p1 = item_pre(b1 + min(lane, max(n1 - 1, 0)), cb);
                 const bool sh0 = !__ballot(lane < n0 && (p0.r.y >> 16) > 2);
                 const bool sh1 = !__ballot(lane < n1 && (p1.r.y >> 16) > 2);
-                if (s0 > q) lds_wait_geq(&lds_rdone, ch.r0 + s0);
+                if (s0 > q) lds_wait_geq(&lds_rdone, ch.r0 + s0, ch.r0 + sp);
                 if (lane < n0) item_post(b0 + lane, cb, p0, sh0);
                 wave_order();
                 if (has1) {
@@ -891,6 +904,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 if (lane == 0)
                     __hip_atomic_store(&lds_rdone, ch.r0 + s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+            sp = s0;
             s0 = s1;
         }
     };
@@ -1565,7 +1579,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 v2 = lval[gi];
             }
             const int L = ch.l0 + q;
-            if (L > L0) lds_wait_geq(&lds_done, L);
+            if (L > L0) lds_wait_geq(&lds_done, L, L - 1);
             T s = group_fma(R.x, v1, i1);
             if (two) {
                 s = group_fma(s, v2, i2);
