@@ -594,7 +594,7 @@ hvec<int> factor_thin_rows(const int *rp, const IluHostPlan &hp) {
 // piece is writing concurrently (never its own chunk or the one before) only
 // ever gets "not here" — the relaxed atomics make those reads well defined.
 // The staged positions of the current chunk sit in a piece-private hash.
-static constexpr int kRndPieceItems = 1 << 17;
+static constexpr int kRndPieceItems = 1 << 16;  // A/B (scripts/piece_ab.sh): 2^17 / 2^16 / 2^15 gave factor 58.58 / 58.58 / 58.73 ms, circuits plan faster with smaller pieces
 
 static void build_factor_plan(int n, const int *rp, const int *ci,
                               const hvec<int> &dpos, const hvec<int> &hasdiag,
