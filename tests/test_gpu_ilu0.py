@@ -346,6 +346,33 @@ def test_device_analysis_same_plan_as_host(handle, monkeypatch, name, scale):
     il.close()
 
 
+@pytest.mark.parametrize("knobs", [{"RSP_ILU_THIN_SOLVE": "0"}, {"RSP_ILU_THIN_SOLVE": "1"},
+                                   {"RSP_ILU_GROUP": "2"}, {"RSP_ILU_FAT_PAD": "0"},
+                                   {"RSP_ILU_THIN_TERMS": "64"}])
+@pytest.mark.parametrize("name,scale", [("dc1", 0.3), ("stomach", 0.05), ("ecology2", 0.05)])
+def test_device_solve_terms_same_plan_under_schedule_knobs(handle, monkeypatch, knobs, name, scale):
+    """The device-built per-term solve plan equals the host's whatever the
+    segment structure: every level fat, single-row thin levels, term groups
+    of 2, unpadded fat short rows, tiny thin chunks."""
+    import ctypes as C
+    from respasol_amd._lib import rsp
+    monkeypatch.setenv("RSP_ILU_DIGEST", "1")
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    A = csr.surrogate(name, scale)
+    rp, ci, _ = upload_csr(A.rowptr, A.colidx, A.values)
+    il = Ilu0(handle, rp, ci)
+    il.analysis()
+    dev = C.c_uint64()
+    assert rsp.rsp_ilu0_plan_digest(il._info, C.byref(dev)) == 0
+    hst = C.c_uint64()
+    r = np.ascontiguousarray(A.rowptr, np.int32)
+    c = np.ascontiguousarray(A.colidx, np.int32)
+    assert rsp.rsp_ilu0_analysis_host(A.n, r.ctypes.data, c.ctypes.data, None, None, C.byref(hst), None) == 0
+    assert dev.value == hst.value
+    il.close()
+
+
 @pytest.mark.parametrize("waves", [1, 2, 3, 8])
 @pytest.mark.parametrize("name,scale", [("dc1", 1.0), ("G2_circuit", 0.5), ("thermomech_TK", 0.5)])
 def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, name, scale):
