@@ -1207,6 +1207,9 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
     });
     long long total = 0;
     hvec<int> slot_levels;
+    // RSP_ILU_SLOT_PAD: A/B knob, the padded size a level may take over its
+    // rows' own structure
+    const long long pad_ratio = std::max(1, env_int("RSP_ILU_SLOT_PAD", 2));
     for (int l = 0; l < nlev; l++) {
         const LevStat &st = ls[(size_t)l];
         if (!st.fat || st.rm == 0) continue;
@@ -1215,7 +1218,7 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
         const int qm = std::max(st.qm, 1);
         const int stride = (rsp::fac_pairs_at(st.rm) + 2 * qm + 3) & ~3;
         const long long cnt = lp[(size_t)l + 1] - lp[(size_t)l];
-        if (cnt * stride > 2 * st.own) continue;  // padding would dominate
+        if (cnt * stride > pad_ratio * st.own) continue;  // padding would dominate
         if (total + cnt * stride > slot_cap) continue;
         hp.fslev[(size_t)l] = rsp::FacSlotLevel{total, stride, st.rm, qm, 0};
         total += cnt * stride;
