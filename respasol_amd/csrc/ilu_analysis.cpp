@@ -1208,7 +1208,9 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
     long long total = 0;
     hvec<int> slot_levels;
     // RSP_ILU_SLOT_PAD: A/B knob, the padded size a level may take over its
-    // rows' own structure
+    // rows' own structure (2 / 4 / 16: config-3 fp64 factor 58.6 / 58.7 /
+    // 58.6 ms; the ~280 single fat levels per run left on the FacRow path
+    // are hub-row levels, not padding-dominated ones)
     const long long pad_ratio = std::max(1, env_int("RSP_ILU_SLOT_PAD", 2));
     for (int l = 0; l < nlev; l++) {
         const LevStat &st = ls[(size_t)l];
