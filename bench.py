@@ -137,63 +137,59 @@ def workload_names(w):
     return w.split(",")
 
 
-def host_cpu_facts():
-    """What the CPU baseline ran on: this process's CPU set (the box's share),
-    the machine's logical CPUs and the CPU model."""
-    model = None
+def host_cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"cpuset_cpus": len(os.sched_getaffinity(0)), "machine_logical_cpus": os.cpu_count(), "model": model}
+    return None
 
 
-def cpu_baseline(slices, seconds):
+def cpu_baseline(workload, seconds, threads=0):
     """The reference's CPU path (test_spmv.c's CSR SpMV, restated by the
     oracle as an OpenMP row-parallel loop) on the same matrices, two ways
-    (BASELINE.md §4):
-      B (value): all threads of this process's CPU set, steady-state mean,
-        repeated until `seconds` of CPU work;
-      A (method_a): the reference's own methodology - 4 threads
+    (BASELINE.md §4), each in a child process (tests/cpu_baseline_run.py) so
+    the OpenMP placement is set before the OpenMP runtime starts:
+      B (value): one thread per physical core of one socket of this
+        process's CPU set, OMP_PROC_BIND=close, capped by the CPU share the
+        job is given (OMP_NUM_THREADS; the GPU pool sets 16 per GPU box) or
+        --cpu-threads; steady-state mean over `seconds` of full passes;
+      A (method_a): the reference's own methodology - 4 threads on 4 cores
         (run_spmv.sh:45 OMP_NUM_THREADS=4 taskset -c 0-3), ONE cold call per
         matrix (test_spmv.c:165-183)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_bind as ob
-    xs = [csr.dlarnv(1, [0, 0, 0, 1], s.n)[0] for s in slices]
-    facts = host_cpu_facts()
-    threads_b = ob.lib.oracle_num_threads()
-    # method A first: 4 threads, one cold call per matrix
-    ob.lib.oracle_set_threads(4)
-    t_a, flops_a = 0.0, 0.0
-    for s, x in zip(slices, xs):
-        t0 = time.perf_counter()
-        ob.spmv(s.host[0], s.host[1], s.host[2], x, threads=True)
-        t_a += time.perf_counter() - t0
-        flops_a += 2.0 * s.nnz_local
-    ob.lib.oracle_set_threads(threads_b)
-    for s, x in zip(slices, xs):  # warm (page-in) pass
-        ob.spmv(s.host[0], s.host[1], s.host[2], x, threads=True)
-    flops, t0, passes = 0.0, time.perf_counter(), 0
-    while True:
-        for s, x in zip(slices, xs):
-            ob.spmv(s.host[0], s.host[1], s.host[2], x, threads=True)
-            flops += 2.0 * s.nnz_local
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(flops / el / 1e9, 3), "unit": "GFLOP/s", "cores": threads_b,
+    import subprocess
+    runner = os.path.join(ROOT, "tests", "cpu_baseline_run.py")
+
+    def run(*extra):
+        r = subprocess.run([sys.executable, runner, "--workload", workload, *extra],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    a = run("--method", "A")
+    b = run("--method", "B", "--seconds", str(seconds), *(["--threads", str(threads)] if threads else []))
+    pl = b["placement"]
+    cap = ("--cpu-threads" if threads else
+           f"OMP_NUM_THREADS={os.environ['OMP_NUM_THREADS']} (this job's CPU share)"
+           if os.environ.get("OMP_NUM_THREADS") else "none")
+    return {"value": round(b["gflops"], 3), "unit": "GFLOP/s", "cores": b["threads"],
             "kind": "port",
-            "sample": f"method B: {passes} full fp64 passes over the {len(slices)}-matrix workload "
-                      f"({el:.1f} s), OpenMP row-parallel CSR on {threads_b} threads "
-                      f"(= this process's CPU set of {facts['cpuset_cpus']} CPUs), x=dlarnv(1,{{0,0,0,1}})",
-            "host": facts,
-            "method_a": {"value": round(flops_a / t_a / 1e9, 3), "unit": "GFLOP/s", "threads": 4,
-                         "note": "the reference's methodology: OMP_NUM_THREADS=4, one cold call per matrix "
-                                 "(run_spmv.sh:45, test_spmv.c:165-183), summed over the workload"}}
+            "sample": f"method B: {b['passes']} full fp64 passes over the {workload} set ({b['seconds']:.1f} s), "
+                      f"OpenMP row-parallel CSR, {b['threads']} threads pinned one per physical core "
+                      f"(OMP_PROC_BIND=close) on socket {pl['socket']} of {pl['sockets_in_cpuset']} in a "
+                      f"CPU set of {pl['cpuset_cpus']} logical CPUs ({pl['physical_cores_socket']} physical "
+                      f"cores on that socket; thread cap: {cap}), x=dlarnv(1,{{0,0,0,1}})",
+            "host": {"model": host_cpu_model(), "cpuset_cpus": pl["cpuset_cpus"],
+                     "sockets_in_cpuset": pl["sockets_in_cpuset"],
+                     "physical_cores_socket": pl["physical_cores_socket"], "threads": b["threads"],
+                     "places": pl["places"]},
+            "method_a": {"value": round(a["gflops"], 3), "unit": "GFLOP/s", "threads": a["threads"],
+                         "places": a["placement"]["places"],
+                         "note": "the reference's methodology: OMP_NUM_THREADS=4 on 4 physical cores, one cold "
+                                 "call per matrix (run_spmv.sh:45, test_spmv.c:165-183), summed over the set"}}
 
 
 def spmv_kernel_sha():
@@ -214,7 +210,7 @@ def spmv_kernel_sha():
     return hsh.hexdigest()[:16]
 
 
-def pmc_traffic(workload, batched):
+def pmc_traffic(workload, batched, dtype="f64"):
     """HBM bytes per dominant-kernel launch (the batched launch, or one
     per-matrix launch with --no-batch) from a committed rocprofv3 --pmc
     summary (profiles/*pmc*.json written by scripts/pmc_summary.py) recorded
@@ -227,7 +223,7 @@ def pmc_traffic(workload, batched):
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") != workload:
+        if d.get("workload") != workload or d.get("dtype", "f64") != dtype:
             continue
         seen.append(os.path.relpath(p, ROOT))
         if d.get("kernel_sha") != sha:
@@ -388,10 +384,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="big")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: physical cores of one socket, capped by "
+                         "OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--ramp-ms", type=float, default=200.0,
                     help="untimed clock ramp before the warm-up steps (ms of repeated steps)")
-    ap.add_argument("--fp32-reps", type=int, default=10)
+    ap.add_argument("--fp32-reps", type=int, default=20)
     ap.add_argument("--exchange", default="halo", choices=["halo", "allgather"],
                     help="N>1 x exchange: halo-only all_to_all (default) or full all-gather")
     ap.add_argument("--no-bucket", action="store_true",
@@ -521,6 +520,34 @@ def main():
     fp32 = {"kernel_gflops_rank0": round(sum(2.0 * s.nnz_local for s in slices) / (ms32 * 1e6), 2),
             "kernel_gbps_rank0": round(bytes32 / (ms32 * 1e6), 1),
             "ms_per_pass_rank0": round(ms32, 4)}
+    # fp32 roofline of its dominant kernel (the fp32 batched launch; one
+    # launch per matrix with --no-batch), as the fp64 one below: algorithmic
+    # bytes (8 B per stored entry + 4(m+1) + 4 n + 4 m) per launch
+    # over the average launch duration from the event pair around the reps
+    per32 = per_step
+    avg32_ms = ms32 / per32
+    b32_launch = bytes32 / per32
+    if b32 is not None:
+        saved32 = 2 * b32.info()["entries_16bit"]
+    else:
+        saved32 = 2 * sum(s.mat32.plan_info()["entries_16bit"] for s in slices)
+    ach32 = b32_launch / (avg32_ms * 1e6)
+    moved32 = (bytes32 - saved32) / per32 / (avg32_ms * 1e6)
+    tr32, tr32_src = (pmc_traffic(args.workload, bool(batches), "f32") if world == 1
+                      else (None, {"file": None, "note": "PMC summaries are recorded at N = 1"}))
+    fp32["roofline"] = {
+        "bound": "hbm",
+        "kernel": ("rsp_k::spmv_tiles_batch<float,true,false,true>" if b32 is not None
+                   else "rsp_k::spmv_tiles<float,true,false>"),
+        "achieved": round(ach32, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(ach32 / HBM_PEAK_GBS, 4), "traffic": tr32, "traffic_source": tr32_src,
+        "avg_launch_us": round(avg32_ms * 1e3, 3), "bytes_per_launch_avg": int(b32_launch),
+        "index_bytes_saved_per_launch": int(saved32 / per32),
+        "entries_16bit_share_rank0": round(saved32 / 2 / max(1, sum(s.nnz_local for s in slices)), 4),
+        "moved_achieved": round(moved32, 1), "moved_frac": round(moved32 / HBM_PEAK_GBS, 4),
+        "launches": args.fp32_reps * per32,
+        "note": "fp32 companion of the fp64 roofline: same workload in fp32 (fp32 accumulation, "
+                "the reference's CUDA_R_32F SpMV); event pair on the kernels' stream around the reps"}
 
     # parity spot check of this rank's slice of the largest matrix vs the oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -562,7 +589,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(slices, args.cpu_seconds)
+        cpu = cpu_baseline(args.workload, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
         traffic, traffic_src = (pmc_traffic(args.workload, bool(batches)) if world == 1  # PMC run was N = 1

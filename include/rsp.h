@@ -166,6 +166,21 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t handle, int n, int nnz, const int *d
  * structurally missing (after analysis) or U(j,j) == 0 (after the numeric
  * factorisation); the smallest such j is reported. Otherwise SUCCESS, -1. */
 rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t handle, rsp_ilu0_info_t info, int *position);
+/* Also RSP_STATUS_EXECUTION_FAILED after a factor whose persistent (flow)
+ * launch gave up a dependency wait (bounded by RSP_ILU_FLOW_TIMEOUT_US,
+ * default 0.2 s; never expected): its values are wrong. Reported for the
+ * LAST factor call only (each call starts clean). */
+
+/* cusparseXcsrsv2_zeroPivot (the csrsv2 infos of GPU/ilu0.cu:143-150) for
+ * the solves below; which = RSP_TRSV_L (op N), RSP_TRSV_LT (op T) or
+ * RSP_TRSV_U (rsp_trsv_upper). Host-blocking. Reports on the LAST solve of
+ * that kind: RSP_STATUS_EXECUTION_FAILED if its flow launch gave up a wait
+ * (its y is wrong); for RSP_TRSV_U, ZERO_PIVOT + *position as
+ * rsp_ilu0_zero_pivot (U divides by u_jj); else SUCCESS, -1. */
+#define RSP_TRSV_L 0
+#define RSP_TRSV_LT 1
+#define RSP_TRSV_U 2
+rsp_status_t rsp_trsv_zero_pivot(rsp_handle_t handle, rsp_ilu0_info_t info, int which, int *position);
 
 /* cusparse?csrilu02 (GPU/ilu0.cu:264-268): in-place ILU(0) on the CSR
  * pattern, IKJ order: for each row i, for each k < i in the pattern

@@ -99,6 +99,7 @@ RSP_PROTOS = {
     "rsp_ilu0_buffer_size": (i32, [vp, i32, i32, i32, vp, C.POINTER(C.c_size_t)]),
     "rsp_ilu0_analysis": (i32, [vp, i32, i32, vp, vp, vp]),
     "rsp_ilu0_zero_pivot": (i32, [vp, vp, ip]),
+    "rsp_trsv_zero_pivot": (i32, [vp, vp, i32, ip]),
     "rsp_ilu0_factor": (i32, [vp, vp, i32, vp]),
     "rsp_trsv_lower_unit": (i32, [vp, i32, vp, vp, i32, vp, vp, vp]),
     "rsp_trsv_upper": (i32, [vp, vp, vp, i32, vp, vp, vp]),
@@ -143,7 +144,7 @@ HOST_PROTOS = {
 }
 
 
-def _load(name: str, protos: dict, path: str | None = None) -> C.CDLL:
+def _load(name: str, protos: dict, path: str | None = None, probe: bool = False) -> C.CDLL:
     path = path or os.path.join(LIB_DIR, name)
     if not os.path.exists(path):
         raise ImportError(
@@ -151,6 +152,8 @@ def _load(name: str, protos: dict, path: str | None = None) -> C.CDLL:
             f"(python -c 'import __graft_entry__ as g; g.build()' or make -C respasol_amd/csrc)")
     lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
     for fname, (res, args) in protos.items():
+        if probe and not hasattr(lib, fname):  # an older diagnostic build (A/B runs)
+            continue
         fn = getattr(lib, fname)
         fn.restype = res
         fn.argtypes = args
@@ -160,7 +163,10 @@ def _load(name: str, protos: dict, path: str | None = None) -> C.CDLL:
 host = _load("librsp_host.so", HOST_PROTOS)
 # RSP_PROBE_LIB: a diagnostic build of librsp.so (scripts/spmv_probe.py only)
 _RSP_PATH = os.environ.get("RSP_PROBE_LIB") or os.path.join(LIB_DIR, "librsp.so")
-rsp = _load("librsp.so", RSP_PROTOS, _RSP_PATH)
+# RSP_HOST_ONLY=1: host library only (bench.py's CPU-baseline child process,
+# which must not load the HIP runtime); the device operators are then absent
+rsp = (None if os.environ.get("RSP_HOST_ONLY") == "1"
+       else _load("librsp.so", RSP_PROTOS, _RSP_PATH, probe=bool(os.environ.get("RSP_PROBE_LIB"))))
 
 
 def check(status: int, where: str) -> None:

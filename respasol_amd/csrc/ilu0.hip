@@ -368,7 +368,62 @@ struct FlowWord<float> {
     typedef unsigned int U;
     static constexpr U kNotYet = 0x7fa5eed1u;
 };
-constexpr unsigned long long kFlowTimeout = 20000000ull;  // wall-clock ticks (100 MHz): 0.2 s
+// A flow wait gives up after fc.ticks of the 100 MHz wall clock (default
+// 0.2 s, RSP_ILU_FLOW_TIMEOUT_US) and records the call's generation in
+// *fc.status (rsp::FlowCtl).
+__device__ __forceinline__ void flow_give_up(const rsp::FlowCtl &fc) {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(fc.status, fc.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Work-item claims of a flow launch (rsp::FlowCtl): lane 0 takes the next
+// item with an agent-scope fetch_add, issued one item ahead (its return is
+// read at the top of the next item, so the atomic's latency overlaps the
+// current item); flow_item() turns the claim into the item index.
+__device__ __forceinline__ unsigned long long flow_claim(const rsp::FlowCtl &fc) {
+    return (threadIdx.x & 63) == 0
+               ? __hip_atomic_fetch_add(fc.claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+               : 0ull;
+}
+__device__ __forceinline__ int flow_item(unsigned long long c, unsigned long long base, int it0, int it1) {
+    // the difference fits an int (claims of this launch); lane 0's is the one
+    const long long d = (long long)(c - base);
+    return __builtin_amdgcn_readfirstlane((int)min(d, (long long)(it1 - it0))) + it0;
+}
+
+// One wave's walk over the items [it0, it1) of a flow launch. Dynamic
+// (default): claims in start order, TWO items ahead — the claim for item
+// j + 2 is issued during item j, behind its first loads (claim_ahead), and
+// read when item j + 1 ends, so the atomic's latency hides under a whole
+// item. A wave makes 2 + (items it processes) claims, so a launch advances
+// the counter by exactly items + 2 W (flow_claims on the host). The lowest
+// unfinished item is always some running wave's CURRENT item (a wave's
+// claimed items are above its current one), so progress needs no
+// co-residency. Static (RSP_ILU_FLOW_MODE bit 0, A/B only): w, w + W, ...
+struct FlowClaims {
+    const rsp::FlowCtl &fc;
+    unsigned long long base, c1 = 0, c2 = 0;
+    int it0, it1, cur, stride;
+    bool dyn;
+    __device__ FlowClaims(const rsp::FlowCtl &f, unsigned long long b, int i0, int i1, int w, int W)
+        : fc(f), base(b), it0(i0), it1(i1), cur(i0 + w), stride(W), dyn(!(f.mode & rsp::kFlowStatic)) {}
+    __device__ int first() {
+        if (!dyn) return cur;
+        const unsigned long long c0 = flow_claim(fc);
+        c1 = flow_claim(fc);
+        return flow_item(c0, base, it0, it1);
+    }
+    __device__ void claim_ahead() {
+        __builtin_amdgcn_sched_barrier(0);
+        if (dyn) c2 = flow_claim(fc);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __device__ int next() {
+        if (!dyn) return cur += stride;
+        const int it = flow_item(c1, base, it0, it1);
+        c1 = c2;
+        return it;
+    }
+};
 
 template <typename T>
 __device__ __forceinline__ typename FlowWord<T>::U flow_load(const T *p) {
@@ -385,7 +440,7 @@ __device__ __forceinline__ void flow_store(T *p, T v) {
 // max_sleep s_sleep units of 64 clocks).
 template <typename T, int NB>
 __device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], const int (&id)[NB], int n,
-                                          const T *y, int *timeouts, int max_sleep) {
+                                          const T *y, const rsp::FlowCtl &fc, int max_sleep) {
     constexpr auto kNot = FlowWord<T>::kNotYet;
     auto pending = [&] {
         bool p = false;
@@ -401,8 +456,8 @@ __device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], cons
         for (int b = 0; b < NB; ++b)
             if (b < n && w[b] == kNot) w[b] = flow_load(y + id[b]);
         if (!__ballot(pending())) return;
-        if (wall_clock64() - t0 > kFlowTimeout) {
-            if ((threadIdx.x & 63) == 0) atomicAdd(timeouts, 1);
+        if (wall_clock64() - t0 > fc.ticks) {
+            flow_give_up(fc);
             return;
         }
     }
@@ -416,12 +471,12 @@ __device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], cons
 // 8 per lane, slowed the loads on the critical path). Row g's item has a
 // lower index, so the gate cannot deadlock.
 template <typename T>
-__device__ __forceinline__ void flow_gate(int g, const T *y, int *timeouts, int max_sleep) {
+__device__ __forceinline__ void flow_gate(int g, const T *y, const rsp::FlowCtl &fc, int max_sleep) {
     if (g < 0) return;
     typename FlowWord<T>::U w[1] = {0};
     int id[1] = {g};
     if ((threadIdx.x & 63) == 0) w[0] = flow_load(y + g);
-    flow_wait<T, 1>(w, id, (threadIdx.x & 63) == 0 ? 1 : 0, y, timeouts, max_sleep);
+    flow_wait<T, 1>(w, id, (threadIdx.x & 63) == 0 ? 1 : 0, y, fc, max_sleep);
 }
 
 // Fat level in the slot layout (rsp::FacSlotLevel): the row's structure is
@@ -495,73 +550,104 @@ __global__ __launch_bounds__(64) void ilu0_level_slot(IluArgs a, const int *__re
     for (int x = lane; x < nr; x += 64) vals[rs + x] = rv[x];
 }
 
-// Poll the per-row done flags of this lane's wanted rows (need[b]) until each
-// reads gen (wave-uniform loop, bounded like flow_wait).
-template <int NB>
-__device__ __forceinline__ void flag_wait(const int (&row)[NB], const bool (&need)[NB], const int *fdone, int gen,
-                                          int *timeouts, int max_sleep) {
-    bool miss[NB];
-    bool any = false;
+// Re-read this lane's operand words that are still kNotYet (need[b] set)
+// until none of the wave's is (wave-uniform loop, bounded like flow_wait).
+template <typename T, int NB>
+__device__ __forceinline__ void tagged_wait(typename FlowWord<T>::U (&w)[NB], const int (&pos)[NB],
+                                            const bool (&need)[NB], const T *vals, const rsp::FlowCtl &fc,
+                                            int max_sleep) {
+    constexpr auto kNot = FlowWord<T>::kNotYet;
+    auto pending = [&] {
+        bool p = false;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        miss[b] = need[b] && __hip_atomic_load((int *)fdone + row[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen;
-        any |= miss[b];
-    }
-    if (!__ballot(any)) return;
+        for (int b = 0; b < NB; ++b) p |= need[b] && w[b] == kNot;
+        return p;
+    };
+    if (!__ballot(pending())) return;
     const unsigned long long t0 = wall_clock64();
     for (int sl = 1;; sl = min(2 * sl, max_sleep)) {
         for (int q = 0; q < sl; ++q) __builtin_amdgcn_s_sleep(1);
-        any = false;
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            if (miss[b])
-                miss[b] = __hip_atomic_load((int *)fdone + row[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen;
-            any |= miss[b];
-        }
-        if (!__ballot(any)) return;
-        if (wall_clock64() - t0 > kFlowTimeout) {
-            if ((threadIdx.x & 63) == 0) atomicAdd(timeouts, 1);
+        for (int b = 0; b < NB; ++b)
+            if (need[b] && w[b] == kNot) w[b] = flow_load(vals + pos[b]);
+        if (!__ballot(pending())) return;
+        if (wall_clock64() - t0 > fc.ticks) {
+            flow_give_up(fc);
             return;
         }
     }
 }
 
+// A finished factor value as it is published: a value whose bits are the
+// kNotYet pattern (only an untouched input can be: arithmetic never makes a
+// signalling NaN) is published as the quiet NaN of the same payload.
+template <typename T>
+__device__ __forceinline__ T flow_publishable(T v) {
+    typedef typename FlowWord<T>::U U;
+    constexpr U kQuiet = sizeof(T) == 8 ? (U)0x0008000000000000ull : (U)0x00400000u;
+    const U b = __builtin_bit_cast(U, v);
+    return b == FlowWord<T>::kNotYet ? __builtin_bit_cast(T, (U)(b | kQuiet)) : v;
+}
+
+// Before a factor call's flow runs (one launch over all their items): each
+// flow row's upper part (diagonal included) — the values its consumers read
+// as u_kk and u_kj — is saved to forig and replaced by kNotYet in vals, so
+// that vals itself tells a consumer whether an operand is final (the
+// data-tagged hand-off trsv_flow uses for y). A wave per item.
+template <typename T>
+__global__ __launch_bounds__(256) void ilu0_flow_prep(IluArgs a, int nitems) {
+    const int lane = threadIdx.x & 63;
+    const int it = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (it >= nitems) return;
+    const int *slot = a.fslots + a.fitems[it].off;
+    const int rs = slot[1], nlo = slot[2], nr = slot[3];
+    T *vals = (T *)a.vals, *orig = (T *)a.forig;
+    typedef typename FlowWord<T>::U U;
+    for (int x = nlo + lane; x < nr; x += 64) {
+        orig[rs + x] = vals[rs + x];
+        reinterpret_cast<U *>(vals)[rs + x] = FlowWord<T>::kNotYet;
+    }
+}
+
 // Flow run of the factor (rsp::FacFlowRun): ONE launch of a.flow_grid
 // workgroups over the run's rows in level order instead of a launch per fat
-// level. Wave w takes items w, w + W, ... (W = the grid's waves); a row waits
-// for the rows it reads — the columns k of its lower entries, whose u_kk and
-// u_kj are its operands — only where those rows are inside this run (level >=
-// lb; earlier rows finished in earlier launches), by their done flags: the
-// producing wave stores its row's values device-scope (sc1, write-through),
-// waits for them (s_waitcnt vmcnt(0)), then stores its flag = this call's
-// generation (sc1); the consumer polls the flags with sc1 loads and only then
-// reads the operands with sc1 loads (MI355X_MICROARCH.md, the valid hand-off
-// form: one signalling wave per storing wave, every load of the handed-off
-// bytes sc1, one workgroup per CU). A gate row three levels back is awaited
-// first (one word) so that waves far ahead of the front poll little. Flags
-// carry the call's generation, so nothing is reset between calls.
-// Deadlock-free as trsv_flow (items wait for lower items only; the grid is
-// resident); a wait past kFlowTimeout gives up and counts in flow_timeouts.
-// Structure and arithmetic as ilu0_level_slot (the level's rm / qm at run
-// time, budgets KR / KQ at their maximum): the same bits.
+// level. Waves claim items in order from the flow counter (rsp::FlowCtl),
+// two items ahead. The hand-off is DATA-TAGGED, as trsv_flow's: the rows of
+// flow runs start the call with their upper values (the u_kk and u_kj other
+// rows read) set to kNotYet by ilu0_flow_prep (originals in forig); a row
+// reads its operands (divisors and update-pair values) straight from vals
+// with agent-scope atomic loads and re-reads those still kNotYet; the
+// producer publishes each final value with one agent-scope atomic store.
+// Every hand-off is a single location written once by an atomic and read by
+// atomics (coherence alone orders it under the HIP memory model): no flag,
+// no fence, no dependency lookup. Operands of rows outside flow runs are
+// final in vals (earlier kernels) and never kNotYet. A gate row three levels
+// back is polled first (lane 0, its first upper value) so that waves far
+// ahead of the front poll one word. Deadlock-free as trsv_flow (an item
+// waits for lower items only, and every lower item is held by a running
+// wave); a wait past fc.ticks gives up (rsp::FlowCtl). Structure and
+// arithmetic as ilu0_level_slot (the level's rm / qm at run time, budgets
+// KR / KQ at their maximum): the same bits.
 template <typename T>
-__global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, int lb) {
+__global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, unsigned long long base) {
     constexpr int R = rsp::kFacRow, Q = rsp::kFacPairs, KR = R / 64, KQ = Q / 64;
+    typedef typename FlowWord<T>::U U;
     __shared__ T rv_[4][R], dv_[4][R], pu_[4][Q];
     __shared__ int up_[4][R + 1], lo_[4][R], le_[4][R];
     __shared__ unsigned short pl_[4][Q];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int W = gridDim.x * 4;
     T *rv = rv_[wv], *dv = dv_[wv], *pu = pu_[wv];
     int *up = up_[wv], *lo = lo_[wv], *le = le_[wv];
     unsigned short *pl = pl_[wv];
     T *vals = (T *)a.vals;
-    for (int it = it0 + blockIdx.x * 4 + wv; it < it1; it += W) {
+    const T *orig = (const T *)a.forig;
+    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4);
+    for (int it = fq.first(); it < it1; it = fq.next()) {
         const rsp::FacFlowItem f = a.fitems[it];
         const int *slot = a.fslots + f.off;
         const int rm = f.rmqm & 0xffff, qm = f.rmqm >> 16, pa = rsp::fac_pairs_at(rm);
-        int dpos_[KR], bw[KR], dep[KR];
+        int dpos_[KR], bw[KR];
         int2 pr[KQ];
 #pragma unroll
         for (int k = 0; k < KR; ++k)
@@ -574,43 +660,52 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, in
         for (int k = 0; k < KQ; ++k)
             if (64 * k < qm) pr[k] = *reinterpret_cast<const int2 *>(slot + pa + 2 * min(lane + 64 * k, qm - 1));
         const int i = slot[0], rs = slot[1], nlo = slot[2], nr = slot[3], nq = slot[4], hasdiag = slot[5];
-        // the rows this row reads, and whether each is inside the run
-        bool need[KR];
-#pragma unroll
-        for (int k = 0; k < KR; ++k) {
-            const int x = lane + 64 * k;
-            dep[k] = x < nlo ? a.colidx[rs + x] : 0;
+        int gp = -1, ge = -1;  // the gate row's first upper position and its row end
+        if (f.gate >= 0 && lane == 0) {
+            gp = a.dpos[f.gate];
+            ge = a.rowptr[f.gate + 1];
         }
-#pragma unroll
-        for (int k = 0; k < KR; ++k) need[k] = lane + 64 * k < nlo && a.lev[dep[k]] >= lb;
+        fq.claim_ahead();  // behind this item's structure loads
+        // the row's own a_ij: lower part from vals, upper part from forig
+        // (its vals entries hold kNotYet until this row publishes them)
         T av[KR];
 #pragma unroll
         for (int k = 0; k < KR; ++k)
-            if (64 * k < rm) av[k] = vals[rs + min(lane + 64 * k, max(nr - 1, 0))];  // the row's own a_ij
-        if (f.gate >= 0) {
-            int g[1] = {f.gate};
-            bool gn[1] = {lane == 0};
-            flag_wait<1>(g, gn, a.fdone, a.gen, a.flow_timeouts, a.flow_sleep);
-        }
-        flag_wait<KR>(dep, need, a.fdone, a.gen, a.flow_timeouts, a.flow_sleep);
-        T dd[KR], uv[KQ];
-#pragma unroll
-        for (int k = 0; k < KR; ++k)
             if (64 * k < rm) {
-                typedef typename FlowWord<T>::U U;
-                const U b = flow_load(vals + max(dpos_[k], 0));
-                dd[k] = __builtin_bit_cast(T, b);
+                const int x = min(lane + 64 * k, max(nr - 1, 0));
+                av[k] = x < nlo ? vals[rs + x] : orig[rs + x];
             }
+        if (lane == 0 && gp >= 0 && gp < ge) {
+            U gw[1] = {flow_load(vals + gp)};
+            const int gpos[1] = {gp};
+            const bool gn[1] = {true};
+            tagged_wait<T, 1>(gw, gpos, gn, vals, a.fc, a.flow_sleep);
+        }
+        // operands: divisors u_kk of the lower entries, u_kj of the update pairs
+        U dw[KR], uw[KQ];
+        int dp[KR], upos[KQ];
+        bool dn[KR], un[KQ];
 #pragma unroll
-        for (int k = 0; k < KQ; ++k)
-            if (64 * k < qm) uv[k] = __builtin_bit_cast(T, flow_load(vals + pr[k].x));
+        for (int k = 0; k < KR; ++k) {
+            dn[k] = 64 * k < rm && lane + 64 * k < nlo && dpos_[k] >= 0;
+            dp[k] = 64 * k < rm ? max(dpos_[k], 0) : 0;
+            dw[k] = 64 * k < rm ? flow_load(vals + dp[k]) : U(0);
+        }
+#pragma unroll
+        for (int k = 0; k < KQ; ++k) {
+            un[k] = 64 * k < qm && lane + 64 * k < nq;
+            upos[k] = 64 * k < qm ? pr[k].x : 0;
+            uw[k] = 64 * k < qm ? flow_load(vals + upos[k]) : U(0);
+        }
+        tagged_wait<T, KR>(dw, dp, dn, vals, a.fc, a.flow_sleep);
+        tagged_wait<T, KQ>(uw, upos, un, vals, a.fc, a.flow_sleep);
         if (nr > 0) {
 #pragma unroll
             for (int k = 0; k < KR; ++k) {
                 const int x = lane + 64 * k;
                 if (64 * k < rm && x < nr) {
                     rv[x] = av[k];
-                    dv[x] = dpos_[k] >= 0 ? dd[k] : T(0);
+                    dv[x] = dpos_[k] >= 0 ? __builtin_bit_cast(T, dw[k]) : T(0);
                     up[x] = bw[k] & 0x7ff;
                     lo[x] = (bw[k] >> 11) & 0x1ff;
                     le[x] = (bw[k] >> 20) & 0x1ff;
@@ -622,14 +717,12 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, in
                 const int u = lane + 64 * k;
                 if (64 * k < qm && u < nq) {
                     pl[u] = (unsigned short)pr[k].y;
-                    pu[u] = uv[k];
+                    pu[u] = __builtin_bit_cast(T, uw[k]);
                 }
             }
             row_lds_factor<T>(rv, dv, pu, up, lo, le, pl, nlo, nr, lane, hasdiag, i, a.zero_pivot);
-            for (int x = lane; x < nr; x += 64) flow_store(vals + rs + x, rv[x]);
+            for (int x = lane; x < nr; x += 64) flow_store(vals + rs + x, flow_publishable(rv[x]));
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the row's stores performed before its flag
-        if (lane == 0) __hip_atomic_store(a.fdone + i, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1123,9 +1216,9 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
 }
 
 // Flow segments (a solve DAG's runs of two or more fat levels): ONE launch of
-// a.flow_grid workgroups instead of a launch per level. Wave w of the grid
-// takes the segment's work items (rsp::FlowItem, level order) w, w + W, ...
-// (W = the grid's waves); an item starts as soon as the y values it reads
+// a.flow_grid workgroups instead of a launch per level. The waves claim the
+// segment's work items (rsp::FlowItem, level order) in order from the flow
+// counter (rsp::FlowCtl); an item starts as soon as the y values it reads
 // exist, not when its whole previous level has ended. Existence is read from
 // the value itself: trsv_stream sets every y to kNotYet, a signalling-NaN
 // bit pattern that no y can have (every y is an arithmetic result — alpha x_i,
@@ -1134,21 +1227,21 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
 // reads its operands with device-scope (sc1) loads, re-reading (after an
 // s_sleep) those still kNotYet: the data-tagged hand-off of the price list
 // in MI355X_MICROARCH.md (handoff-1to1) — no flag, no fence.
-// Deadlock-free: an item waits only for items of lower index, each wave runs
-// its items in index order, and the grid (one 4-wave workgroup per CU by
-// default) is resident at once, so the lowest unfinished item always makes
-// progress. A wait beyond kFlowTimeout (never expected) gives up and counts
-// in a.flow_timeouts (rsp_ilu0_zero_pivot then returns EXECUTION_FAILED)
-// instead of hanging the GPU.
+// Deadlock-free without any co-residency assumption: an item waits only for
+// items of lower index; items are claimed in index order by waves that are
+// running, and a wave's claimed next item is higher than its current one, so
+// the lowest unfinished item is some running wave's current item, whose
+// operands are all done. A wait beyond fc.ticks (never expected) gives up and
+// records the call in *fc.status (rsp_trsv_zero_pivot then returns
+// EXECUTION_FAILED) instead of hanging the GPU.
 // Same terms, same order, same fma chain as trsv_level: the same bits.
 template <typename T, int KIND>
-__global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1) {
+__global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, unsigned long long base) {
     typedef typename FlowWord<T>::U U;
     constexpr int F = rsp::kFatLongTerms;
     __shared__ T fwv[4][64], fwy[4][64];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int W = gridDim.x * 4;
     const T *sval = (const T *)a.sval, *sx = (const T *)a.sx;
     T *y = (T *)a.y;
     const int *src = a.plan.src;
@@ -1157,7 +1250,9 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     };
-    for (int it = it0 + blockIdx.x * 4 + wv; it < it1; it += W) {
+    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4);
+    // claims are issued behind each item's first loads (task, term values and sources)
+    for (int it = fq.first(); it < it1; it = fq.next()) {
         const rsp::FlowItem f = a.plan.fitems[it];
         if (f.n > 0) {  // short rows, a lane each (lanes past them repeat the last row)
             const int r = min(lane, f.n - 1), x = f.x0 + r;
@@ -1183,11 +1278,12 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1) {
                 }
             }
             T s = sx[x];
-            flow_gate<T>(f.gate, y, a.flow_timeouts, a.flow_sleep);
+            fq.claim_ahead();
+            flow_gate<T>(f.gate, y, a.fc, a.flow_sleep);
             U w[F];
 #pragma unroll
             for (int b = 0; b < F; ++b) w[b] = b < n ? flow_load(y + id[b]) : U(0);
-            flow_wait<T, F>(w, id, n, y, a.flow_timeouts, a.flow_sleep);
+            flow_wait<T, F>(w, id, n, y, a.fc, a.flow_sleep);
 #pragma unroll
             for (int b = 0; b < F; ++b)
                 if (b < n) s = fma_t(-v[b], __builtin_bit_cast(T, w[b]), s);
@@ -1197,13 +1293,14 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1) {
             const int x = f.x0;
             const rsp::RowTask t = a.plan.tasks[x];
             T s = sx[x];
-            flow_gate<T>(f.gate, y, a.flow_timeouts, a.flow_sleep);
+            fq.claim_ahead();
+            flow_gate<T>(f.gate, y, a.fc, a.flow_sleep);
             for (int base = t.t0; base < t.t1; base += 64) {
                 const int k = min(base + lane, t.t1 - 1);
                 const T v = sval[k];
                 int id[1] = {src[k]};
                 U w[1] = {flow_load(y + id[0])};
-                flow_wait<T, 1>(w, id, 1, y, a.flow_timeouts, a.flow_sleep);
+                flow_wait<T, 1>(w, id, 1, y, a.fc, a.flow_sleep);
                 fwv[wv][lane] = v;
                 fwy[wv][lane] = __builtin_bit_cast(T, w[0]);
                 wave_sync();
@@ -1696,10 +1793,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
 
 // --------------------------------------------------------------- launchers
 
-// Workgroups of a flow launch: every one must be resident at once (a wait is
-// for lower items only, so the lowest unfinished item must be running). The
-// occupancy query, less one workgroup per CU of margin (it can overstate by
-// one, MI355X_MICROARCH.md residency notes), caps the requested grid.
+// Workgroups of a flow launch. Items are claimed in order by running waves
+// (rsp::FlowCtl), so co-residency is not needed for progress; the occupancy
+// query (less one workgroup per CU of margin) still caps the grid so that
+// waves that cannot run yet do not sit in the dispatcher.
 template <auto KERNEL>
 static int flow_grid(int want, int cus, int items) {
     static int occ = 0;  // per kernel
@@ -1711,10 +1808,23 @@ static int flow_grid(int want, int cus, int items) {
     return max(1, min(min(want, cus * occ), (items + 3) / 4));
 }
 
+// A flow launch of `items` items on `grid` 4-wave workgroups: its claim base,
+// and the host mirror advanced by the claims it will make (rsp::FlowCtl).
+static unsigned long long flow_claims(const rsp::FlowCtl &fc, int items, int grid) {
+    const unsigned long long base = *fc.claim_host;
+    if (fc.mode & rsp::kFlowStatic) return base;  // (A/B knob: no claims)
+    *fc.claim_host = base + (unsigned long long)items + 2ull * 4ull * (unsigned long long)grid;
+    return base;
+}
+
 template <typename T, int B>
 static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
     const LevelPlan &P = a.plan;
     int fr = 0;  // next flow run (sorted by level)
+    if (a.flow && a.nfruns > 0) {  // the flow rows' upper values become kNotYet (ilu0_flow_prep)
+        const int nitems = a.fruns[a.nfruns - 1].c1;
+        hipLaunchKernelGGL((ilu0_flow_prep<T>), dim3((nitems + 3) / 4), dim3(256), 0, s, a, nitems);
+    }
     for (int g = 0; g < P.nseg; ++g) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
@@ -1726,7 +1836,8 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
             if (a.flow && fr < a.nfruns && a.fruns[fr].lb == l) {  // flow run: one persistent launch
                 const rsp::FacFlowRun r = a.fruns[fr];
                 const int grid = flow_grid<ilu0_flow<T>>(a.flow_grid, a.flow_cus, r.c1 - r.c0);
-                hipLaunchKernelGGL((ilu0_flow<T>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, r.lb);
+                const unsigned long long base = flow_claims(a.fc, r.c1 - r.c0, grid);
+                hipLaunchKernelGGL((ilu0_flow<T>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, base);
                 l = r.le - 1;
                 continue;
             }
@@ -1774,7 +1885,8 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
         }
         if (a.flow && sg.c1 > sg.c0) {  // flow segment: one persistent launch
             const int grid = flow_grid<trsv_flow<T, KIND>>(a.flow_grid, a.flow_cus, sg.c1 - sg.c0);
-            hipLaunchKernelGGL((trsv_flow<T, KIND>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1);
+            const unsigned long long base = flow_claims(a.fc, sg.c1 - sg.c0, grid);
+            hipLaunchKernelGGL((trsv_flow<T, KIND>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1, base);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

@@ -86,7 +86,12 @@ struct rsp_ilu0_info {
     int factored;
     int *d_dpos, *d_hasdiag;
     int *d_upd_ptr, *d_upd_l, *d_upd_u, *d_lord, *d_lend, *d_udiv;
+    // d_zero: [0] numerical zero pivot (atomicMin), [1] generation of the
+    // last factor call whose flow wait gave up, [2..4] the same for the L,
+    // L^T and U solves (rsp::FlowCtl), [6..7] the flow claim counter
     int *d_zero;
+    unsigned long long claim_host = 0;  // flow claims issued (rsp::FlowCtl)
+    int solve_gen[3] = {0, 0, 0};       // per solve kind: generation of the last call
     long long n_updates;
     // one level set per DAG: L (factor + L solve), L^T, U
     struct Dag {
@@ -116,8 +121,7 @@ struct rsp_ilu0_info {
     int *d_fslots = nullptr;                   // fat factor levels, slot layout (ilu0_level_slot)
     rsp_an::hvec<rsp::FacFlowRun> fruns;        // factor flow runs (ilu0_flow)
     rsp::FacFlowItem *d_ffitems = nullptr;
-    int *d_lev = nullptr;                      // L level of each row
-    int *d_fdone = nullptr;                    // per row: generation of the factor call that finished it
+    void *d_forig = nullptr;                   // flow rows' upper input values (ilu0_flow_prep), fp64-sized
     int fac_gen = 0;
     rsp_an::hvec<rsp::FacSlotLevel> fslev;      // per L level (stride 0: FacRow path)
     int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
@@ -998,7 +1002,7 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     f->fslev.clear();
     f->fruns.clear();
     f->d_ffitems = nullptr;
-    f->d_lev = f->d_fdone = nullptr;
+    f->d_forig = nullptr;
     f->d_frow = nullptr;
     f->d_rchunks = nullptr;
     f->d_ritems = nullptr;
@@ -1471,13 +1475,8 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     ar.up(&f->d_frow, hp->frow);
     ar.up(&f->d_ffitems, hp->ffitems);
     f->fruns = hp->fruns;
-    // the L level of each row (flow runs: which producers are inside the run;
-    // kept alive until the commit below copies it)
-    rsp_an::hvec<int> lev((size_t)std::max(n, 1), 0);
-    for (size_t l = 0; l + 1 < hp->L.ptr.size(); l++)
-        for (int x = hp->L.ptr[l]; x < hp->L.ptr[l + 1]; x++) lev[(size_t)hp->L.rows[(size_t)x]] = (int)l;
-    ar.up(&f->d_lev, lev);
-    ar.space((void **)&f->d_fdone, (size_t)std::max(n, 1) * sizeof(int));
+    // flow runs: the saved upper input values of their rows (ilu0_flow_prep)
+    if (!hp->fruns.empty()) ar.space(&f->d_forig, (size_t)std::max(hp->nnz_s, 1) * sizeof(double));
     rsp_k::SolveTermsArgs tl{}, tt{};
     if (dev_terms) {
         dag_upload_rows(ar, f->L, hp->L, n, tl);
@@ -1498,7 +1497,7 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     ar.space(&f->d_sval, nt * sizeof(double));
     ar.space(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
     ar.space(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
-    ar.space((void **)&f->d_zero, 2 * sizeof(int));  // zero pivot, flow time-outs
+    ar.space((void **)&f->d_zero, 8 * sizeof(int));  // zero pivot, flow give-ups, claim counter
     int4 *d_desc = nullptr;
     long long *d_offs = nullptr;
     if (!hp->slot_desc.empty()) {
@@ -1519,9 +1518,10 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         f->digest = e == hipSuccess && f->digest ? rsp_an::digest(*hp) : 0;
     }
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
-    if (e == hipSuccess) e = hipMemsetD32(f->d_zero + 1, 0, 1);
-    if (e == hipSuccess) e = hipMemsetD32(f->d_fdone, 0, (size_t)std::max(n, 1));
+    if (e == hipSuccess) e = hipMemsetD32(f->d_zero + 1, 0, 7);
     f->fac_gen = 0;
+    f->claim_host = 0;
+    f->solve_gen[0] = f->solve_gen[1] = f->solve_gen[2] = 0;
     // fat factor slots, written on the device from the uploaded symbolic
     // arrays; the layout is an optimisation: without its memory, or if the
     // build fails, the FacRow path factors every fat level (same bits)
@@ -1636,16 +1636,57 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
     *position = -1;
     if (!f->analysed) return RSP_STATUS_INVALID_VALUE;
     int pos = f->structural_zero;
-    int z[2] = {INT_MAX, 0};  // zero pivot, flow time-outs of earlier solves
+    int z[2] = {INT_MAX, 0};  // zero pivot, give-up generation of the factor calls
     RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
     RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
-    if (z[1] != 0) return RSP_STATUS_EXECUTION_FAILED;  // a flow solve gave up waiting: its y is wrong
+    // the last factor's flow wait gave up: its values are wrong
+    if (f->factored && f->fac_gen > 0 && z[1] == f->fac_gen) return RSP_STATUS_EXECUTION_FAILED;
     if (f->factored && z[0] != INT_MAX && (pos < 0 || z[0] < pos)) pos = z[0];
     if (pos >= 0) {
         *position = pos;
         return RSP_STATUS_ZERO_PIVOT;
     }
     return RSP_STATUS_SUCCESS;
+}
+
+// cusparseXcsrsv2_zeroPivot for the solves (reference: the csrsv2 info
+// objects of GPU/ilu0.cu:143-150). Host-blocking. EXECUTION_FAILED: the last
+// solve of that kind gave up a flow wait (its y is wrong; never expected, a
+// bound instead of a GPU hang). The unit-lower solves have no pivots; the U
+// solve (extension) reports the factor's zero pivot, which it divides by.
+rsp_status_t rsp_trsv_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int which, int *position) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!f || !position || which < RSP_TRSV_L || which > RSP_TRSV_U) return RSP_STATUS_INVALID_VALUE;
+    *position = -1;
+    if (!f->analysed) return RSP_STATUS_INVALID_VALUE;
+    int z[5];
+    RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
+    RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+    const int g = f->solve_gen[which];
+    if (g > 0 && z[2 + which] == g) return RSP_STATUS_EXECUTION_FAILED;
+    if (which == RSP_TRSV_U) {
+        int pos = f->structural_zero;
+        if (f->factored && z[0] != INT_MAX && (pos < 0 || z[0] < pos)) pos = z[0];
+        if (pos >= 0) {
+            *position = pos;
+            return RSP_STATUS_ZERO_PIVOT;
+        }
+    }
+    return RSP_STATUS_SUCCESS;
+}
+
+// Flow launch control of one call (rsp::FlowCtl): status word and generation,
+// give-up bound, the info's claim counter.
+static rsp::FlowCtl flow_ctl(rsp_ilu0_info *f, int word, int gen) {
+    rsp::FlowCtl c;
+    c.status = f->d_zero + word;
+    c.gen = gen;
+    const long long us = std::max(env_int("RSP_ILU_FLOW_TIMEOUT_US", 200000), 0);
+    c.ticks = (unsigned long long)us * 100ull;  // 100 MHz wall clock
+    c.claim = reinterpret_cast<unsigned long long *>(f->d_zero + 6);
+    c.claim_host = &f->claim_host;
+    c.mode = env_int("RSP_ILU_FLOW_MODE", 0);
+    return c;
 }
 
 static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const rsp_an::hvec<rsp::LevelSeg> &segs,
@@ -1713,10 +1754,10 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.fitems = f->d_ffitems;
     a.fruns = f->fruns.empty() ? nullptr : f->fruns.data();
     a.nfruns = a.fat_slots ? (int)f->fruns.size() : 0;
-    a.lev = f->d_lev;
-    a.fdone = f->d_fdone;
-    if (f->fac_gen >= (1 << 30)) {  // generations wrap: clear the flags
-        RSP_CHECK_HIP(hipMemsetD32Async(f->d_fdone, 0, (size_t)std::max(f->n, 1), h->stream));
+    a.lev = nullptr;
+    a.forig = f->d_forig;
+    if (f->fac_gen >= (1 << 30)) {  // generations wrap
+        RSP_CHECK_HIP(hipMemsetD32Async(f->d_zero + 1, 0, 1, h->stream));  // no stale give-up
         f->fac_gen = 0;
     }
     a.gen = ++f->fac_gen;
@@ -1724,7 +1765,7 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
     a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 4), 4), 16) / 4;
     a.flow_cus = h->num_cus;
     a.flow_sleep = std::min(std::max(env_int("RSP_ILU_FLOW_SLEEP", 1), 1), 64);
-    a.flow_timeouts = f->d_zero + 1;
+    a.fc = flow_ctl(f, 1, a.gen);
     // diagnostics: RSP_ILU_FTRACE=<file> appends per-chunk shader-clock stamps
     // of the thin factor runs (host-blocking; never set in timed runs)
     const char *trace_file = getenv("RSP_ILU_FTRACE");
@@ -1788,9 +1829,19 @@ static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alp
     // order): 256-thread workgroups, RSP_ILU_FLOW_WPC (default 4) waves per CU
     a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 4), 4), 16) / 4;
     a.flow_cus = h->num_cus;
-    a.flow_timeouts = f->d_zero + 1;
     a.flow_sleep = std::min(std::max(env_int("RSP_ILU_FLOW_SLEEP", 1), 1), 64);
     return a;
+}
+
+// A solve call of kind `which` (RSP_TRSV_*): its generation (status word
+// 2 + which; generations restart with the factor's wrap-around below 2^30).
+static void trsv_begin(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp::TrsvArgs &a) {
+    int &g = f->solve_gen[which];
+    if (g >= (1 << 30)) {  // wrap: no stale give-up may match a new generation
+        (void)hipMemsetD32Async(f->d_zero + 2 + which, 0, 1, h->stream);
+        g = 0;
+    }
+    a.fc = flow_ctl(f, 2 + which, ++g);
 }
 
 rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void *alpha,
@@ -1815,6 +1866,8 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
     }
     hipError_t e;
     const bool f64 = value_type == RSP_R_64F, ftz = h->ftz != 0;
+    if (op != RSP_OPERATION_NON_TRANSPOSE && op != RSP_OPERATION_TRANSPOSE) return RSP_STATUS_INVALID_VALUE;
+    trsv_begin(h, f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, a);
     if (op == RSP_OPERATION_NON_TRANSPOSE) {
         e = f64 ? rsp_k::trsv_lower_n_f64(a, h->stream)
                 : (ftz ? rsp_k_ftz::trsv_lower_n_f32(a, h->stream) : rsp_k::trsv_lower_n_f32(a, h->stream));
@@ -1858,6 +1911,7 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
     a.plan = level_plan(f->U, f->U.segs, f->U.batch);
     a.sval = f->d_usval;
+    trsv_begin(h, f, RSP_TRSV_U, a);
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::trsv_upper_f64(a, h->stream);

@@ -268,6 +268,28 @@ struct FacFlowRun {
     int lb, le, c0, c1;
 };
 
+// Flow launches (ilu0_flow, trsv_flow): every wave CLAIMS its work items
+// from one device counter in the order waves actually run (agent-scope
+// fetch_add), so an item that is waited on is always held by a running wave:
+// progress needs no co-residency of the grid. The counter is never reset: a
+// launch over items [it0, it1) with W waves advances it by exactly
+// (it1 - it0) + W (every wave stops after its first claim past it1), which
+// the launcher adds to the host mirror, so the next launch knows its base.
+// A wait longer than `ticks` (100 MHz wall clock) gives up — never expected;
+// a bound instead of a hang — and stores `gen` (the call's generation) into
+// *status, which rsp_ilu0_zero_pivot / rsp_trsv_zero_pivot compare with the
+// generation of the call they report on.
+struct FlowCtl {
+    int *status;                      // device word: generation of the last call that gave up
+    int gen;                          // this call's generation (>= 1)
+    unsigned long long ticks;         // give-up bound (RSP_ILU_FLOW_TIMEOUT_US)
+    unsigned long long *claim;        // device claim counter
+    unsigned long long *claim_host;   // host: claims issued by the launches enqueued so far
+    int mode;                         // A/B knob (RSP_ILU_FLOW_MODE): kFlowStatic
+};
+constexpr int kFlowStatic = 1;   // items w, w + W, ... per wave (needs a co-resident grid; round 3)
+
+
 struct IluArgs {
     int n;
     const int *rowptr;
@@ -308,11 +330,11 @@ struct IluArgs {
     const FacFlowRun *fruns;    // host
     int nfruns;
     const int *lev;             // device: L level of each row
-    int *fdone;                 // device: per row, the generation of the factor that finished it
+    void *forig;                // device: flow rows' upper input values (ilu0_flow_prep), nnz_s T
     int gen;                    // this factor call's generation (>= 1)
     int flow, flow_grid, flow_sleep;
-    int flow_cus;               // CUs of the device (residency cap of a flow grid)
-    int *flow_timeouts;
+    int flow_cus;               // CUs of the device (caps a flow grid)
+    FlowCtl fc;                 // flow launches: give-up status word, claim counter
 };
 
 struct TrsvArgs {
@@ -336,8 +358,8 @@ struct TrsvArgs {
     int narrow_waves;           // thin runs: waves sharing a narrow run, levels round-robin (RSP_ILU_NARROW_WAVES)
     int flow;                   // run flow segments persistently (RSP_ILU_FLOW, default 1)
     int flow_grid;              // flow launch: 256-thread workgroups (RSP_ILU_FLOW_WPC waves per CU)
-    int flow_cus;               // CUs of the device (residency cap of a flow grid)
-    int *flow_timeouts;         // device counter: flow waits that gave up (never expected)
+    int flow_cus;               // CUs of the device (caps a flow grid)
+    FlowCtl fc;                 // flow launches: give-up status word, claim counter
     int flow_sleep;             // flow polls: longest pause, s_sleep units (RSP_ILU_FLOW_SLEEP)
 };
 

@@ -126,9 +126,14 @@ int main(int argc, char **argv) {
     hipEventElapsedTime(&time_numeric, start, stop);
 
     int numerical_zero = -1;
-    if (rsp_ilu0_zero_pivot(handle, info, &numerical_zero) == RSP_STATUS_ZERO_PIVOT) {
+    rsp_status_t st = rsp_ilu0_zero_pivot(handle, info, &numerical_zero);
+    if (st == RSP_STATUS_ZERO_PIVOT) {
         printf("L(%d,%d) is zero\n", numerical_zero, numerical_zero);
         return 0;
+    }
+    if (st != RSP_STATUS_SUCCESS) {  /* e.g. EXECUTION_FAILED: the factor is not valid */
+        fprintf(stderr, "Error: ILU(0) factorisation failed (%s)\n", rsp_get_error_string(st));
+        return 1;
     }
 
     hipEventRecord(start, NULL);
@@ -141,6 +146,16 @@ int main(int argc, char **argv) {
     hipEventSynchronize(stop);
     float time_solve = 0.0f;
     hipEventElapsedTime(&time_solve, start, stop);
+    /* the solves' status (csrsv2_zeroPivot), outside the timed region */
+    const int kinds[2] = {RSP_TRSV_L, true_lu ? RSP_TRSV_U : RSP_TRSV_LT};
+    for (int q = 0; q < 2; q++) {
+        int pos = -1;
+        st = rsp_trsv_zero_pivot(handle, info, kinds[q], &pos);
+        if (st != RSP_STATUS_SUCCESS) {
+            fprintf(stderr, "Error: triangular solve %d failed (%s)\n", kinds[q], rsp_get_error_string(st));
+            return 1;
+        }
+    }
 
     printf(fp32 ? "SINGLE PRECISION SOLVE IN  MILLISECONDS\n " : "DOUBLE PRECISION SOLVE IN  MILLISECONDS\n ");
     printf("Symbolic = %f\n Numeric = %f \n Symbolic+ Numeric = %f\n Solve = %f\n", time_symbolic,

@@ -12,6 +12,7 @@ Mapping to the reference's cuSPARSE usage:
                          cuSPARSE counterpart; bits equal to SpMat.spmv each)
   Ilu0.analysis          csrilu02_analysis + 2x csrsv2_analysis (GPU/ilu0.cu:203-252)
   Ilu0.zero_pivot        cusparseXcsrilu02_zeroPivot         (GPU/ilu0.cu:222,278)
+  Ilu0.solve_zero_pivot  cusparseXcsrsv2_zeroPivot (the csrsv2 infos, GPU/ilu0.cu:143-150)
   Ilu0.factor            cusparse?csrilu02                   (GPU/ilu0.cu:264-268)
   Ilu0.solve_lower       cusparse?csrsv2_solve, desc_L, op N / op T (GPU/ilu0.cu:296-302)
 Errors raise RspError carrying the rsp_status_t (numbered like cusparseStatus_t).
@@ -235,6 +236,20 @@ class Ilu0:
         if st == _lib.STATUS_ZERO_PIVOT:
             return pos.value
         check(st, "rsp_ilu0_zero_pivot")
+        return -1
+
+    TRSV_L, TRSV_LT, TRSV_U = 0, 1, 2
+
+    def solve_zero_pivot(self, which: int) -> int:
+        """cusparseXcsrsv2_zeroPivot for the last solve of kind `which`
+        (TRSV_L / TRSV_LT / TRSV_U): -1 if none, else the 0-based row (U
+        only); raises RspError(EXECUTION_FAILED) if that solve's persistent
+        launch gave up a dependency wait."""
+        pos = C.c_int(-1)
+        st = rsp.rsp_trsv_zero_pivot(self.handle.ptr, self._info, which, C.byref(pos))
+        if st == _lib.STATUS_ZERO_PIVOT:
+            return pos.value
+        check(st, "rsp_trsv_zero_pivot")
         return -1
 
     def levels(self) -> tuple[int, int]:

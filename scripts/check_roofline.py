@@ -15,13 +15,15 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--stats", required=True)
 ap.add_argument("--bench", required=True)
 ap.add_argument("--kernel", default="spmv_tiles_batch<double")
+ap.add_argument("--fp32", action="store_true", help="check the line's fp32.roofline (kernel spmv_tiles_batch<float)")
 args = ap.parse_args()
 path = args.stats
 if os.path.isdir(path):
     path = glob.glob(os.path.join(path, "**", "*kernel_stats.csv"), recursive=True)[0]
-row = next(r for r in csv.DictReader(open(path)) if args.kernel in r["Name"])
+kernel = "spmv_tiles_batch<float" if args.fp32 else args.kernel
+row = next(r for r in csv.DictReader(open(path)) if kernel in r["Name"])
 b = json.loads(open(args.bench).read().strip().splitlines()[-1])
-rf = b["roofline"]
+rf = b["fp32"]["roofline"] if args.fp32 else b["roofline"]
 prof_us = float(row["AverageNs"]) / 1e3
 bytes_ = rf["bytes_per_launch_avg"]
 frac_prof = bytes_ / (prof_us * 1e3) / rf["peak"]

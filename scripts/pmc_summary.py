@@ -43,12 +43,16 @@ def main():
     ap.add_argument("--meta", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--workload", default="big")
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--commit", default=os.environ.get("RSP_COMMIT"),
                     help="git commit the profiled tree was taken from (the GPU box has no .git)")
     args = ap.parse_args()
     meta = json.load(open(args.meta))
-    fetch = load(args.fetch, "FETCH_SIZE")
-    write = load(args.write, "WRITE_SIZE")
+    if args.dtype == "f32":
+        meta = meta["f32"]
+    tn = "double" if args.dtype == "f64" else "float"
+    fetch = load(args.fetch, "FETCH_SIZE", f"spmv_tiles<{tn}")
+    write = load(args.write, "WRITE_SIZE", f"spmv_tiles<{tn}")
     nc = meta["calibration"]["launches"]
     nm = len(meta["matrices"])
     cal = meta["calibration"]
@@ -69,12 +73,12 @@ def main():
     steady = per[nm:] if launches > nm else per
     hbm = sum(p["hbm_bytes"] for p in steady) / len(steady)
     algb = sum(p["alg_bytes"] for p in steady) / len(steady)
-    per_matrix = {"kernel": "rsp_k::spmv_tiles<double,true,false>",
+    per_matrix = {"kernel": f"rsp_k::spmv_tiles<{tn},true,false>",
                   "hbm_bytes_per_launch": round(hbm), "algorithmic_bytes_per_launch": round(algb),
                   "traffic_over_algorithmic": round(hbm / algb, 4)}
     # batched launches (one per <= 32 matrices per pass): same correction
-    fb = load(args.fetch, "FETCH_SIZE", "spmv_tiles_batch<double")
-    wb = load(args.write, "WRITE_SIZE", "spmv_tiles_batch<double")
+    fb = load(args.fetch, "FETCH_SIZE", f"spmv_tiles_batch<{tn}")
+    wb = load(args.write, "WRITE_SIZE", f"spmv_tiles_batch<{tn}")
     batch = None
     nb = min(len(fb), len(wb))
     lpp = meta.get("batch_launches_per_pass", 1)
@@ -86,7 +90,7 @@ def main():
         if e16 is None:
             e16 = sum(m.get("entries_16bit", 0) for m in meta["matrices"])
         moved_b = alg_b - 2.0 * e16
-        batch = {"kernel": "rsp_k::spmv_tiles_batch<double,true,false,true>",
+        batch = {"kernel": f"rsp_k::spmv_tiles_batch<{tn},true,false,true>",
                  "hbm_bytes_per_launch": round(hbm_b), "algorithmic_bytes_per_launch": round(alg_b),
                  "traffic_over_algorithmic": round(hbm_b / alg_b, 4),
                  "moved_bytes_per_launch": round(moved_b), "traffic_over_moved": round(hbm_b / moved_b, 4),
@@ -96,6 +100,7 @@ def main():
     from bench import spmv_kernel_sha  # the build bench.py accepts this summary for
     out = {
         "workload": args.workload,
+        "dtype": args.dtype,
         "kernel_sha": spmv_kernel_sha(),
         "commit": args.commit,
         "kernel": top["kernel"],

@@ -7,7 +7,7 @@
 #      it) -> stats/ + bench_prof.json; scripts/check_roofline.py then checks
 #      that the rocprof average of spmv_tiles_batch<double> agrees with the
 #      line's avg_launch_us
-#   2. rocprofv3 --pmc FETCH_SIZE on scripts/pmc_run.py (own run)
+#   2. rocprofv3 --pmc FETCH_SIZE on scripts/pmc_run.py (own run; fp64 then fp32)
 #   3. rocprofv3 --pmc WRITE_SIZE on scripts/pmc_run.py (own run)
 #   4. scripts/pmc_summary.py -> <tag>_pmc.json stamped with the kernel
 #      source hash (bench.py refuses a summary of another build) and the
@@ -33,4 +33,7 @@ rc=$?; echo "write rc=$rc"; fatal $rc write
 cd "$ROOT"
 python3 scripts/pmc_summary.py --fetch "$OUT/fetch" --write "$OUT/write" --meta "$OUT/meta.json" \
     --out "$OUT/${TAG}_pmc.json"
+python3 scripts/pmc_summary.py --fetch "$OUT/fetch" --write "$OUT/write" --meta "$OUT/meta.json" \
+    --dtype f32 --out "$OUT/${TAG}_pmc_f32.json"
 python3 scripts/check_roofline.py --stats "$OUT/stats" --bench "$OUT/bench_prof.json" | tee "$OUT/roofline_check.txt"
+python3 scripts/check_roofline.py --fp32 --stats "$OUT/stats" --bench "$OUT/bench_prof.json" | tee -a "$OUT/roofline_check.txt"

@@ -44,7 +44,9 @@ def gpu_ilu(handle, A, dtype, ftz=False, x=None, true_lu=False):
     z = il.solve_lower(va, xx)
     y = il.solve_upper(va, z) if true_lu else il.solve_lower(va, z, transpose=True)
     torch.cuda.synchronize()
-    assert il.zero_pivot() == zp  # (raises if a flow solve gave up waiting)
+    assert il.zero_pivot() == zp  # (raises if the factor's flow launch gave up waiting)
+    assert il.solve_zero_pivot(il.TRSV_L) == -1  # (raise if a solve's flow launch gave up)
+    il.solve_zero_pivot(il.TRSV_U if true_lu else il.TRSV_LT)
     handle.set_ftz(False)
     return va.cpu().numpy(), zp, z.cpu().numpy(), y.cpu().numpy(), il
 
@@ -400,3 +402,45 @@ def test_flow_segments(handle, monkeypatch, flow, wpc, name, scale):
     x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
     compare(A, torch.float64, handle, x=x)
     compare(A, torch.float32, handle, x=x, true_lu=True)
+
+
+def test_flow_give_up_is_reported(handle, monkeypatch):
+    """A persistent (flow) launch whose dependency wait gives up is reported,
+    not silent: forced with a zero wait bound
+    (RSP_ILU_FLOW_TIMEOUT_US=0) and every level fat, so every level is in a
+    flow run. The factor's zero_pivot and the solves' status then raise
+    EXECUTION_FAILED; the next call with the normal bound starts clean,
+    reports SUCCESS and gives the oracle's bits."""
+    from respasol_amd._lib import STATUS_EXECUTION_FAILED, RspError
+    monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
+    monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
+    A = csr.surrogate("G2_circuit", 0.1)
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
+    va0 = va.clone()
+    il = Ilu0(handle, rp, ci, nnz=A.nnz)
+    il.analysis()
+    assert il.zero_pivot() == -1
+    ones = torch.ones(A.n, dtype=torch.float64, device="cuda")
+    monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", "0")
+    il.factor(va)
+    with pytest.raises(RspError) as e:
+        il.zero_pivot()
+    assert e.value.status == STATUS_EXECUTION_FAILED
+    z = il.solve_lower(va, ones)
+    il.solve_lower(va, z, transpose=True)
+    for which in (il.TRSV_L, il.TRSV_LT):
+        with pytest.raises(RspError) as e:
+            il.solve_zero_pivot(which)
+        assert e.value.status == STATUS_EXECUTION_FAILED
+    monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", "200000")
+    va.copy_(va0)
+    il.factor(va)
+    assert il.zero_pivot() == -1
+    z = il.solve_lower(va, ones)
+    assert il.solve_zero_pivot(il.TRSV_L) == -1
+    y = il.solve_lower(va, z, transpose=True)
+    assert il.solve_zero_pivot(il.TRSV_LT) == -1
+    _, _, _, rz, ry = oracle_ilu(A, torch.float64)
+    rv, _, _ = ob.ilu0(A.rowptr, A.colidx, A.values)
+    assert np.array_equal(va.cpu().numpy(), rv)
+    assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)
