@@ -390,22 +390,22 @@ __device__ __forceinline__ int flow_item(unsigned long long c, unsigned long lon
     return __builtin_amdgcn_readfirstlane((int)min(d, (long long)(it1 - it0))) + it0;
 }
 
-// One wave's walk over the items [it0, it1) of a flow launch. Dynamic
-// (default): claims in start order, TWO items ahead — the claim for item
+// One wave's walk over the items [it0, it1) of a flow launch (rsp::FlowCtl).
+// Static (default): w, w + W, ... Claimed (kFlowClaims): in start order, TWO items ahead — the claim for item
 // j + 2 is issued during item j, behind its first loads (claim_ahead), and
 // read when item j + 1 ends, so the atomic's latency hides under a whole
 // item. A wave makes 2 + (items it processes) claims, so a launch advances
 // the counter by exactly items + 2 W (flow_claims on the host). The lowest
 // unfinished item is always some running wave's CURRENT item (a wave's
 // claimed items are above its current one), so progress needs no
-// co-residency. Static (RSP_ILU_FLOW_MODE bit 0, A/B only): w, w + W, ...
+// co-residency.
 struct FlowClaims {
     const rsp::FlowCtl &fc;
     unsigned long long base, c1 = 0, c2 = 0;
     int it0, it1, cur, stride;
     bool dyn;
     __device__ FlowClaims(const rsp::FlowCtl &f, unsigned long long b, int i0, int i1, int w, int W)
-        : fc(f), base(b), it0(i0), it1(i1), cur(i0 + w), stride(W), dyn(!(f.mode & rsp::kFlowStatic)) {}
+        : fc(f), base(b), it0(i0), it1(i1), cur(i0 + w), stride(W), dyn((f.mode & rsp::kFlowClaims) != 0) {}
     __device__ int first() {
         if (!dyn) return cur;
         const unsigned long long c0 = flow_claim(fc);
@@ -611,8 +611,8 @@ __global__ __launch_bounds__(256) void ilu0_flow_prep(IluArgs a, int nitems) {
 
 // Flow run of the factor (rsp::FacFlowRun): ONE launch of a.flow_grid
 // workgroups over the run's rows in level order instead of a launch per fat
-// level. Waves claim items in order from the flow counter (rsp::FlowCtl),
-// two items ahead. The hand-off is DATA-TAGGED, as trsv_flow's: the rows of
+// level; the waves walk the items statically or by claims (FlowClaims,
+// rsp::FlowCtl). The hand-off is DATA-TAGGED, as trsv_flow's: the rows of
 // flow runs start the call with their upper values (the u_kk and u_kj other
 // rows read) set to kNotYet by ilu0_flow_prep (originals in forig); a row
 // reads its operands (divisors and update-pair values) straight from vals
@@ -623,9 +623,12 @@ __global__ __launch_bounds__(256) void ilu0_flow_prep(IluArgs a, int nitems) {
 // no fence, no dependency lookup. Operands of rows outside flow runs are
 // final in vals (earlier kernels) and never kNotYet. A gate row three levels
 // back is polled first (lane 0, its first upper value) so that waves far
-// ahead of the front poll one word. Deadlock-free as trsv_flow (an item
-// waits for lower items only, and every lower item is held by a running
-// wave); a wait past fc.ticks gives up (rsp::FlowCtl). Structure and
+// ahead of the front poll one word. Progress as trsv_flow (an item waits
+// for lower items only); a wait past fc.ticks gives up (rsp::FlowCtl).
+// Config 3 against the round-3 flag hand-off (flags stored relaxed after an
+// s_waitcnt, which the HIP memory model does not order): fp64 factor 58.6 ->
+// 59.5 ms; the same flags with an agent-scope release / acquire pair (an L2
+// write-back and an L2 invalidate per row) took 116 ms. Structure and
 // arithmetic as ilu0_level_slot (the level's rm / qm at run time, budgets
 // KR / KQ at their maximum): the same bits.
 template <typename T>
@@ -1216,9 +1219,9 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
 }
 
 // Flow segments (a solve DAG's runs of two or more fat levels): ONE launch of
-// a.flow_grid workgroups instead of a launch per level. The waves claim the
-// segment's work items (rsp::FlowItem, level order) in order from the flow
-// counter (rsp::FlowCtl); an item starts as soon as the y values it reads
+// a.flow_grid workgroups instead of a launch per level. The waves walk the
+// segment's work items (rsp::FlowItem, level order) statically or by claims
+// (FlowClaims, rsp::FlowCtl); an item starts as soon as the y values it reads
 // exist, not when its whole previous level has ended. Existence is read from
 // the value itself: trsv_stream sets every y to kNotYet, a signalling-NaN
 // bit pattern that no y can have (every y is an arithmetic result — alpha x_i,
@@ -1227,13 +1230,12 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
 // reads its operands with device-scope (sc1) loads, re-reading (after an
 // s_sleep) those still kNotYet: the data-tagged hand-off of the price list
 // in MI355X_MICROARCH.md (handoff-1to1) — no flag, no fence.
-// Deadlock-free without any co-residency assumption: an item waits only for
-// items of lower index; items are claimed in index order by waves that are
-// running, and a wave's claimed next item is higher than its current one, so
-// the lowest unfinished item is some running wave's current item, whose
-// operands are all done. A wait beyond fc.ticks (never expected) gives up and
-// records the call in *fc.status (rsp_trsv_zero_pivot then returns
-// EXECUTION_FAILED) instead of hanging the GPU.
+// Progress: an item waits only for items of lower index, and each wave runs
+// its items in index order; with static items the grid is resident at once
+// (the lowest unfinished item is some wave's current item), with claims any
+// item waited on is held by a running wave. A wait beyond fc.ticks (never
+// expected) gives up and records the call in *fc.status (rsp_trsv_zero_pivot
+// then returns EXECUTION_FAILED) instead of hanging the GPU.
 // Same terms, same order, same fma chain as trsv_level: the same bits.
 template <typename T, int KIND>
 __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, unsigned long long base) {
@@ -1793,10 +1795,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
 
 // --------------------------------------------------------------- launchers
 
-// Workgroups of a flow launch. Items are claimed in order by running waves
-// (rsp::FlowCtl), so co-residency is not needed for progress; the occupancy
-// query (less one workgroup per CU of margin) still caps the grid so that
-// waves that cannot run yet do not sit in the dispatcher.
+// Workgroups of a flow launch: with static items every one must be resident
+// at once (rsp::FlowCtl): the occupancy query, less one workgroup per CU of
+// margin (it can overstate by one, MI355X_MICROARCH.md residency notes),
+// caps the requested grid.
 template <auto KERNEL>
 static int flow_grid(int want, int cus, int items) {
     static int occ = 0;  // per kernel
@@ -1812,7 +1814,7 @@ static int flow_grid(int want, int cus, int items) {
 // and the host mirror advanced by the claims it will make (rsp::FlowCtl).
 static unsigned long long flow_claims(const rsp::FlowCtl &fc, int items, int grid) {
     const unsigned long long base = *fc.claim_host;
-    if (fc.mode & rsp::kFlowStatic) return base;  // (A/B knob: no claims)
+    if (!(fc.mode & rsp::kFlowClaims)) return base;  // static items: no claims
     *fc.claim_host = base + (unsigned long long)items + 2ull * 4ull * (unsigned long long)grid;
     return base;
 }

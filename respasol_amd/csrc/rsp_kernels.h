@@ -268,13 +268,24 @@ struct FacFlowRun {
     int lb, le, c0, c1;
 };
 
-// Flow launches (ilu0_flow, trsv_flow): every wave CLAIMS its work items
-// from one device counter in the order waves actually run (agent-scope
-// fetch_add), so an item that is waited on is always held by a running wave:
-// progress needs no co-residency of the grid. The counter is never reset: a
-// launch over items [it0, it1) with W waves advances it by exactly
-// (it1 - it0) + W (every wave stops after its first claim past it1), which
-// the launcher adds to the host mirror, so the next launch knows its base.
+// Flow launches (ilu0_flow, trsv_flow): one persistent launch over a run of
+// work items in level order; an item waits only for items of lower index.
+// Item assignment (FlowCtl::mode):
+//  * static (default): wave w of the grid takes items w, w + W, ... Progress
+//    needs every workgroup of the grid resident together: the grid is sized
+//    from the occupancy query (one 4-wave workgroup per CU by default), and
+//    a wait that outlasts `ticks` gives up and is REPORTED (below), so a
+//    co-running kernel that keeps workgroups from being scheduled shows up
+//    as EXECUTION_FAILED, never as a hang;
+//  * claimed (kFlowClaims, RSP_ILU_FLOW_MODE=1): waves claim items in the
+//    order they actually run from one device counter (agent-scope
+//    fetch_add, two items ahead), so an item that is waited on is always
+//    held by a running wave and no co-residency is needed. Measured on
+//    config 3: fp64 factor 59.5 -> 85.8 ms, solve 43.6 -> 53.5 ms (every
+//    claim serialises on the one counter), hence opt-in. The counter is
+//    never reset: a launch over items [it0, it1) with W waves advances it by
+//    exactly (it1 - it0) + 2 W, which the launcher adds to the host mirror,
+//    so the next launch knows its base.
 // A wait longer than `ticks` (100 MHz wall clock) gives up — never expected;
 // a bound instead of a hang — and stores `gen` (the call's generation) into
 // *status, which rsp_ilu0_zero_pivot / rsp_trsv_zero_pivot compare with the
@@ -285,9 +296,9 @@ struct FlowCtl {
     unsigned long long ticks;         // give-up bound (RSP_ILU_FLOW_TIMEOUT_US)
     unsigned long long *claim;        // device claim counter
     unsigned long long *claim_host;   // host: claims issued by the launches enqueued so far
-    int mode;                         // A/B knob (RSP_ILU_FLOW_MODE): kFlowStatic
+    int mode;                         // RSP_ILU_FLOW_MODE: 0 static items, kFlowClaims claimed items
 };
-constexpr int kFlowStatic = 1;   // items w, w + W, ... per wave (needs a co-resident grid; round 3)
+constexpr int kFlowClaims = 1;
 
 
 struct IluArgs {

@@ -388,16 +388,18 @@ def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, name, scale):
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
-@pytest.mark.parametrize("flow,wpc", [(0, 8), (1, 4), (1, 8), (1, 16)])
+@pytest.mark.parametrize("flow,wpc,mode", [(0, 8, 0), (1, 4, 0), (1, 8, 0), (1, 16, 0), (1, 4, 1), (1, 16, 1)])
 @pytest.mark.parametrize("name,scale", [("xenon2", 0.3), ("offshore", 0.2), ("cfd2", 0.3), ("ss1", 0.2)])
-def test_flow_segments(handle, monkeypatch, flow, wpc, name, scale):
+def test_flow_segments(handle, monkeypatch, flow, wpc, mode, name, scale):
     """Fat solve segments and fat factor levels as one persistent launch each
     (trsv_flow: items start when the y they read exist, read from y itself;
-    ilu0_flow: rows start when the rows they read have set their done flags)
-    or a launch per level, 1-4 workgroups per CU: bitwise equal to the oracle
-    for the factor, L, L^T and U."""
+    ilu0_flow: rows start when the u values they read exist, read from the
+    values themselves) or a launch per level, 1-4 workgroups per CU, items
+    walked statically (mode 0) or claimed from the flow counter (mode 1):
+    bitwise equal to the oracle for the factor, L, L^T and U."""
     monkeypatch.setenv("RSP_ILU_FLOW", str(flow))
     monkeypatch.setenv("RSP_ILU_FLOW_WPC", str(wpc))
+    monkeypatch.setenv("RSP_ILU_FLOW_MODE", str(mode))
     A = csr.surrogate(name, scale)
     x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
     compare(A, torch.float64, handle, x=x)
