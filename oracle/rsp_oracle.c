@@ -225,6 +225,109 @@ int oracle_ilu0_f32(int n, const int *rp, const int *ci, float *v, int *zero_piv
 ORACLE_TRSV(double, d, fma)
 ORACLE_TRSV(float, s, fmaf)
 
+/* The solves in the SPLIT term order of the MI355X plans (round 4): the
+ * terms of row i whose producer lies exactly one level below i in the
+ * solve's DAG ("late": the level is the longest dependency path, so every
+ * row of level > 0 has at least one) are applied after all its other terms
+ * ("early"); each part keeps the reference's order (L: column ascending, as
+ * the csrsv2 NON_TRANSPOSE sweep; L^T: j descending, as the TRANSPOSE column
+ * sweep). Same terms, same fma per term; only the order of the sum differs,
+ * within SURVEY 8c's solve tolerance (tests/test_oracle.py). The GPU can
+ * then sum a row's early terms while the level just below it is still
+ * running. */
+static int *levels_l(int n, const int *rp, const int *ci) {
+    int *lv = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int i = 0; i < n; i++) {
+        int l = 0;
+        for (int p = rp[i]; p < rp[i + 1] && ci[p] < i; p++)
+            if (lv[ci[p]] + 1 > l) l = lv[ci[p]] + 1;
+        lv[i] = l;
+    }
+    return lv;
+}
+/* the strict lower part by columns: for column k, the rows j > k with
+ * l_jk != 0 in j-descending order (tp: CSR positions, tr: rows) */
+static void lower_by_cols(int n, const int *rp, const int *ci, int **cp_, int **tp_, int **tr_) {
+    int *cp = (int *)calloc((size_t)n + 1, sizeof(int));
+    for (int j = 0; j < n; j++)
+        for (int p = rp[j]; p < rp[j + 1] && ci[p] < j; p++) cp[ci[p] + 1]++;
+    for (int k = 0; k < n; k++) cp[k + 1] += cp[k];
+    int m = cp[n] > 0 ? cp[n] : 1;
+    int *tp = (int *)malloc((size_t)m * sizeof(int)), *tr = (int *)malloc((size_t)m * sizeof(int));
+    int *fill = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int k = 0; k < n; k++) fill[k] = cp[k];
+    for (int j = n - 1; j >= 0; j--)
+        for (int p = rp[j]; p < rp[j + 1] && ci[p] < j; p++) {
+            tp[fill[ci[p]]] = p;
+            tr[fill[ci[p]]++] = j;
+        }
+    free(fill);
+    *cp_ = cp;
+    *tp_ = tp;
+    *tr_ = tr;
+}
+
+#define ORACLE_TRSV_SPLIT(T, SUF, FMA)                                                         \
+    static void lower_n_split_##SUF(int n, const int *rp, const int *ci, const T *v, T alpha,  \
+                                    const T *x, T *y) {                                        \
+        int *lv = levels_l(n, rp, ci);                                                         \
+        for (int i = 0; i < n; i++) {                                                          \
+            T s = alpha * x[i];                                                                \
+            for (int late = 0; late < 2; late++)                                               \
+                for (int p = rp[i]; p < rp[i + 1] && ci[p] < i; p++)                           \
+                    if ((lv[ci[p]] == lv[i] - 1) == late) s = FMA(-v[p], y[ci[p]], s);         \
+            y[i] = s;                                                                          \
+        }                                                                                      \
+        free(lv);                                                                              \
+    }                                                                                          \
+    static void lower_t_split_##SUF(int n, const int *rp, const int *ci, const T *v, T alpha,  \
+                                    const T *x, T *y) {                                        \
+        int *cp, *tp, *tr;                                                                     \
+        lower_by_cols(n, rp, ci, &cp, &tp, &tr);                                               \
+        int *lv = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));                        \
+        for (int k = n - 1; k >= 0; k--) { /* L^T levels: longest path from above */         \
+            int l = 0;                                                                         \
+            for (int q = cp[k]; q < cp[k + 1]; q++)                                            \
+                if (lv[tr[q]] + 1 > l) l = lv[tr[q]] + 1;                                      \
+            lv[k] = l;                                                                         \
+        }                                                                                      \
+        for (int k = n - 1; k >= 0; k--) {                                                     \
+            T s = alpha * x[k];                                                                \
+            for (int late = 0; late < 2; late++)                                               \
+                for (int q = cp[k]; q < cp[k + 1]; q++)                                        \
+                    if ((lv[tr[q]] == lv[k] - 1) == late) s = FMA(-v[tp[q]], y[tr[q]], s);     \
+            y[k] = s;                                                                          \
+        }                                                                                      \
+        free(lv);                                                                              \
+        free(cp);                                                                              \
+        free(tp);                                                                              \
+        free(tr);                                                                              \
+    }
+
+ORACLE_TRSV_SPLIT(double, d, fma)
+ORACLE_TRSV_SPLIT(float, s, fmaf)
+
+void oracle_trsv_lower_n_split_f64(int n, const int *rp, const int *ci, const double *v, double alpha,
+                                   const double *x, double *y) {
+    lower_n_split_d(n, rp, ci, v, alpha, x, y);
+}
+void oracle_trsv_lower_n_split_f32(int n, const int *rp, const int *ci, const float *v, float alpha,
+                                   const float *x, float *y, int ftz) {
+    unsigned old = ftz_enter(ftz);
+    lower_n_split_s(n, rp, ci, v, alpha, x, y);
+    ftz_leave(old);
+}
+void oracle_trsv_lower_t_split_f64(int n, const int *rp, const int *ci, const double *v, double alpha,
+                                   const double *x, double *y) {
+    lower_t_split_d(n, rp, ci, v, alpha, x, y);
+}
+void oracle_trsv_lower_t_split_f32(int n, const int *rp, const int *ci, const float *v, float alpha,
+                                   const float *x, float *y, int ftz) {
+    unsigned old = ftz_enter(ftz);
+    lower_t_split_s(n, rp, ci, v, alpha, x, y);
+    ftz_leave(old);
+}
+
 void oracle_trsv_lower_n_f64(int n, const int *rp, const int *ci, const double *v, double alpha,
                              const double *x, double *y) {
     lower_n_d(n, rp, ci, v, alpha, x, y);

@@ -73,6 +73,17 @@ void oracle_trsv_lower_t_f64(int n, const int *rowptr, const int *colidx, const 
                              double alpha, const double *x, double *y);
 void oracle_trsv_lower_t_f32(int n, const int *rowptr, const int *colidx, const float *vals,
                              float alpha, const float *x, float *y, int ftz);
+/* The same two solves in the split term order of the MI355X plans: a row's
+ * terms from the level just below its own (in the solve's DAG) applied
+ * last, each part in the order above (rsp_oracle.c ORACLE_TRSV_SPLIT). */
+void oracle_trsv_lower_n_split_f64(int n, const int *rowptr, const int *colidx, const double *vals,
+                                   double alpha, const double *x, double *y);
+void oracle_trsv_lower_n_split_f32(int n, const int *rowptr, const int *colidx, const float *vals,
+                                   float alpha, const float *x, float *y, int ftz);
+void oracle_trsv_lower_t_split_f64(int n, const int *rowptr, const int *colidx, const double *vals,
+                                   double alpha, const double *x, double *y);
+void oracle_trsv_lower_t_split_f32(int n, const int *rowptr, const int *colidx, const float *vals,
+                                   float alpha, const float *x, float *y, int ftz);
 /* U y = alpha x (upper incl. diagonal) — the desc_U extension. */
 void oracle_trsv_upper_f64(int n, const int *rowptr, const int *colidx, const double *vals,
                            double alpha, const double *x, double *y);

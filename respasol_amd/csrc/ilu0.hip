@@ -1408,6 +1408,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     __shared__ TermIds<G> lidx[rsp::kChunkTerms / G + 1];
     __shared__ ThinRow<T> lrow[rsp::kChunkRows];
     __shared__ int lrowi[rsp::kChunkRows];
+    __shared__ unsigned char legr[rsp::kChunkRows];  // per row: its early term groups (split order)
     __shared__ T ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
     __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];
     __shared__ int lds_done;  // multi-wave narrow runs: absolute levels completed
@@ -1502,8 +1503,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             ThinRow<T> r;
             r.x = p.xv;
             r.g = p.r.g;
-            r.out = p.r.out * (int)sizeof(T);
+            r.out = (p.r.out & 0xffff) * (int)sizeof(T);
             lrow[tid] = r;
+            legr[tid] = (unsigned char)(p.r.out >> 16);  // early groups (split order)
             lrowi[tid] = p.r.i;
             if constexpr (KIND == 2) ldg[tid] = p.dg;
         }
@@ -1647,6 +1649,100 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             p3 = p4;
         }
     };
+    // Narrow run in the SPLIT term order (L / L^T: a row's terms from the
+    // level just below it are its last groups, legr[] = the groups before
+    // them), wave 0 alone, software-pipelined so that only the late part of a
+    // level is on the critical path: after level q's y stores, the wave issues
+    // the late y loads of level q+1 and, while they are in flight, finishes
+    // level q+1's EARLY partial sum (its producers are two or more levels back,
+    // done) and prefetches the records of the levels after; then it waits for
+    // the late y, runs the late fmas from the early partial and stores. A
+    // wave's LDS accesses are performed in order, so no counter and no barrier
+    // orders consecutive levels. Lanes past a level's rows repeat its last row
+    // (same value to the same slot); groups past a row's own read the pad
+    // group (exact no-op fmas); past the run, records are clamped and unused.
+    // Same terms, same order (early then late), same fma chain as every other
+    // solve path in the split order: same bits.
+    auto narrow_run_split = [&](const rsp::LevelChunk &ch, int q0, int q1) {  // wave 0
+        const int lane = tid, x0 = ch.x0, nl = ch.l1 - ch.l0;
+        auto lpt = [&](int q) { return lptr[min(q, nl)]; };
+        struct Lev {
+            ThinRow<T> R;
+            int eg;  // early groups; late groups = (R.g >> 16) - eg
+        };
+        auto lev = [&](int q) {
+            const int p0 = lpt(q), p1 = lpt(q + 1);
+            const int cr = max(p0 - x0 + min(lane, p1 - p0 - 1), 0);
+            Lev v;
+            v.R = lrow[cr];
+            v.eg = legr[cr];
+            return v;
+        };
+        auto early_grp = [&](const Lev &v, int gi) { return gi < v.eg ? (v.R.g & 0xffff) + gi : kPadGroup; };
+        auto late_grp = [&](const Lev &v, int gi) {
+            return gi < (v.R.g >> 16) - v.eg ? (v.R.g & 0xffff) + v.eg + gi : kPadGroup;
+        };
+        auto fma_group = [&](T s, const TermGroup<T, G> &g, const T (&y)[G]) {
+#pragma unroll
+            for (int j = 0; j < G; ++j) s = fma_t(-g.v[j], y[j], s);
+            return s;
+        };
+        auto ygroup = [&](T (&y)[G], const TermIds<G> &id) {
+#pragma unroll
+            for (int j = 0; j < G; ++j) y[j] = yb(id.v[j]);
+        };
+        Lev c = lev(q0), n = lev(q0 + 1);
+        // early partial of level q0 (its early producers are done)
+        T e = c.R.x;
+        for (int gi = 0; __ballot(gi < c.eg); ++gi) {
+            const int gg = early_grp(c, gi);
+            e = group_fma(e, lval[gg], lidx[gg]);
+        }
+        TermGroup<T, G> cLV = lval[late_grp(c, 0)];
+        TermIds<G> nEI = lidx[early_grp(n, 0)];
+        TermGroup<T, G> nEV = lval[early_grp(n, 0)];
+        T cy[G];
+        {
+            const TermIds<G> cLI = lidx[late_grp(c, 0)];
+            ygroup(cy, cLI);
+        }
+        for (int q = q0; q < q1; ++q) {
+            // early y of level q+1 (producers two or more levels back)
+            T ny[G];
+            ygroup(ny, nEI);
+            // records of level q+2, the late group 0 of level q+1
+            const Lev m = lev(q + 2);
+            const int nlg = late_grp(n, 0);
+            const TermIds<G> nLI = lidx[nlg];
+            const TermGroup<T, G> nLV = lval[nlg];
+            // level q: the late part (critical path)
+            T s = fma_group(e, cLV, cy);
+            for (int gi = 1; __ballot(gi < (c.R.g >> 16) - c.eg); ++gi) {
+                const int gg = late_grp(c, gi);
+                s = group_fma(s, lval[gg], lidx[gg]);
+            }
+            put(c.R.out, s);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            // late y of level q+1 (after level q's stores)
+            ygroup(cy, nLI);
+            // level q+1's early partial, under those loads
+            T e2 = fma_group(n.R.x, nEV, ny);
+            for (int gi = 1; __ballot(gi < n.eg); ++gi) {
+                const int gg = early_grp(n, gi);
+                e2 = group_fma(e2, lval[gg], lidx[gg]);
+            }
+            // early group 0 of level q+2
+            const int meg = early_grp(m, 0);
+            nEI = lidx[meg];
+            nEV = lval[meg];
+            e = e2;
+            c = n;
+            n = m;
+            cLV = nLV;
+        }
+    };
     // Narrow run on K waves (a.narrow_waves): wave w computes levels q0 + w,
     // q0 + w + K, ... A level reads its row records, term indices and values
     // first (nothing there depends on a y), then waits until the run's
@@ -1703,7 +1799,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             if (narrow(q)) {
                 const int qe = run_end(q, nl);
                 const int K = min(a.narrow_waves, (int)(blockDim.x >> 6));  // waves of this launch
-                if (K > 1) {
+                if (KIND != 2 && G == 2 && a.narrow_split) {  // (G = 4: the registers are not there)
+                    if constexpr (KIND != 2 && G == 2)
+                        if (tid < 64) narrow_run_split(ch, q, qe);
+                } else if (K > 1) {
                     if (tid < 64 * K) narrow_run_mw(ch, q, qe, K);
                 } else if (tid < 64) {
                     if (a.trace)

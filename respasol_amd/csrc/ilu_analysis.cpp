@@ -124,9 +124,15 @@ class Pool {
         std::atomic<int> next{0}, done{0};
         std::mutex m;
         std::condition_variable cv;
+        std::exception_ptr err;  // the first exception of a block (rethrown by run)
         void work() {
             for (int b; (b = next.fetch_add(1, std::memory_order_relaxed)) < nb;) {
-                body(b);
+                try {
+                    body(b);
+                } catch (...) {
+                    std::lock_guard<std::mutex> g(m);
+                    if (!err) err = std::current_exception();
+                }
                 if (done.fetch_add(1, std::memory_order_acq_rel) + 1 == nb) {
                     std::lock_guard<std::mutex> g(m);
                     cv.notify_all();
@@ -180,6 +186,9 @@ class Pool {
         j->work();
         std::unique_lock<std::mutex> g(j->m);
         j->cv.wait(g, [&] { return j->done.load(std::memory_order_acquire) == nb; });
+        // every block has finished (no worker still runs body over the
+        // caller's locals): a block's exception is the caller's now
+        if (j->err) std::rethrow_exception(j->err);
     }
 };
 
@@ -258,23 +267,33 @@ static int chain_batch(long long total, long long count) {
 //                    instead, the same arrays bit for bit): per flat term
 //                    its position and y source, the window remap, the thin
 //                    runs' row records, y indices and staged terms.
-template <typename RowCount>
+// A thin-run row's padded terms: its early and its late terms (split order,
+// IluHostPlan::lpos) each padded to whole groups, at least one group.
+static inline int split_padded(int ne, int cnt, int group) {
+    const int pe = (ne + group - 1) / group * group, pl = (cnt - ne + group - 1) / group * group;
+    return std::max(group, pe + pl);
+}
+
+template <typename RowCount, typename RowEarly>
 static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
                             int thin_rows, int group, const hvec<int> &diag,
-                            RowCount row_count, SolvePlan &sp) {
+                            RowCount row_count, RowEarly row_early, SolvePlan &sp) {
     const int nlev = (int)ptr.size() - 1;
     const long long nx = (long long)rows.size();
     constexpr long long kGrain = 1 << 14;
     hvec<int> order(rows);
-    hvec<int> nt_row((size_t)n, 0);
+    hvec<int> nt_row((size_t)n, 0), ne_row((size_t)n, 0);
     pfor(n, kGrain, [&](long long a, long long b) {
-        for (long long i = a; i < b; i++) nt_row[(size_t)i] = row_count((int)i);
+        for (long long i = a; i < b; i++) {
+            nt_row[(size_t)i] = row_count((int)i);
+            ne_row[(size_t)i] = row_early((int)i);
+        }
     });
-    auto padded = [&](int cnt) { return std::max(1, (cnt + group - 1) / group) * group; };
+    auto padded_row = [&](int i) { return split_padded(ne_row[(size_t)i], nt_row[(size_t)i], group); };
     hvec<int> lpad((size_t)std::max(nlev, 1), 0);
     pfor_dyn(nlev, nx, kGrain, [&](int l) {
         int t = 0;
-        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) t += padded(nt_row[(size_t)order[(size_t)x]]);
+        for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) t += padded_row(order[(size_t)x]);
         lpad[(size_t)l] = t;
     });
     // RSP_ILU_THIN_TERMS: tuning knob (a thin level's padded terms, <= kChunkTerms)
@@ -324,7 +343,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
         const bool padl = pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0;
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
             const int i = order[(size_t)x], t = nt_row[(size_t)i];
-            const int t1 = thin_lev[(size_t)l] ? padded(t) : t;
+            const int t1 = thin_lev[(size_t)l] ? padded_row(i) : t;
             len[(size_t)x] = padl && x - ptr[(size_t)l] < sp.nshort[(size_t)l] ? std::max(t1, rsp::kFatLongTerms) : t1;
             sp.tasks[(size_t)x].t1 = t1;  // length for now
         }
@@ -423,20 +442,36 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
 }
 
 // row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
-// (row_count(i) of them, as given to solve_plan_rows).
-template <typename RowTerms>
-static void solve_plan_terms(int n, const hvec<int> &ptr, int group, RowTerms row_terms, SolvePlan &sp) {
+// (row_count(i) of them, as given to solve_plan_rows; the first row_early(i)
+// of them early). A thin row (its task spans split_padded terms) places its
+// late terms at the first group after its early ones; other rows keep their
+// terms contiguous (when split_padded equals the count the two coincide).
+static inline int late_offset(int ne, int cnt, int len, int group) {
+    return len == split_padded(ne, cnt, group) ? (ne + group - 1) / group * group : ne;
+}
+template <typename RowTerms, typename RowEarly>
+static void solve_plan_terms(int n, const hvec<int> &ptr, int group, RowTerms row_terms, RowEarly row_early,
+                             SolvePlan &sp) {
     constexpr long long kGrain = 1 << 14;
     const int nlev = (int)ptr.size() - 1;
     const long long nx = (long long)ptr[(size_t)nlev], total = sp.nterm;
     sp.tpos.assign((size_t)total, -1);
     hvec<int> col((size_t)total, -1);
+    hvec<int> egroups((size_t)std::max(nx, 1LL), 0);  // thin rows: whole groups of early terms
     pfor(nx, kGrain, [&](long long a, long long b) {
         for (long long x = a; x < b; x++) {
-            int k = sp.tasks[(size_t)x].t0;
-            row_terms(sp.tasks[(size_t)x].i, [&](int tp, int c) {
+            const rsp::RowTask &t = sp.tasks[(size_t)x];
+            const int ne = row_early(t.i);
+            int cnt = 0;
+            row_terms(t.i, [&](int, int) { cnt++; });
+            const int lo = late_offset(ne, cnt, t.t1 - t.t0, group);
+            if (t.t1 - t.t0 == split_padded(ne, cnt, group)) egroups[(size_t)x] = lo / group;
+            int o = 0;
+            row_terms(t.i, [&](int tp, int c) {
+                const int k = t.t0 + (o < ne ? o : lo + (o - ne));
                 sp.tpos[(size_t)k] = tp;
-                col[(size_t)k++] = c;
+                col[(size_t)k] = c;
+                o++;
             });
         }
     });
@@ -498,7 +533,7 @@ static void solve_plan_terms(int n, const hvec<int> &ptr, int group, RowTerms ro
         for (int x = ch.x0; x < ch.x1; x++) {
             const rsp::RowTask &t = sp.tasks[(size_t)x];
             sp.trow[(size_t)x] = {(t.t0 - ch.k0) / group | ((t.t1 - t.t0) / group) << 16,
-                                  (x - base) & (rsp::kYWin - 1), t.i, t.d};
+                                  ((x - base) & (rsp::kYWin - 1)) | egroups[(size_t)x] << 16, t.i, t.d};
             for (int k = t.t0; k < t.t1; k++) {
                 const int sc = sp.src[(size_t)k];
                 if (sc < 0) {
@@ -514,12 +549,12 @@ static void solve_plan_terms(int n, const hvec<int> &ptr, int group, RowTerms ro
 }
 
 // Both parts on the host.
-template <typename RowCount, typename RowTerms>
+template <typename RowCount, typename RowTerms, typename RowEarly>
 static void build_solve_plan(int n, const hvec<int> &ptr, const hvec<int> &rows,
                              int thin_rows, int group, const hvec<int> &diag,
-                             RowCount row_count, RowTerms row_terms, SolvePlan &sp) {
-    solve_plan_rows(n, ptr, rows, thin_rows, group, diag, row_count, sp);
-    solve_plan_terms(n, ptr, group, row_terms, sp);
+                             RowCount row_count, RowTerms row_terms, RowEarly row_early, SolvePlan &sp) {
+    solve_plan_rows(n, ptr, rows, thin_rows, group, diag, row_count, row_early, sp);
+    solve_plan_terms(n, ptr, group, row_terms, row_early, sp);
 }
 
 // Which levels of the L DAG the factor runs thin. A level runs thin up to
@@ -973,7 +1008,7 @@ void plan_u(const int *rp, const int *ci, IluHostPlan &hp) {
                      [&](int i) { return rp[(size_t)i + 1] - dpos[(size_t)i] - hasdiag[(size_t)i]; },
                      [&](int i, auto emit) {
         for (int p = dpos[(size_t)i] + hasdiag[(size_t)i]; p < rp[(size_t)i + 1]; p++) emit(p, ci[(size_t)p]);
-    }, hp.U.sp);
+    }, [](int) { return 0; }, hp.U.sp);  // (the U solve keeps the reference order: no split)
     hp.U.planned = true;
 }
 
@@ -1030,6 +1065,54 @@ rsp_status_t plan_validate(int n, const int *rpp, const int *cip, IluHostPlan &h
     return RSP_STATUS_SUCCESS;
 }
 
+// The split term order of both solve DAGs (IluHostPlan::lpos): per row, its
+// early terms, then its late ones (producer one level below the row's), each
+// part in the reference's order; a stable partition per row, rows in
+// parallel. (The oracle restates it: rsp_oracle.c ORACLE_TRSV_SPLIT.)
+static void split_terms(const int *rp, const int *ci, IluHostPlan &hp) {
+    const int n = hp.n;
+    const hvec<int> &dpos = hp.dpos, &lv = hp.lev_l, &lvt = hp.lev_lt;
+    hp.lpos.assign((size_t)std::max(hp.nnz_s, 1), 0);
+    hp.ne_l.assign((size_t)std::max(n, 1), 0);
+    hp.ne_lt.assign((size_t)std::max(n, 1), 0);
+    parallel_rows(n, [&](int r0, int r1) {
+        hvec<int> late, late_c;
+        for (int i = r0; i < r1; i++) {
+            // L: row i reads y_j, j = ci[p] < i
+            int k = rp[i];
+            late.clear();
+            for (int p = rp[i]; p < dpos[(size_t)i]; p++) {
+                if (lv[(size_t)ci[p]] == lv[(size_t)i] - 1)
+                    late.push_back(p);
+                else
+                    hp.lpos[(size_t)k++] = p;
+            }
+            hp.ne_l[(size_t)i] = k - rp[i];
+            for (int p : late) hp.lpos[(size_t)k++] = p;
+            // L^T: row i reads y_j, j = ltc[q] > i, q in [ltp[i], ltp[i+1])
+            const int q0 = hp.ltp[(size_t)i], q1 = hp.ltp[(size_t)i + 1];
+            late.clear();
+            late_c.clear();
+            int w = q0;
+            for (int q = q0; q < q1; q++) {
+                const int j = hp.ltc[(size_t)q], tp = hp.lts[(size_t)q];
+                if (lvt[(size_t)j] == lvt[(size_t)i] - 1) {
+                    late.push_back(tp);
+                    late_c.push_back(j);
+                } else {
+                    hp.lts[(size_t)w] = tp;
+                    hp.ltc[(size_t)w++] = j;
+                }
+            }
+            hp.ne_lt[(size_t)i] = w - q0;
+            for (size_t u = 0; u < late.size(); u++) {
+                hp.lts[(size_t)w] = late[u];
+                hp.ltc[(size_t)w++] = late_c[u];
+            }
+        }
+    });
+}
+
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     const int n = hp.n;
     const hvec<int> &dpos = hp.dpos;
@@ -1039,8 +1122,9 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     // the L^T levels; each level set then grouped (counting sort).
     // levels of the lower DAG (factor + L solve): the longest path ending at
     // each row (each row needs its producers')
-    std::thread tl([&] {
-        hvec<int> lv((size_t)n, 0);
+    Task tl([&] {
+        hvec<int> &lv = hp.lev_l;
+        lv.assign((size_t)n, 0);
         int nl = n > 0 ? 1 : 0;
         for (int i = 0; i < n; i++) {
             int l = 0;
@@ -1051,8 +1135,9 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
         group_levels(lv, nl, hp.L.ptr, hp.L.rows);
     });
     // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
-    std::thread tt([&] {
-        hvec<int> lvt((size_t)n, 0);
+    Task tt([&] {
+        hvec<int> &lvt = hp.lev_lt;
+        lvt.assign((size_t)n, 0);
         int nlt = n > 0 ? 1 : 0;
         for (int j = n - 1; j >= 0; j--) {
             nlt = std::max(nlt, lvt[(size_t)j] + 1);
@@ -1082,6 +1167,7 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     }
     tl.join();
     tt.join();
+    split_terms(rp, ci, hp);
 }
 
 rsp_status_t plan_symbolic(const int *rpp, const int *cip, IluHostPlan &hp) {
@@ -1123,27 +1209,37 @@ static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool
     long long nlo = 0;
     for (int i = 0; i < n; i++) nlo += dpos[(size_t)i] - rp[(size_t)i];
     hp.L.batch = hp.LT.batch = chain_batch(nlo, n);
-    for (DagHost *d : {&hp.L, &hp.LT})  // thin-run term groups
-        d->group = env_int("RSP_ILU_GROUP", d->batch == 2 ? 2 : 4) == 2 ? 2 : 4;
+    // thin-run term groups: 2 where a row's two parts (split order: early,
+    // late) are short on average (mean chain <= 5 terms: the deep circuits;
+    // their narrow runs take the single-wave split loop, G = 2 only), else 4
+    const int g_dflt = n > 0 && (double)nlo / n <= 5.0 ? 2 : 4;
+    for (DagHost *d : {&hp.L, &hp.LT})
+        d->group = env_int("RSP_ILU_GROUP", g_dflt) == 2 ? 2 : 4;
     auto cnt_l = [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; };
     auto cnt_lt = [&](int i) { return ltp[(size_t)i + 1] - ltp[(size_t)i]; };
+    // split term order (IluHostPlan::lpos): early terms first
+    auto ne_l = [&](int i) { return hp.ne_l[(size_t)i]; };
+    auto ne_lt = [&](int i) { return hp.ne_lt[(size_t)i]; };
     // the two DAGs' plans (flat terms in level order, thin-run chunks, y
     // sources) are independent: built concurrently
-    std::thread tl([&] {
+    Task tl([&] {
         timed_plan(n, "L", [&] {
-            solve_plan_rows(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, hvec<int>(), cnt_l, hp.L.sp);
+            solve_plan_rows(n, hp.L.ptr, hp.L.rows, thin_solve, hp.L.group, hvec<int>(), cnt_l, ne_l, hp.L.sp);
             if (terms_on_host)
                 solve_plan_terms(n, hp.L.ptr, hp.L.group, [&](int i, auto emit) {
-                    for (int p = rp[(size_t)i]; p < dpos[(size_t)i]; p++) emit(p, ci[(size_t)p]);
-                }, hp.L.sp);
+                    for (int o = rp[(size_t)i]; o < dpos[(size_t)i]; o++) {
+                        const int p = hp.lpos[(size_t)o];
+                        emit(p, ci[(size_t)p]);
+                    }
+                }, ne_l, hp.L.sp);
         });
     });
     timed_plan(n, "LT", [&] {
-        solve_plan_rows(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, hvec<int>(), cnt_lt, hp.LT.sp);
+        solve_plan_rows(n, hp.LT.ptr, hp.LT.rows, thin_solve, hp.LT.group, hvec<int>(), cnt_lt, ne_lt, hp.LT.sp);
         if (terms_on_host)
             solve_plan_terms(n, hp.LT.ptr, hp.LT.group, [&](int i, auto emit) {
                 for (int q = ltp[(size_t)i]; q < ltp[(size_t)i + 1]; q++) emit(lts[(size_t)q], ltc[(size_t)q]);
-            }, hp.LT.sp);
+            }, ne_lt, hp.LT.sp);
     });
     tl.join();
     hp.L.planned = hp.LT.planned = true;
@@ -1282,7 +1378,7 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
 
 
 void plan_rest(const int *rp, const int *ci, long long slot_cap, bool want_u, IluHostPlan &hp) {
-    std::thread ts([&] {
+    Task ts([&] {
         plan_solves(rp, ci, hp);
         if (want_u) plan_u(rp, ci, hp);
     });

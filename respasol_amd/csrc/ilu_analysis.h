@@ -11,7 +11,10 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <exception>
 #include <functional>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "rsp.h"
@@ -19,6 +22,34 @@
 #include "rsp_kernels.h"
 
 namespace rsp_an {
+
+// A helper thread of the analysis whose exception (std::bad_alloc from the
+// pool, say) is carried to join(), which rethrows it in the caller; the
+// destructor joins too, so a caller that unwinds first never leaves it
+// running over the caller's locals (nor calls std::terminate).
+class Task {
+    std::exception_ptr err_;
+    std::thread t_;
+
+  public:
+    template <typename F>
+    explicit Task(F f) : t_([this, f] {
+          try {
+              f();
+          } catch (...) {
+              err_ = std::current_exception();
+          }
+      }) {}
+    Task(const Task &) = delete;
+    Task &operator=(const Task &) = delete;
+    void join() {
+        if (t_.joinable()) t_.join();
+        if (err_) std::rethrow_exception(std::exchange(err_, nullptr));
+    }
+    ~Task() {
+        if (t_.joinable()) t_.join();
+    }
+};
 
 inline int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
@@ -75,6 +106,12 @@ struct IluHostPlan {
     DagHost L, LT, U;
     // transposed strict lower part (row k: (position of l_jk, j), j descending)
     hvec<int> ltp, lts, ltc;
+    // the solves' SPLIT term order (round 4): a row's terms from the level
+    // just below its own in the DAG ("late") after its other ("early") terms,
+    // each part in the reference's order. L: lpos[rp[i] + o] = position of
+    // the o-th term of row i; L^T: lts / ltc above, permuted per row the same
+    // way; ne_l / ne_lt = early terms per row. lev_l / lev_lt: the levels.
+    hvec<int> lpos, ne_l, ne_lt, lev_l, lev_lt;
     FacPlan fplan;
     int fac_batch = 8;
     hvec<rsp::FacRow> frow;

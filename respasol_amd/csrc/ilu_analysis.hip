@@ -343,30 +343,43 @@ hipError_t ilu_an_gather_pairs(const int *rows, int nrows, const int *rp, const 
 // (ilu_analysis.cpp solve_plan_terms restated; see SolveTermsArgs)
 namespace {
 
+// a row's padded terms and the offset of its late terms (ilu_analysis.cpp
+// split_padded / late_offset restated)
+__device__ __forceinline__ int st_split_padded(int ne, int cnt, int g) {
+    const int pe = (ne + g - 1) / g * g, pl = (cnt - ne + g - 1) / g * g;
+    return max(g, pe + pl);
+}
+__device__ __forceinline__ int st_row_terms(const rsp_k::SolveTermsArgs &a, int i, int *j0) {
+    if (a.kind == 0) {
+        *j0 = a.rp[i];
+        return a.dpos[i] - *j0;
+    }
+    *j0 = a.ltp[i];
+    return a.ltp[i + 1] - *j0;
+}
+
 // one wave per level-order slot x: its flat terms [t0, next t0) — the row's
-// terms in order, then pads (position -1, source the zero slot) — y index
-// "zero slot" (thin runs overwrite theirs), slot_of, default row record
+// terms in the split order (a thin row's late terms from the first group
+// after its early ones), pads (position -1, source the zero slot) elsewhere —
+// y index "zero slot" (thin runs overwrite theirs), slot_of, default row record
 __global__ __launch_bounds__(256) void st_rows(rsp_k::SolveTermsArgs a) {
     const int x = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (x >= a.nx) return;
     const rsp::RowTask t = a.tasks[x];
     const int i = t.i;
-    int j0, cnt;
-    if (a.kind == 0) {
-        j0 = a.rp[i];
-        cnt = a.dpos[i] - j0;
-    } else {
-        j0 = a.ltp[i];
-        cnt = a.ltp[i + 1] - j0;
-    }
+    int j0;
+    const int cnt = st_row_terms(a, i, &j0);
+    const int ne = a.kind == 2 ? 0 : a.ne[i], g = a.group;
+    const int lo = t.t1 - t.t0 == st_split_padded(ne, cnt, g) ? (ne + g - 1) / g * g : ne;
     const int tend = x + 1 < a.nx ? a.tasks[x + 1].t0 : a.total;
-    for (int o = lane; o < tend - t.t0; o += 64) {
-        const int k = t.t0 + o;
+    for (int q = lane; q < tend - t.t0; q += 64) {
+        const int k = t.t0 + q;
+        const int o = q < ne ? q : (q >= lo && q - lo < cnt - ne ? ne + q - lo : -1);  // term, or pad
         int tp = -1, c = rsp::kPadSrc;
-        if (o < cnt) {
+        if (o >= 0) {
             const int j = j0 + o;
-            tp = a.kind == 0 ? j : a.lts[j];
-            c = a.kind == 0 ? a.ci[j] : a.ltc[j];
+            tp = a.kind == 0 ? a.lpos[j] : a.lts[j];
+            c = a.kind == 0 ? a.ci[tp] : a.ltc[j];
         }
         a.tpos[k] = tp;
         a.src[k] = c;
@@ -442,8 +455,11 @@ __global__ __launch_bounds__(256) void st_fill(rsp_k::SolveTermsArgs a) {
     const int G = a.group;
     for (int x = ch.x0 + (int)threadIdx.x; x < ch.x1; x += 256) {
         const rsp::RowTask t = a.tasks[x];
+        int j0;
+        const int cnt = st_row_terms(a, t.i, &j0), ne = a.kind == 2 ? 0 : a.ne[t.i];
+        const int eg = t.t1 - t.t0 == st_split_padded(ne, cnt, G) ? (ne + G - 1) / G : 0;  // early groups
         a.trow[x] = rsp::ThinRowPlan{(t.t0 - ch.k0) / G | ((t.t1 - t.t0) / G) << 16,
-                                     (x - base) & (rsp::kYWin - 1), t.i, t.d};
+                                     ((x - base) & (rsp::kYWin - 1)) | eg << 16, t.i, t.d};
     }
     int run = st0;
     for (int kb = ch.k0; kb < ch.k1; kb += 256) {
@@ -472,7 +488,7 @@ hipError_t ilu_an_solve_terms(const SolveTermsArgs &a, hipStream_t s) {
     hipError_t e = hipMemsetAsync(a.nst + a.nch, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     size_t tb = 0;
-    ilu_an_scan(nullptr, nullptr, a.nch + 1, nullptr, &tb, s);
+    (void)ilu_an_scan(nullptr, nullptr, a.nch + 1, nullptr, &tb, s);
     e = ilu_an_scan(a.nst, a.nst_ptr, a.nch + 1, a.scan, &tb, s);
     if (e != hipSuccess) return e;
     st_fill<<<a.nch, 256, 0, s>>>(a);

@@ -347,7 +347,7 @@ static int spmv_row_align(rsp_handle_t h, rsp_datatype_t t) {
 
 static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t compute_type);
 
-rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+static rsp_status_t rsp_spmv_buffer_size_impl(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                   rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
                                   size_t *buffer_size) {
     (void)alpha;
@@ -658,7 +658,7 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     return RSP_STATUS_SUCCESS;
 }
 
-rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+static rsp_status_t rsp_spmv_preprocess_impl(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                  rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
                                  rsp_datatype_t compute_type, void *d_buffer) {
     (void)alpha;
@@ -739,13 +739,13 @@ static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alp
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
 }
 
-rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
+static rsp_status_t rsp_spmv_impl(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
                       const void *d_x, const void *beta, void *d_y, rsp_datatype_t compute_type,
                       void *d_buffer) {
     return spmv_run(h, op, alpha, mat, d_x, beta, d_y, compute_type, d_buffer, 0);
 }
 
-rsp_status_t rsp_spmv_part(rsp_handle_t h, const void *alpha, rsp_spmat_t mat, const void *d_x,
+static rsp_status_t rsp_spmv_part_impl(rsp_handle_t h, const void *alpha, rsp_spmat_t mat, const void *d_x,
                            const void *beta, void *d_y, rsp_datatype_t compute_type,
                            void *d_buffer, int part) {
     if (part < 0 || part > 2) return RSP_STATUS_INVALID_VALUE;
@@ -768,7 +768,7 @@ struct rsp_spmv_batch {
     }
 };
 
-rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t *mats,
+static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const rsp_spmat_t *mats,
                                    const void *const *d_x, void *const *d_y,
                                    void *const *d_buffers, rsp_datatype_t compute_type,
                                    int part, rsp_spmv_batch_t *batch) {
@@ -784,8 +784,6 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         if (!A) return RSP_STATUS_INVALID_VALUE;
         if (A->type != compute_type) return RSP_STATUS_NOT_SUPPORTED;
         if (A->rows > 0 && (!d_y[j] || (A->cols > 0 && !d_x[j]))) return RSP_STATUS_INVALID_VALUE;
-        for (int q = 0; q < j; q++)  // a matrix's long-row tickets serve one launch slot
-            if (mats[q] == A) return RSP_STATUS_INVALID_VALUE;
         if (!A->planned || A->plan_type != compute_type) {
             rsp_status_t st = spmv_plan(h, A, compute_type);
             if (st != RSP_STATUS_SUCCESS) return st;
@@ -801,13 +799,18 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
     // full tiles, and spread only when the launch's tiles together do not
     // fill the resident slots (each matrix over its nnz share of them).
     // Long rows and their partial slots are the same in every spread of a
-    // matrix, so the partials stay in d_buffers[j].
+    // matrix; the batch keeps its own partials and tickets per member, so a
+    // matrix may appear in several batches and several times in one (the
+    // same A with several right-hand sides), and a batch never shares
+    // tickets with single calls of its matrices.
     const int64_t R = spmv_resident_tiles(h, compute_type);
     const bool spread_ok = !(h->spmv_variant & 16), c16_ok = !(h->spmv_variant & 32);
     rsp_an::hvec<TilePlan> plans((size_t)count);
     // layout: per launch [entries | tiles | tile column bases | long rows |
-    // 16-bit column offsets of each matrix], each 16-B aligned
-    struct Span { int first, count; size_t off_e, off_t, off_c, off_l; rsp_an::hvec<size_t> off_16; };
+    // 16-bit column offsets of each matrix | long-row partials and tickets of
+    // each matrix (zeroed)], each 16-B aligned
+    struct Span { int first, count; size_t off_e, off_t, off_c, off_l; rsp_an::hvec<size_t> off_16, off_p; };
+    size_t part_lo = SIZE_MAX, part_hi = 0;  // the partials' byte range (zeroed after the copy)
     rsp_an::hvec<Span> spans;
     size_t bytes = 0;
     auto tile_range = [part](const TilePlan &p, int *t0, int *t1) {
@@ -815,7 +818,7 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         *t1 = part == 1 ? p.nint : (int)p.blocks.size();
     };
     for (int first = 0; first < count; first += rsp::kSpmvBatchMax) {
-        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, {}};
+        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, {}, {}};
         rsp_an::hvec<rsp_an::hvec<int>> rps((size_t)sp.count), cis((size_t)sp.count);
         int64_t nt_full = 0, nnz_all = 0;
         for (int q = 0; q < sp.count; q++) {
@@ -862,6 +865,15 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
             sp.off_16.push_back(bytes);
             bytes += (plans[first + q].c16.size() * sizeof(uint16_t) + 15) & ~(size_t)15;
         }
+        for (int q = 0; q < sp.count; q++) {
+            sp.off_p.push_back(bytes);
+            const size_t pb = (size_t)plans[first + q].nslots * 2 * elem_size(compute_type);
+            if (pb > 0) {
+                part_lo = std::min(part_lo, bytes);
+                part_hi = bytes + pb;
+            }
+            bytes += (pb + 15) & ~(size_t)15;
+        }
         spans.push_back(sp);
     }
     if (bytes > 0) RSP_CHECK_HIP(hipMalloc(&b->d_mem, bytes));
@@ -879,7 +891,6 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         for (int q = 0; q < sp.count; q++) {
             rsp_spmat_t A = mats[sp.first + q];
             const TilePlan &p = plans[sp.first + q];
-            const char *buf = (const char *)A->d_plan;  // its long-row partials and tickets
             int t0, t1;
             tile_range(p, &t0, &t1);
             const int nlq = part == 1 ? 0 : (int)p.longrows.size();
@@ -889,7 +900,7 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
             e.vals = A->vals;
             e.x = d_x[sp.first + q];
             e.y = d_y[sp.first + q];
-            e.partials = (void *)(buf + A->off_part);
+            e.partials = (void *)((char *)b->d_mem + sp.off_p[q]);  // this member's own
             e.cidx = (const unsigned short *)((char *)b->d_mem + sp.off_16[q]);
             e.cmax = A->cols > 0 ? (int)(A->cols - 1) : 0;
             e.nnz = A->nnz_s;
@@ -919,6 +930,8 @@ rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t 
         b->launches.push_back(a);
     }
     if (bytes > 0) RSP_CHECK_HIP(hipMemcpy(b->d_mem, host.data(), bytes, hipMemcpyHostToDevice));
+    // long-row tickets start (and stay) at 0
+    if (part_hi > part_lo) RSP_CHECK_HIP(hipMemset((char *)b->d_mem + part_lo, 0, part_hi - part_lo));
     for (int j = 0; j < count; j++) {
         b->mats.push_back(mats[j]);
         b->plan_gen.push_back(mats[j]->plan_gen);
@@ -1379,7 +1392,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     return RSP_STATUS_SUCCESS;
 }
 
-rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_offsets,
+static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const int *d_row_offsets,
                                const int *d_col_ind, rsp_ilu0_info_t f) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     // diagnostics: RSP_ILU_TIMING=1 prints the wall time of each analysis phase
@@ -1428,17 +1441,19 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
     // their per-term half is built on the device after the upload
     // (RSP_ILU_HOST_TERMS=1: on the host, as rsp_ilu0_analysis_host does; A/B)
     const bool dev_terms = n > 0 && !env_int("RSP_ILU_HOST_TERMS", 0);
-    std::thread solves;
+    // (declared after rp, ci, hp: destroyed - joined - before them if the
+    // factor plan throws)
+    std::unique_ptr<rsp_an::Task> solves;
     rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph, [&] {
-        solves = std::thread([&] {
+        solves.reset(new rsp_an::Task([&] {
             if (dev_terms)
                 rsp_an::plan_solves_rows(rp.data(), ci.data(), *hp);
             else
                 rsp_an::plan_solves(rp.data(), ci.data(), *hp);
-        });
+        }));
     });
     if (st == RSP_STATUS_SUCCESS) rsp_an::plan_factor(rp.data(), ci.data(), slot_cap_ints(), *hp);
-    if (solves.joinable()) solves.join();
+    if (solves) solves->join();  // rethrows the solve plans' exception
     if (st != RSP_STATUS_SUCCESS) {
         ilu_free_device(f);
         return st;
@@ -1484,10 +1499,13 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_
         tl.kind = 0;
         tl.rp = d_row_offsets;
         tl.ci = d_col_ind;
+        ar.up((int **)&tl.lpos, hp->lpos);  // the split term order (rsp_an::split_terms)
+        ar.up((int **)&tl.ne, hp->ne_l);
         tt.kind = 1;
         ar.up((int **)&tt.ltp, hp->ltp);
         ar.up((int **)&tt.lts, hp->lts);
         ar.up((int **)&tt.ltc, hp->ltc);
+        ar.up((int **)&tt.ne, hp->ne_lt);
     } else {
         dag_upload(ar, f->L, hp->L);
         dag_upload(ar, f->LT, hp->LT);
@@ -1599,7 +1617,7 @@ static rsp_status_t ilu_plan_u(rsp_handle_t h, rsp_ilu0_info *f) {
     return RSP_STATUS_SUCCESS;
 }
 
-rsp_status_t rsp_ilu0_analysis_host(int n, const int *row_offsets, const int *col_ind,
+static rsp_status_t rsp_ilu0_analysis_host_impl(int n, const int *row_offsets, const int *col_ind,
                                     int *levels_lower, int *levels_upper, uint64_t *digest,
                                     double *phase_ms) {
     rsp_an::Phases ph;
@@ -1718,7 +1736,7 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const rsp_an::hvec
     return p;
 }
 
-rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
+static rsp_status_t rsp_ilu0_factor_impl(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
                              void *d_values) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     if (!f || !f->analysed || (f->nnz_s > 0 && !d_values)) return RSP_STATUS_INVALID_VALUE;
@@ -1823,6 +1841,7 @@ static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alp
     a.trace_clk = 0;
     a.wave_lds = env_int("RSP_ILU_WAVE_LDS", 1);
     a.narrow_waves = std::min(std::max(env_int("RSP_ILU_NARROW_WAVES", 4), 1), rsp::kThinThreads / 64);
+    a.narrow_split = env_int("RSP_ILU_NARROW_SPLIT", 1) != 0;
     a.flow = env_int("RSP_ILU_FLOW", 1) != 0;
     // every workgroup of a flow launch must be resident at once (an item waits
     // for items of lower index only, and workgroups take items in index
@@ -1844,7 +1863,7 @@ static void trsv_begin(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp::TrsvArg
     a.fc = flow_ctl(f, 2 + which, ++g);
 }
 
-rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                  rsp_ilu0_info_t f, rsp_datatype_t value_type,
                                  const void *d_values, const void *d_x, void *d_y) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
@@ -1899,7 +1918,7 @@ rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void 
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
 }
 
-rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f,
+static rsp_status_t rsp_trsv_upper_impl(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f,
                             rsp_datatype_t value_type, const void *d_values, const void *d_x,
                             void *d_y) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
@@ -1918,6 +1937,86 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f
     else
         e = h->ftz ? rsp_k_ftz::trsv_upper_f32(a, h->stream) : rsp_k::trsv_upper_f32(a, h->stream);
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+
+}  // extern "C"
+
+// C-ABI entry points never let a C++ exception out (std::bad_alloc from the
+// host plans' pools, say): it becomes a status, after `cleanup`.
+template <typename F, typename C>
+static rsp_status_t guarded(F body, C cleanup) {
+    try {
+        return body();
+    } catch (const std::bad_alloc &) {
+        cleanup();
+        return RSP_STATUS_ALLOC_FAILED;
+    } catch (...) {
+        cleanup();
+        return RSP_STATUS_INTERNAL_ERROR;
+    }
+}
+
+extern "C" {
+
+
+rsp_status_t rsp_spmv_buffer_size(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                  rsp_spmat_t mat, const void *beta, rsp_datatype_t compute_type,
+                                  size_t *buffer_size) {
+    return guarded([&] { return rsp_spmv_buffer_size_impl(h, op, alpha, mat, beta, compute_type, buffer_size); }, [] {});
+}
+
+rsp_status_t rsp_spmv_preprocess(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                 rsp_spmat_t mat, const void *d_x, const void *beta, void *d_y,
+                                 rsp_datatype_t compute_type, void *d_buffer) {
+    return guarded([&] { return rsp_spmv_preprocess_impl(h, op, alpha, mat, d_x, beta, d_y, compute_type, d_buffer); }, [] {});
+}
+
+rsp_status_t rsp_spmv(rsp_handle_t h, rsp_operation_t op, const void *alpha, rsp_spmat_t mat,
+                      const void *d_x, const void *beta, void *d_y, rsp_datatype_t compute_type,
+                      void *d_buffer) {
+    return guarded([&] { return rsp_spmv_impl(h, op, alpha, mat, d_x, beta, d_y, compute_type, d_buffer); }, [] {});
+}
+
+rsp_status_t rsp_spmv_part(rsp_handle_t h, const void *alpha, rsp_spmat_t mat, const void *d_x,
+                           const void *beta, void *d_y, rsp_datatype_t compute_type,
+                           void *d_buffer, int part) {
+    return guarded([&] { return rsp_spmv_part_impl(h, alpha, mat, d_x, beta, d_y, compute_type, d_buffer, part); }, [] {});
+}
+
+rsp_status_t rsp_spmv_batch_create(rsp_handle_t h, int count, const rsp_spmat_t *mats,
+                                   const void *const *d_x, void *const *d_y,
+                                   void *const *d_buffers, rsp_datatype_t compute_type,
+                                   int part, rsp_spmv_batch_t *batch) {
+    return guarded([&] { return rsp_spmv_batch_create_impl(h, count, mats, d_x, d_y, d_buffers, compute_type, part, batch); }, [] {});
+}
+
+rsp_status_t rsp_ilu0_analysis(rsp_handle_t h, int n, int nnz, const int *d_row_offsets,
+                               const int *d_col_ind, rsp_ilu0_info_t f) {
+    return guarded([&] { return rsp_ilu0_analysis_impl(h, n, nnz, d_row_offsets, d_col_ind, f); }, [&] { if (f) { ilu_free_device(f); f->analysed = 0; } });
+}
+
+rsp_status_t rsp_ilu0_analysis_host(int n, const int *row_offsets, const int *col_ind,
+                                    int *levels_lower, int *levels_upper, uint64_t *digest,
+                                    double *phase_ms) {
+    return guarded([&] { return rsp_ilu0_analysis_host_impl(n, row_offsets, col_ind, levels_lower, levels_upper, digest, phase_ms); }, [] {});
+}
+
+rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
+                             void *d_values) {
+    return guarded([&] { return rsp_ilu0_factor_impl(h, f, value_type, d_values); }, [] {});
+}
+
+rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                 rsp_ilu0_info_t f, rsp_datatype_t value_type,
+                                 const void *d_values, const void *d_x, void *d_y) {
+    return guarded([&] { return rsp_trsv_lower_unit_impl(h, op, alpha, f, value_type, d_values, d_x, d_y); }, [] {});
+}
+
+rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f,
+                            rsp_datatype_t value_type, const void *d_values, const void *d_x,
+                            void *d_y) {
+    return guarded([&] { return rsp_trsv_upper_impl(h, alpha, f, value_type, d_values, d_x, d_y); }, [] {});
 }
 
 }  // extern "C"

@@ -367,6 +367,7 @@ struct TrsvArgs {
     int trace_clk;              // level stamps in shader clock cycles (s_memtime) instead
     int wave_lds;               // fat-level wave rows: chain on LDS broadcast operands (RSP_ILU_WAVE_LDS)
     int narrow_waves;           // thin runs: waves sharing a narrow run, levels round-robin (RSP_ILU_NARROW_WAVES)
+    int narrow_split;           // L / L^T narrow runs: one wave, early sums under the late loads (RSP_ILU_NARROW_SPLIT)
     int flow;                   // run flow segments persistently (RSP_ILU_FLOW, default 1)
     int flow_grid;              // flow launch: 256-thread workgroups (RSP_ILU_FLOW_WPC waves per CU)
     int flow_cus;               // CUs of the device (caps a flow grid)
@@ -434,10 +435,10 @@ hipError_t ilu_an_stages(int n, int maxlen, const int *rp, const int *ci, const 
 // The per-term half of a solve plan (ilu_analysis.cpp solve_plan_terms, same
 // arrays bit for bit) from its per-row half already on the device: flat term
 // positions and y sources, the thin runs' window remap, row records, y
-// indices, staged terms and the chunks' staged ranges. Row i's terms: kind 0
-// (L) positions [rp[i], dpos[i]) (column ci[p]); kind 1 (L^T) entries
-// [ltp[i], ltp[i+1]) of the transposed lower part (position lts[q], column
-// ltc[q]). stg holds room for every thin-run term (>= 1 entry); scratch:
+// indices, staged terms and the chunks' staged ranges. Row i's terms, in the
+// split order (early, then late): kind 0 (L) positions lpos[rp[i] .. dpos[i])
+// (column ci[p]); kind 1 (L^T) entries [ltp[i], ltp[i+1]) of the transposed
+// lower part (position lts[q], column ltc[q]); ne[i] of them early. stg holds room for every thin-run term (>= 1 entry); scratch:
 // slot_of (n ints), nst / nst_ptr (nch + 1 ints each), scan (temp bytes of
 // ilu_an_scan over nch + 1). nstg_out (device, may be null): staged terms.
 struct SolveTermsArgs {
@@ -446,6 +447,8 @@ struct SolveTermsArgs {
     const int *ptr;  // level pointers
     const int *rp, *ci, *dpos;
     const int *ltp, *lts, *ltc;
+    const int *lpos;  // kind 0: the split term order (position of term o of row i at lpos[rp[i] + o])
+    const int *ne;    // per row: its early terms (split order; ilu_analysis.cpp split_padded)
     rsp::LevelChunk *chunks;
     const int *cbase;  // per chunk: its thin run's first slot
     int *tpos, *src, *sid;

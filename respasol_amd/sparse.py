@@ -128,6 +128,26 @@ class SpMat:
                            _ptr(y), _DT[self.dtype], _ptr(self.buffer)), "rsp_spmv")
         return y
 
+    def bind(self, x: torch.Tensor, y: torch.Tensor, alpha: float = 1.0, beta: float = 0.0):
+        """The call y = alpha*A*x + beta*y with its C arguments converted once:
+        returns a no-argument callable that issues exactly one rsp_spmv (the
+        C driver's per-call cost, without the per-call Python argument
+        conversion of spmv(); for timing loops of many short calls)."""
+        if x.dtype != self.dtype or x.numel() < self.n or y.dtype != self.dtype or y.numel() < self.m:
+            raise ValueError("x / y have the wrong dtype or length")
+        a, b = _scalar(alpha, self.dtype), _scalar(beta, self.dtype)
+        args = (self.handle.ptr, _lib.OP_N, C.byref(a), self._mat, _ptr(x), C.byref(b), _ptr(y),
+                _DT[self.dtype], _ptr(self.buffer))
+        keep = (a, b, x, y)  # the scalars and tensors the pointers refer to
+        fn = rsp.rsp_spmv
+
+        def call():
+            st = fn(*args)
+            if st:
+                check(st, "rsp_spmv")
+        call.keep = keep
+        return call
+
     def set_local_cols(self, ncols_local: int) -> None:
         """Split the schedule for halo overlap (rsp_spmat_set_local_cols): tiles
         reading columns < ncols_local only (the rank's own x) run as part 1."""

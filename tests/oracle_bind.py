@@ -34,7 +34,7 @@ def _load():
     lib.oracle_ilu0_f64.restype = C.c_int
     lib.oracle_ilu0_f32.argtypes = [C.c_int, ip, ip, vp, ip, C.c_int]
     lib.oracle_ilu0_f32.restype = C.c_int
-    for n in ("lower_n", "lower_t", "upper"):
+    for n in ("lower_n", "lower_t", "upper", "lower_n_split", "lower_t_split"):
         f = getattr(lib, f"oracle_trsv_{n}_f64")
         f.argtypes = [C.c_int, ip, ip, vp, C.c_double, vp, vp]
         f.restype = None
@@ -95,7 +95,13 @@ def ilu0(rowptr, colidx, vals, ftz=False):
 
 
 def trsv(kind, rowptr, colidx, vals, x, alpha=1.0, ftz=False):
-    """kind in {'lower_n', 'lower_t', 'upper'}."""
+    """kind in {'lower_n', 'lower_t', 'upper', 'lower_n_ref', 'lower_t_ref'}.
+    'lower_n' / 'lower_t' are the canonical order of the MI355X plans (the
+    split order: a row's terms from the level just below it applied last,
+    rsp_oracle.c ORACLE_TRSV_SPLIT); '*_ref' the reference's own order (L:
+    column ascending; L^T: the column sweep)."""
+    kind = {"lower_n": "lower_n_split", "lower_t": "lower_t_split",
+            "lower_n_ref": "lower_n", "lower_t_ref": "lower_t"}.get(kind, kind)
     rp = np.ascontiguousarray(rowptr, np.int32)
     ci = np.ascontiguousarray(colidx, np.int32)
     v = np.ascontiguousarray(vals)

@@ -220,3 +220,30 @@ def test_batch_many_chunk_hub_rows(monkeypatch, variant):
             B.close()
     finally:
         h.close()
+
+
+def test_batch_repeats_a_matrix_with_own_tickets(handle):
+    """The same matrix several times in one batch (one A, several right-hand
+    sides) and in a second batch: each batch member has its own long-row
+    partials and tickets, so every y carries the bits of a
+    single rsp_spmv of that x — here on a circuit surrogate whose hub rows
+    are chunked (last-arriving-chunk tickets)."""
+    import oracle_bind as ob
+    A = csr.surrogate("ASIC_320ks", 0.3)
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
+    M = SpMat(handle, rp, ci, va, A.n)
+    xs = [torch.from_numpy(csr.dlarnv(1, [0, 0, k, 1], A.n)[0]).cuda() for k in range(3)]
+    ys = [torch.empty(A.m, dtype=torch.float64, device="cuda") for _ in range(3)]
+    ys2 = [torch.empty(A.m, dtype=torch.float64, device="cuda") for _ in range(2)]
+    B1 = SpmvBatch(handle, [M, M, M], xs, ys)
+    B2 = SpmvBatch(handle, [M, M], xs[:2], ys2)
+    for _ in range(4):  # tickets return to 0 after every launch
+        B1.run()
+        B2.run()
+        M.spmv(xs[2])
+    torch.cuda.synchronize()
+    for k in range(3):
+        ref = ob.spmv(A.rowptr, A.colidx, A.values, xs[k].cpu().numpy(), order="canon")
+        assert same_bits(ref, ys[k].cpu().numpy()), k
+        if k < 2:
+            assert same_bits(ref, ys2[k].cpu().numpy()), k
