@@ -808,9 +808,8 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
     rsp_an::hvec<TilePlan> plans((size_t)count);
     // layout: per launch [entries | tiles | tile column bases | long rows |
     // 16-bit column offsets of each matrix | long-row partials and tickets of
-    // each matrix (zeroed)], each 16-B aligned
+    // each matrix (zero)], each 16-B aligned
     struct Span { int first, count; size_t off_e, off_t, off_c, off_l; rsp_an::hvec<size_t> off_16, off_p; };
-    size_t part_lo = SIZE_MAX, part_hi = 0;  // the partials' byte range (zeroed after the copy)
     rsp_an::hvec<Span> spans;
     size_t bytes = 0;
     auto tile_range = [part](const TilePlan &p, int *t0, int *t1) {
@@ -868,10 +867,6 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
         for (int q = 0; q < sp.count; q++) {
             sp.off_p.push_back(bytes);
             const size_t pb = (size_t)plans[first + q].nslots * 2 * elem_size(compute_type);
-            if (pb > 0) {
-                part_lo = std::min(part_lo, bytes);
-                part_hi = bytes + pb;
-            }
             bytes += (pb + 15) & ~(size_t)15;
         }
         spans.push_back(sp);
@@ -929,9 +924,9 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
         a.longs_at.begin[sp.count] = nl;
         b->launches.push_back(a);
     }
+    // the image is value-initialised, so every member's long-row partials and
+    // tickets go up as 0 (tickets start, and stay, at 0 between launches)
     if (bytes > 0) RSP_CHECK_HIP(hipMemcpy(b->d_mem, host.data(), bytes, hipMemcpyHostToDevice));
-    // long-row tickets start (and stay) at 0
-    if (part_hi > part_lo) RSP_CHECK_HIP(hipMemset((char *)b->d_mem + part_lo, 0, part_hi - part_lo));
     for (int j = 0; j < count; j++) {
         b->mats.push_back(mats[j]);
         b->plan_gen.push_back(mats[j]->plan_gen);
