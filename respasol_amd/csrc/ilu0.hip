@@ -1691,6 +1691,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
 #pragma unroll
             for (int j = 0; j < G; ++j) y[j] = yb(id.v[j]);
         };
+        auto nlate = [&](const Lev &v) { return (v.R.g >> 16) - v.eg; };
         Lev c = lev(q0), n = lev(q0 + 1);
         // early partial of level q0 (its early producers are done)
         T e = c.R.x;
@@ -1698,28 +1699,38 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             const int gg = early_grp(c, gi);
             e = group_fma(e, lval[gg], lidx[gg]);
         }
-        TermGroup<T, G> cLV = lval[late_grp(c, 0)];
+        // a level's first two late groups are read ahead (values and y
+        // indices do not depend on any y), and their y are loaded together
+        // right after the previous level's stores: one LDS round trip on the
+        // critical path for rows of up to 2 G late terms
+        bool c2 = __ballot(nlate(c) >= 2) != 0;
+        TermGroup<T, G> cLV = lval[late_grp(c, 0)], cLV1 = lval[late_grp(c, 1)];
         TermIds<G> nEI = lidx[early_grp(n, 0)];
         TermGroup<T, G> nEV = lval[early_grp(n, 0)];
-        T cy[G];
+        T cy[G], cy1[G];
         {
-            const TermIds<G> cLI = lidx[late_grp(c, 0)];
+            const TermIds<G> cLI = lidx[late_grp(c, 0)], cLI1 = lidx[late_grp(c, 1)];
             ygroup(cy, cLI);
+            ygroup(cy1, cLI1);
         }
         for (int q = q0; q < q1; ++q) {
             // early y of level q+1 (producers two or more levels back)
             T ny[G];
             ygroup(ny, nEI);
-            // records of level q+2, the late group 0 of level q+1
+            // records of level q+2, the late groups 0 and 1 of level q+1
             const Lev m = lev(q + 2);
-            const int nlg = late_grp(n, 0);
-            const TermIds<G> nLI = lidx[nlg];
-            const TermGroup<T, G> nLV = lval[nlg];
+            const bool n2 = __ballot(nlate(n) >= 2) != 0;
+            const int nlg = late_grp(n, 0), nlg1 = late_grp(n, 1);
+            const TermIds<G> nLI = lidx[nlg], nLI1 = lidx[nlg1];
+            const TermGroup<T, G> nLV = lval[nlg], nLV1 = lval[nlg1];
             // level q: the late part (critical path)
             T s = fma_group(e, cLV, cy);
-            for (int gi = 1; __ballot(gi < (c.R.g >> 16) - c.eg); ++gi) {
-                const int gg = late_grp(c, gi);
-                s = group_fma(s, lval[gg], lidx[gg]);
+            if (c2) {
+                s = fma_group(s, cLV1, cy1);
+                for (int gi = 2; __ballot(gi < nlate(c)); ++gi) {
+                    const int gg = late_grp(c, gi);
+                    s = group_fma(s, lval[gg], lidx[gg]);
+                }
             }
             put(c.R.out, s);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -1727,6 +1738,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
             // late y of level q+1 (after level q's stores)
             ygroup(cy, nLI);
+            if (n2) ygroup(cy1, nLI1);
             // level q+1's early partial, under those loads
             T e2 = fma_group(n.R.x, nEV, ny);
             for (int gi = 1; __ballot(gi < n.eg); ++gi) {
@@ -1740,7 +1752,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             e = e2;
             c = n;
             n = m;
+            c2 = n2;
             cLV = nLV;
+            cLV1 = nLV1;
         }
     };
     // Narrow run on K waves (a.narrow_waves): wave w computes levels q0 + w,

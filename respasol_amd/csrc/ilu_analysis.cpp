@@ -1075,6 +1075,12 @@ static void split_terms(const int *rp, const int *ci, IluHostPlan &hp) {
     hp.lpos.assign((size_t)std::max(hp.nnz_s, 1), 0);
     hp.ne_l.assign((size_t)std::max(n, 1), 0);
     hp.ne_lt.assign((size_t)std::max(n, 1), 0);
+    if (!hp.split) {  // the reference's order: every term "late", none moved
+        pfor(std::max(hp.nnz_s, 1), 1 << 16, [&](long long a, long long b) {
+            for (long long p = a; p < b; p++) hp.lpos[(size_t)p] = (int)p;
+        });
+        return;
+    }
     parallel_rows(n, [&](int r0, int r1) {
         hvec<int> late, late_c;
         for (int i = r0; i < r1; i++) {
@@ -1115,6 +1121,7 @@ static void split_terms(const int *rp, const int *ci, IluHostPlan &hp) {
 
 void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     const int n = hp.n;
+    hp.split = env_int("RSP_ILU_SPLIT", 0) != 0;
     const hvec<int> &dpos = hp.dpos;
     // three independent sequential passes over the strict lower part, run
     // concurrently (each is memory-latency bound; splitting one over threads
@@ -1209,10 +1216,10 @@ static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool
     long long nlo = 0;
     for (int i = 0; i < n; i++) nlo += dpos[(size_t)i] - rp[(size_t)i];
     hp.L.batch = hp.LT.batch = chain_batch(nlo, n);
-    // thin-run term groups: 2 where a row's two parts (split order: early,
-    // late) are short on average (mean chain <= 5 terms: the deep circuits;
-    // their narrow runs take the single-wave split loop, G = 2 only), else 4
-    const int g_dflt = n > 0 && (double)nlo / n <= 5.0 ? 2 : 4;
+    // thin-run term groups: the reference order (default) 2 for DAGs of
+    // short chains (chain_batch), else 4; the split order (RSP_ILU_SPLIT=1)
+    // 2 where a row's two parts are short on average (mean chain <= 5 terms)
+    const int g_dflt = hp.split ? (n > 0 && (double)nlo / n <= 5.0 ? 2 : 4) : (hp.L.batch == 2 ? 2 : 4);
     for (DagHost *d : {&hp.L, &hp.LT})
         d->group = env_int("RSP_ILU_GROUP", g_dflt) == 2 ? 2 : 4;
     auto cnt_l = [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; };

@@ -106,11 +106,15 @@ struct IluHostPlan {
     DagHost L, LT, U;
     // transposed strict lower part (row k: (position of l_jk, j), j descending)
     hvec<int> ltp, lts, ltc;
-    // the solves' SPLIT term order (round 4): a row's terms from the level
-    // just below its own in the DAG ("late") after its other ("early") terms,
-    // each part in the reference's order. L: lpos[rp[i] + o] = position of
-    // the o-th term of row i; L^T: lts / ltc above, permuted per row the same
-    // way; ne_l / ne_lt = early terms per row. lev_l / lev_lt: the levels.
+    // the solves' term order. Default: the reference's (L column ascending,
+    // L^T the column sweep: lpos is the identity, ne_* = 0). RSP_ILU_SPLIT=1
+    // (split = 1; round 4, measured slower): a row's terms from
+    // the level just below its own in the DAG ("late") after its other
+    // ("early") terms, each part in the reference's order. L: lpos[rp[i] + o]
+    // = position of the o-th term of row i; L^T: lts / ltc above, permuted
+    // per row the same way; ne_l / ne_lt = early terms per row. lev_l /
+    // lev_lt: the levels.
+    int split = 0;
     hvec<int> lpos, ne_l, ne_lt, lev_l, lev_lt;
     FacPlan fplan;
     int fac_batch = 8;

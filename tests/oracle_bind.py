@@ -95,12 +95,16 @@ def ilu0(rowptr, colidx, vals, ftz=False):
 
 
 def trsv(kind, rowptr, colidx, vals, x, alpha=1.0, ftz=False):
-    """kind in {'lower_n', 'lower_t', 'upper', 'lower_n_ref', 'lower_t_ref'}.
-    'lower_n' / 'lower_t' are the canonical order of the MI355X plans (the
-    split order: a row's terms from the level just below it applied last,
-    rsp_oracle.c ORACLE_TRSV_SPLIT); '*_ref' the reference's own order (L:
-    column ascending; L^T: the column sweep)."""
-    kind = {"lower_n": "lower_n_split", "lower_t": "lower_t_split",
+    """kind in {'lower_n', 'lower_t', 'upper', 'lower_n_ref', 'lower_t_ref',
+    'lower_n_split', 'lower_t_split'}. '*_ref' is the reference's own order
+    (L: column ascending; L^T: the column sweep), '*_split' the split order
+    (a row's terms from the level just below it applied last, rsp_oracle.c
+    ORACLE_TRSV_SPLIT); 'lower_n' / 'lower_t' follow the product's plan
+    order: the reference's, or the split one where RSP_ILU_SPLIT=1 is set
+    (the analysis knob)."""
+    split = os.environ.get("RSP_ILU_SPLIT", "0") not in ("", "0")
+    kind = {"lower_n": "lower_n_split" if split else "lower_n",
+            "lower_t": "lower_t_split" if split else "lower_t",
             "lower_n_ref": "lower_n", "lower_t_ref": "lower_t"}.get(kind, kind)
     rp = np.ascontiguousarray(rowptr, np.int32)
     ci = np.ascontiguousarray(colidx, np.int32)

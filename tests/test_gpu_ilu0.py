@@ -375,18 +375,22 @@ def test_device_solve_terms_same_plan_under_schedule_knobs(handle, monkeypatch, 
     il.close()
 
 
-@pytest.mark.parametrize("waves,split,group", [(1, 0, 0), (2, 0, 0), (3, 0, 0), (8, 0, 0), (4, 1, 0), (4, 1, 2),
-                                               (4, 1, 4), (4, 0, 2)])
+@pytest.mark.parametrize("waves,order,nsplit,group", [(1, 0, 0, 0), (2, 0, 0, 0), (3, 0, 0, 0), (8, 0, 0, 0),
+                                                      (4, 0, 0, 0), (4, 0, 1, 2), (4, 1, 1, 0), (4, 1, 1, 2),
+                                                      (4, 1, 0, 4), (4, 1, 0, 2)])
 @pytest.mark.parametrize("name,scale", [("dc1", 1.0), ("G2_circuit", 0.5), ("thermomech_TK", 0.5),
                                         ("matrix-new_3", 0.5)])
-def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, split, group, name, scale):
-    """Narrow solve levels of L and L^T in the split order on one wave (early
-    sums under the late loads; the default for term groups of 2), or shared
-    round-robin by 1-8 waves (an LDS counter of completed levels orders
-    them), groups of 2 / 4 / the plan's choice (0): bitwise equal to the
-    oracle (split order) for L, L^T and the U extension, fp64 and fp32."""
+def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, order, nsplit, group, name, scale):
+    """Narrow solve levels of L and L^T shared round-robin by 1-8 waves (an
+    LDS counter of completed levels orders them), or on one wave with the
+    late groups' y loaded together (RSP_ILU_NARROW_SPLIT, early sums under
+    the late loads), in the reference's term order (default) or the split
+    order (RSP_ILU_SPLIT=1), groups of 2 / 4 / the plan's choice (0):
+    bitwise equal to the oracle in that order for L, L^T and the U
+    extension, fp64 and fp32."""
     monkeypatch.setenv("RSP_ILU_NARROW_WAVES", str(waves))
-    monkeypatch.setenv("RSP_ILU_NARROW_SPLIT", str(split))
+    monkeypatch.setenv("RSP_ILU_SPLIT", str(order))
+    monkeypatch.setenv("RSP_ILU_NARROW_SPLIT", str(nsplit))
     if group:
         monkeypatch.setenv("RSP_ILU_GROUP", str(group))
     A = csr.surrogate(name, scale)

@@ -171,8 +171,8 @@ def test_ftz_oracle_flushes_subnormals():
 
 @pytest.mark.parametrize("name,scale", [("dc1", 0.1), ("G2_circuit", 0.1), ("xenon2", 0.03), ("ecology2", 0.02)])
 def test_split_order_solves_within_tolerance(name, scale):
-    """The canonical solve order of the MI355X plans (split: a row's terms
-    from the level just below it last) against the reference's own order
+    """The split solve order (RSP_ILU_SPLIT=1: a row's terms from the level
+    just below it last) against the reference's own order
     (L column ascending, L^T column sweep): same terms, different summation
     order only — normwise within SURVEY 8c's 1e-12 (fp64) and 1e-4 (fp32),
     most entries bitwise."""
@@ -182,7 +182,7 @@ def test_split_order_solves_within_tolerance(name, scale):
     for dt, tol in ((np.float64, 1e-12), (np.float32, 1e-4)):
         vv, xx = v.astype(dt), x.astype(dt)
         for k in ("lower_n", "lower_t"):
-            a = ob.trsv(k, A.rowptr, A.colidx, vv, xx).astype(np.float64)
+            a = ob.trsv(k + "_split", A.rowptr, A.colidx, vv, xx).astype(np.float64)
             b = ob.trsv(k + "_ref", A.rowptr, A.colidx, vv, xx).astype(np.float64)
             assert np.linalg.norm(a - b) <= tol * np.linalg.norm(b)
             assert np.mean(a == b) > 0.5
