@@ -207,6 +207,10 @@ __device__ __forceinline__ void lds_barrier() {
 // one LDS round trip after its producer instead of two (solve 43.5 -> 45.4
 // ms; dc1 4.86 -> 5.62). A narrow level is ~425 cycles (160 ns, dc1,
 // RSP_ILU_TRACE_CLK) and any extra LDS traffic or wake-up delay lands on it.
+// (Mode 1 was removed in round 4 with the other inline-asm ordering.)
+// The counter is published by lds_publish (release) and read here with an
+// acquire fence after the last poll: the HIP memory model orders a wave's y
+// stores before the counter and the waiting wave's y loads after it.
 #ifndef RSP_POLL_MODE
 #define RSP_POLL_MODE 0
 #endif
@@ -214,18 +218,7 @@ __device__ __forceinline__ void lds_barrier() {
 #define RSP_POLL_SLEEP 1
 #endif
 __device__ __forceinline__ void lds_wait_geq(int *p, int want, int near) {
-#if RSP_POLL_MODE == 1
-    const unsigned addr = (unsigned)(size_t)(__attribute__((address_space(3))) int *)p;
-    int a, b;
-    asm volatile("ds_read_b32 %0, %1" : "=v"(a) : "v"(addr) : "memory");
-    for (int it = 0; it < (1 << 25); ++it) {
-        asm volatile("ds_read_b32 %0, %2\n\ts_waitcnt lgkmcnt(1)" : "=&v"(b), "+v"(a) : "v"(addr) : "memory");
-        if (__builtin_amdgcn_readfirstlane(a) >= want) break;
-        asm volatile("ds_read_b32 %0, %2\n\ts_waitcnt lgkmcnt(1)" : "=&v"(a), "+v"(b) : "v"(addr) : "memory");
-        if (__builtin_amdgcn_readfirstlane(b) >= want) break;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#elif RSP_POLL_MODE == 3
+#if RSP_POLL_MODE == 3
     for (int it = 0; it < (1 << 26); ++it) {
         const int c = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -241,6 +234,24 @@ __device__ __forceinline__ void lds_wait_geq(int *p, int want, int near) {
     }
 #endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Publish an LDS counter of completed levels / rounds (lane 0 of the wave
+// that completed them): a workgroup-scope release store, so every LDS store
+// of the wave before it (its y / values) is visible to a wave whose
+// lds_wait_geq has seen the new value. RSP_LDS_RELAXED (A/B builds only): the
+// round-3 form, a relaxed store behind a compiler-only fence, which relied on
+// one wave's LDS operations being performed in order.
+#ifndef RSP_LDS_RELAXED
+#define RSP_LDS_RELAXED 0
+#endif
+__device__ __forceinline__ void lds_publish(int *p, int v, bool leader) {
+#if RSP_LDS_RELAXED
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (leader) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+    if (leader) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
 }
 
 // --------------------------------------------------------------- kernels
@@ -808,8 +819,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
     auto stage = [&](int c, const rsp::RndChunk &ch, const Recs &R, const Pre &P) {
         const int ni = ch.i1 - ch.i0, ns = ch.s1 - ch.s0, np = ch.p1 - ch.p0, nr = ch.r1 - ch.r0;
         const int par = c & 1, cb = par * K;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // earlier chunks' values stored and visible; LDS free
+        __syncthreads();  // earlier chunks' values stored and visible (workgroup scope); LDS free
 #pragma unroll
         for (int j = 0; j < IPT; ++j)
             if (tid + j * NTH < ni) {
@@ -895,8 +905,8 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
     // a wave loads what no value of the run feeds — the first two rounds'
     // item records, initial values a_ij and first four pair indices; then it
     // waits until the segment before its own is complete (an LDS counter of
-    // absolute rounds done, advanced by each segment's wave after its value
-    // stores, in-order LDS), and only then reads operands (divisors, l_ik,
+    // absolute rounds done, published by each segment's wave with a release
+    // store after its value stores, lds_publish), and only then reads operands (divisors, l_ik,
     // u_kj) and runs the fma chains and divisions. While one wave is on its
     // chain, the others have prepared their next levels. Same items, same
     // pairs in the same order, same divisions as the one-wave run: same bits.
@@ -996,9 +1006,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                         wave_order();
                     }
                 }
-                asm volatile("" ::: "memory");  // value stores before the counter (in-order LDS)
-                if (lane == 0)
-                    __hip_atomic_store(&lds_rdone, ch.r0 + s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                lds_publish(&lds_rdone, ch.r0 + s1, lane == 0);  // after the value stores
             }
             sp = s0;
             s0 = s1;
@@ -1493,8 +1501,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     auto stage = [&](int c, int px0, int px1, const rsp::LevelChunk &ch, const Pre &p, const StgY &w) {
         const int nk = ch.k1 - ch.k0, nl = ch.l1 - ch.l0, ns = ch.st1 - ch.st0;
         mark(c, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();  // the previous chunk's levels are done with LDS
+        // the previous chunk's levels are done with LDS, and the y flushed at
+        // earlier switches (global stores of other threads) are ordered before
+        // this chunk's prefetch loads: workgroup-scope release / acquire
+        __syncthreads();
         mark(c, 1);
         const bool flush = tid < px1 - px0;
         const int fi = lrowi[tid];  // read before this thread restages its slot
@@ -1765,9 +1775,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     // the critical part: y loads -> fma chain -> y stores. While one wave is
     // on its critical part, the others prepare their next levels, so a level
     // costs about its critical part alone (one wave did all of it in line).
-    // The counter store follows the y stores of the same wave with no wait:
-    // a wave's LDS operations are performed in order (compiler barrier only),
-    // and a waiting wave issues its y loads after its poll has returned.
+    // The counter is a release store after the wave's y stores (lds_publish)
+    // and the waiting wave's poll ends in an acquire fence, so its y loads
+    // see them (HIP memory model, workgroup scope).
     // Same terms, same order, same fma chain as narrow_run: same bits.
     auto narrow_run_mw = [&](const rsp::LevelChunk &ch, int q0, int q1, int K) {
         const int w = tid >> 6, lane = tid & 63, x0 = ch.x0;
@@ -1797,8 +1807,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             }
             if constexpr (KIND == 2) s = s / ldg[cr];
             put(R.out, s);
-            asm volatile("" ::: "memory");  // y stores before the counter (in-order LDS)
-            if (lane == 0) __hip_atomic_store(&lds_done, L + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            lds_publish(&lds_done, L + 1, lane == 0);  // after the y stores
             if (a.trace && lane == 0 && L < a.trace_cap / 2)  // diagnostics: level end stamps
                 a.trace[a.trace_cap / 2 + L] = a.trace_clk ? clock64() : wall_clock64();
         }

@@ -71,6 +71,9 @@
 #ifndef RSP_PROBE_YSMALL
 #define RSP_PROBE_YSMALL 0  // the short-row y stores aimed at an L2-resident 1024-entry window
 #endif
+#ifndef RSP_RP_SKIP
+#define RSP_RP_SKIP 0  // row-offset loads: skip the instructions no thread of the tile needs (A/B)
+#endif
 #ifndef RSP_PROBE_EMAJOR
 #define RSP_PROBE_EMAJOR 0  // gathers in entry-major lane order (column fetched by ds_bpermute; wrong products)
 #endif
@@ -383,8 +386,17 @@ __device__ __forceinline__ void spmv_tile(
     const int nrows_ld = nrows > 0 ? nrows : 0;  // long-row chunks: r1 < 0
     int rpv[RPQ];
 #pragma unroll
-    for (int q = 0; q < RPQ; ++q)  // unpredicated (clamped) so nothing waits here
+    for (int q = 0; q < RPQ; ++q) {  // unpredicated (clamped) so nothing waits here
+#if RSP_RP_SKIP
+        // a load instruction only where some thread needs it (workgroup-
+        // uniform test on the tile record: a scalar branch, no exec mask)
+        if (q > 0 && q * kSpmvThreads > nrows_ld) {
+            rpv[q] = 0;
+            continue;
+        }
+#endif
         rpv[q] = rowptr[blk.r0 + min(tid + q * kSpmvThreads, nrows_ld)];
+    }
     // vectors may be used unless the tile reaches the last, partial vector
     const bool vec = vector_ok && k1 > k0 && k1 <= (nnz & ~(VW - 1));
     const int kb = vec ? (k0 & ~(VW - 1)) : k0;

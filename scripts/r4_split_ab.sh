@@ -20,6 +20,7 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
             ns1g2) E="RSP_ILU_NARROW_SPLIT=1 RSP_ILU_GROUP=2" ;;
             split) E="RSP_ILU_SPLIT=1 RSP_ILU_NARROW_SPLIT=1" ;;
             r3) P=$PWD/respasol_amd/build/ab/r3/librsp.so ;;
+            p_*) P=$PWD/respasol_amd/build/probe/${v#p_}/librsp.so ;;  # a probe build (make probe)
         esac
         env $E RSP_PROBE_LIB=$P timeout -k 10 300 python scripts/bench_ilu0.py --set "$SET" --fp64-only --reps 5 \
             > "$O/${v}_$r.txt" 2> "$O/${v}_$r.err" || { tail -20 "$O/${v}_$r.err"; exit 1; }
