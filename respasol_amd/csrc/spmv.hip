@@ -71,12 +71,6 @@
 #ifndef RSP_PROBE_YSMALL
 #define RSP_PROBE_YSMALL 0  // the short-row y stores aimed at an L2-resident 1024-entry window
 #endif
-#ifndef RSP_RP_SKIP
-#define RSP_RP_SKIP 0  // row-offset loads: skip the instructions no thread of the tile needs (A/B)
-#endif
-#ifndef RSP_PROBE_EMAJOR
-#define RSP_PROBE_EMAJOR 0  // gathers in entry-major lane order (column fetched by ds_bpermute; wrong products)
-#endif
 #ifndef RSP_PROBE_WALK
 #define RSP_PROBE_WALK 0  // spmv_tiles: each workgroup walks this many consecutive tiles
 #endif
@@ -182,41 +176,15 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
         __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7ffffff0, 0x00020000);
     constexpr int kAux = RSP_GATHER_POL == 1 ? 1 : RSP_GATHER_POL == 2 ? 2 : RSP_GATHER_POL == 3 ? 16 : 0;
 #endif
-#if RSP_PROBE_EMAJOR
-    // diagnostic builds: gather j of a lane takes the column of entry j*64 +
-    // lane of its wave's window (consecutive lanes, consecutive entries),
-    // fetched from the owning lane (ds_bpermute); the product pairs it with
-    // the wrong value (timing of the gather lane order only)
-    const int lane = threadIdx.x & 63;
-#endif
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
             int c;
-#if RSP_PROBE_EMAJOR
-            if constexpr (C16) {
-                const int src = j * (64 / VW) + lane / VW, comp = lane % VW;
-                unsigned int w;
-                if constexpr (VW == 2) {
-                    w = __shfl(__builtin_bit_cast(unsigned int, ch[it]), src, 64);
-                } else {
-                    typedef unsigned int __attribute__((ext_vector_type(2))) U2;
-                    const U2 pk = __builtin_bit_cast(U2, ch[it]);
-                    const unsigned int lo = __shfl(pk[0], src, 64), hi = __shfl(pk[1], src, 64);
-                    w = comp < 2 ? lo : hi;
-                }
-                const int off = (comp & 1) ? (int)(w >> 16) : (int)(w & 0xffff);
-                c = min(cbase + off, cmax);
-            } else {
-                c = ci[it][j];
-            }
-#else
             if constexpr (C16)
                 c = min(cbase + (int)ch[it][j], cmax);
             else
                 c = ci[it][j];
-#endif
 #if RSP_GATHER_POL
             if constexpr (sizeof(T) == 8)
                 xv[it][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr, c * 8, 0, kAux));
@@ -386,17 +354,8 @@ __device__ __forceinline__ void spmv_tile(
     const int nrows_ld = nrows > 0 ? nrows : 0;  // long-row chunks: r1 < 0
     int rpv[RPQ];
 #pragma unroll
-    for (int q = 0; q < RPQ; ++q) {  // unpredicated (clamped) so nothing waits here
-#if RSP_RP_SKIP
-        // a load instruction only where some thread needs it (workgroup-
-        // uniform test on the tile record: a scalar branch, no exec mask)
-        if (q > 0 && q * kSpmvThreads > nrows_ld) {
-            rpv[q] = 0;
-            continue;
-        }
-#endif
+    for (int q = 0; q < RPQ; ++q)  // unpredicated (clamped) so nothing waits here
         rpv[q] = rowptr[blk.r0 + min(tid + q * kSpmvThreads, nrows_ld)];
-    }
     // vectors may be used unless the tile reaches the last, partial vector
     const bool vec = vector_ok && k1 > k0 && k1 <= (nnz & ~(VW - 1));
     const int kb = vec ? (k0 & ~(VW - 1)) : k0;

@@ -16,6 +16,8 @@ tag = os.path.basename(src.rstrip("/"))
 shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, f"{prefix}_kernel_stats.csv"))
 shutil.copy(os.path.join(src, "bench_prof.json"), os.path.join(dst, f"{prefix}_bench_under_rocprof.json"))
 shutil.copy(os.path.join(src, f"{tag}_pmc.json"), os.path.join(dst, f"{prefix}_pmc.json"))
+if os.path.exists(os.path.join(src, f"{tag}_pmc_f32.json")):
+    shutil.copy(os.path.join(src, f"{tag}_pmc_f32.json"), os.path.join(dst, f"{prefix}_pmc_f32.json"))
 if os.path.exists(os.path.join(src, "roofline_check.txt")):
     shutil.copy(os.path.join(src, "roofline_check.txt"), os.path.join(dst, f"{prefix}_roofline_check.txt"))
 with open(os.path.join(src, "stats", "run_kernel_trace.csv")) as f, \

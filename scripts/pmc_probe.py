@@ -16,6 +16,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dirs", nargs="+")
 ap.add_argument("--kernels", default="spmv_tiles_batch<double,spmv_tiles_batch<float")
 ap.add_argument("--out", default="")
+ap.add_argument("--by-grid", action="store_true",
+                help="one entry per kernel and grid size (one matrix each, e.g. --set cage13,Si87H76)")
 args = ap.parse_args()
 kern = args.kernels.split(",")
 vals = {k: {} for k in kern}  # kernel -> counter -> {dispatch: value}
@@ -25,11 +27,17 @@ for d in args.dirs:
             name = r.get("Kernel_Name", "")
             for k in kern:
                 if k in name:
-                    c = vals[k].setdefault(r["Counter_Name"], {})
+                    kk = k
+                    if args.by_grid:
+                        kk = f"{k} grid={r.get('Grid_Size', r.get('Grid_Size_X', ''))}"
+                        vals.setdefault(kk, {})
+                    c = vals[kk].setdefault(r["Counter_Name"], {})
                     disp = (f, int(r["Dispatch_Id"]))
                     c[disp] = c.get(disp, 0.0) + float(r["Counter_Value"])
 out = {}
 for k, cs in vals.items():
+    if not cs:
+        continue
     avg = {}
     for c, dv in cs.items():
         xs = [dv[key] for key in sorted(dv)][1:] or list(dv.values())

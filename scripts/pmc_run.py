@@ -51,7 +51,8 @@ def run_dtype(h, args, dt):
     calib = {"rows": n, "read_bytes": n * (elem + 4 + 4 + elem) - 2 * e16 + 4, "write_bytes": n * elem,
              "launches": 3, "entries_16bit": e16}
     del D, rp, ci, va, x, y
-    names = csr.surrogate_names(1 if args.set == "big" else 0)
+    names = (csr.surrogate_names(1 if args.set == "big" else 0) if args.set in ("big", "moderate")
+             else args.set.split(","))
     mats = []
     for name in names:
         A = csr.surrogate(name)

@@ -48,7 +48,6 @@ PROBES = {
     "ysmall": "-DRSP_PROBE_YSMALL=1",
     "walk2": "-DRSP_PROBE_WALK=2",
     "walk4": "-DRSP_PROBE_WALK=4",
-    "emajor": "-DRSP_PROBE_EMAJOR=1",
 }
 
 
