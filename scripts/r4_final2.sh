@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4 session 2: the full GPU test suite, the driver's bench command, the
+# config-2 bench and the config-3 ILU bench. Each step has its own limit.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/${1:-r04f}
+mkdir -p "$O"
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > "$O/pytest_gpu.txt" 2>&1
+rc=$?; tail -3 "$O/pytest_gpu.txt"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py > "$O/bench_default.json" 2> "$O/bench_default.err" || exit 1
+timeout -k 10 300 python bench.py --workload moderate --no-cpu > "$O/bench_moderate.json" 2> "$O/bench_moderate.err" || exit 1
+timeout -k 10 600 python scripts/bench_ilu0.py --reps 3 --json "$O/ilu_config3.json" > "$O/ilu_config3.txt" 2> "$O/ilu_config3.err" || exit 1
+tail -1 "$O/ilu_config3.txt"
