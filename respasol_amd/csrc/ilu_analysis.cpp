@@ -215,6 +215,10 @@ static void pfor(long long n, long long grain, F f) {
     Pool::get().run(nt, nt, [&](int t) { f(n * t / nt, n * (t + 1) / nt); });
 }
 
+void parallel_for(long long n, long long grain, const std::function<void(long long, long long)> &f) {
+    pfor(n, grain, [&](long long a, long long b) { f(a, b); });
+}
+
 // f(j) for j in [0, n), items handed out dynamically (uneven item costs:
 // levels, segments, chunks); `work` estimates the total cost to size the team.
 template <typename F>

@@ -181,6 +181,10 @@ void plan_u(const int *rp, const int *ci, IluHostPlan &hp);
 // 64-bit digest (FNV-1a) of every array of the plan (tests: identical plans).
 uint64_t digest(const IluHostPlan &hp);
 
+// f(lo, hi) over [0, n) in contiguous blocks of >= grain on the analysis'
+// worker pool (also used by the SpMV planner, rsp_api.cpp make_tile_plan)
+void parallel_for(long long n, long long grain, const std::function<void(long long, long long)> &f);
+
 }  // namespace rsp_an
 
 #endif

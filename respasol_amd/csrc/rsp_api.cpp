@@ -66,8 +66,9 @@ struct rsp_spmat {
     int nblocks, nlong, nslots;
     int nnz_s;                  // rowptr[rows] seen by the planner
     size_t off_long, off_part;  // byte offsets inside d_plan
-    size_t off_cbase, off_cidx;
-    int64_t nnz_c16;            // entries read through 16-bit column offsets
+    size_t off_cbase, off_cidx, off_runs;
+    int64_t nnz_c16;            // entries read through 16-bit column offsets or slot indices
+    int64_t nnz_staged;         // ... of which in staged tiles (x staged in LDS)
     int64_t local_cols;         // rsp_spmat_set_local_cols (-1: not split)
     int nint;                   // interior tiles at the front of the schedule
     unsigned long long plan_gen;  // unique per plan / value rebind (batch staleness key)
@@ -317,17 +318,18 @@ static SpmvBounds spmv_bounds(int64_t rows, int64_t nnz, int cap) {
 }
 
 // Workspace: [tiles | long rows | chunk partials | per-tile column base |
-// 16-bit column offsets (2 B per stored entry)].
+// 16-bit column offsets (2 B per stored entry) | staged tiles' runs].
 struct SpmvLayout {
-    size_t off_long, off_part, off_cbase, off_cidx, bytes;
+    size_t off_long, off_part, off_cbase, off_cidx, off_runs, bytes;
 };
-static SpmvLayout spmv_layout(const SpmvBounds &b, size_t elem, int64_t nnz) {
+static SpmvLayout spmv_layout(const SpmvBounds &b, size_t elem, int64_t nnz, size_t run_ints = 0) {
     SpmvLayout l;
     l.off_long = align256(b.nblocks * sizeof(SpmvBlock));
     l.off_part = l.off_long + align256(b.nlong * sizeof(SpmvLongRow));
     l.off_cbase = l.off_part + align256(b.nslots * 2 * elem);  // value + ticket per slot
     l.off_cidx = l.off_cbase + align256(b.nblocks * sizeof(int));
-    l.bytes = l.off_cidx + align256((size_t)std::max<int64_t>(nnz, 0) * sizeof(uint16_t));
+    l.off_runs = l.off_cidx + align256((size_t)std::max<int64_t>(nnz, 0) * sizeof(uint16_t));
+    l.bytes = l.off_runs + align256(run_ints * sizeof(int));
     return l;
 }
 
@@ -444,7 +446,9 @@ struct TilePlan {
     int nslots = 0, nint = 0;
     rsp_an::hvec<int> cbase;
     rsp_an::hvec<uint16_t> c16;
-    int64_t nnz_c16 = 0;
+    rsp_an::hvec<int> runs;  // staged tiles' run descriptors (int pairs), SpmvArgs::runs
+    int64_t nnz_c16 = 0;     // entries read through 16-bit offsets or slot indices
+    int64_t nnz_staged = 0;  // ... of which in staged tiles
 };
 
 // spread > 0: a plan of fewer tiles than `spread` (the resident workgroup
@@ -454,7 +458,7 @@ struct TilePlan {
 // the same long rows and partial slots.
 static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_bound,
                            rsp_datatype_t type, int64_t spread, int64_t local_cols, bool use_c16,
-                           TilePlan &p, int row_align = 1) {
+                           TilePlan &p, int row_align = 1, bool use_stage = true) {
     const int chunk = chunk_cap(type);
     const int cap = tile_cap(type);
     const int align = row_align;
@@ -494,25 +498,85 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
     }
     // 16-bit column offsets: a tile whose columns span < 65536 reads
     // col = cbase + off (2 B per entry instead of 4; the int32 colidx is not
-    // read for it).
+    // read for it). Staged tiles (round 4, spmv.hip stream_products_staged):
+    // where the tile's distinct columns are few (at most kStageSlots, at most
+    // RSP_SPMV_STAGE_PCT % of its entries, default 60) in at most kStageRuns
+    // contiguous runs, its 16-bit values are instead the entries' slots in the
+    // sorted list of those columns, and the runs ({first column, first slot},
+    // then {0, slots}) go to `runs`. Tiles are planned in parallel.
     const int64_t nnz_s = m > 0 ? rp[(size_t)m] : 0;
     p.cbase.assign(p.blocks.size(), -1);
     p.c16.clear();
+    p.runs.clear();
     p.nnz_c16 = 0;
+    p.nnz_staged = 0;
     if (use_c16 && nnz_s > 0 && nnz_s <= nnz_bound) {
         p.c16.assign((size_t)nnz_s, 0);
-        for (size_t t = 0; t < p.blocks.size(); t++) {
-            const SpmvBlock &bk = p.blocks[t];
-            if (bk.k1 <= bk.k0) continue;
-            int lo = ci[(size_t)bk.k0], hi = lo;
-            for (int k = bk.k0 + 1; k < bk.k1; k++) {
-                lo = std::min(lo, ci[(size_t)k]);
-                hi = std::max(hi, ci[(size_t)k]);
+        const long long nt = (long long)p.blocks.size();
+        const int ucap = type == RSP_R_64F ? SpmvTile<double>::kStageSlots : SpmvTile<float>::kStageSlots;
+        const long long pct = std::min(std::max(env_int("RSP_SPMV_STAGE_PCT", 60), 0), 100);
+        std::vector<std::vector<int>> truns(use_stage ? (size_t)nt : 0);
+        std::atomic<int64_t> n16{0}, nst{0};
+        rsp_an::parallel_for(nt, 64, [&](long long t0, long long t1) {
+            std::vector<int> cols;
+            int64_t c16n = 0, stn = 0;
+            for (long long t = t0; t < t1; t++) {
+                const SpmvBlock &bk = p.blocks[(size_t)t];
+                if (bk.k1 <= bk.k0) continue;
+                int lo = ci[(size_t)bk.k0], hi = lo;
+                for (int k = bk.k0 + 1; k < bk.k1; k++) {
+                    lo = std::min(lo, ci[(size_t)k]);
+                    hi = std::max(hi, ci[(size_t)k]);
+                }
+                if (hi - lo > 65535) continue;
+                const int len = bk.k1 - bk.k0;
+                c16n += len;
+                if (use_stage && bk.r1 >= 0) {  // (long-row chunks keep the offsets)
+                    cols.assign(ci + bk.k0, ci + bk.k1);
+                    std::sort(cols.begin(), cols.end());
+                    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+                    const int U = (int)cols.size();
+                    int R = 1;
+                    for (int u = 1; u < U; u++) R += cols[(size_t)u] != cols[(size_t)u - 1] + 1;
+                    if (U <= ucap && R <= rsp::kStageRuns && 100LL * U <= pct * len) {
+                        std::vector<int> &r = truns[(size_t)t];
+                        r.reserve(2 * (size_t)(R + 1));
+                        for (int u = 0; u < U; u++)
+                            if (u == 0 || cols[(size_t)u] != cols[(size_t)u - 1] + 1) {
+                                r.push_back(cols[(size_t)u]);
+                                r.push_back(u);
+                            }
+                        r.push_back(0);
+                        r.push_back(U);
+                        for (int k = bk.k0; k < bk.k1; k++)
+                            p.c16[(size_t)k] = (uint16_t)(std::lower_bound(cols.begin(), cols.end(), ci[(size_t)k]) -
+                                                          cols.begin());
+                        stn += len;
+                        continue;
+                    }
+                }
+                p.cbase[(size_t)t] = lo;
+                for (int k = bk.k0; k < bk.k1; k++) p.c16[(size_t)k] = (uint16_t)(ci[(size_t)k] - lo);
             }
-            if (hi - lo > 65535) continue;
-            p.cbase[t] = lo;
-            p.nnz_c16 += bk.k1 - bk.k0;
-            for (int k = bk.k0; k < bk.k1; k++) p.c16[(size_t)k] = (uint16_t)(ci[(size_t)k] - lo);
+            n16 += c16n;
+            nst += stn;
+        });
+        p.nnz_c16 = n16;
+        p.nnz_staged = nst;
+        if (use_stage) {  // descriptors concatenated in tile order; cbase = -2 - (pair offset << 8 | runs)
+            for (size_t t = 0; t < truns.size(); t++) {
+                const std::vector<int> &r = truns[t];
+                if (r.empty()) continue;
+                const int64_t off = (int64_t)p.runs.size() / 2;
+                const int nr = (int)r.size() / 2 - 1;
+                if (off >= (1LL << 22)) {  // (encoding range; never reached on real matrices)
+                    p.nnz_c16 -= p.blocks[t].k1 - p.blocks[t].k0;
+                    p.nnz_staged -= p.blocks[t].k1 - p.blocks[t].k0;
+                    continue;  // cbase stays -1: the int32 path
+                }
+                p.cbase[t] = -2 - (int)((off << 8) | nr);
+                p.runs.insert(p.runs.end(), r.begin(), r.end());
+            }
         }
     }
 }
@@ -596,7 +660,8 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     TilePlan p;
     make_tile_plan(rp.data(), ci.data(), m, mat->nnz, compute_type,
                    spread ? spmv_resident_tiles(h, compute_type) : 0,
-                   mat->local_cols, !(h->spmv_variant & 32), p, spmv_row_align(h, compute_type));
+                   mat->local_cols, !(h->spmv_variant & 32), p, spmv_row_align(h, compute_type),
+                   !(h->spmv_variant & rsp::kSpmvVariantNoStage));
     const rsp_an::hvec<SpmvBlock> &blocks = p.blocks;
     const rsp_an::hvec<SpmvLongRow> &longrows = p.longrows;
     const int nslots = p.nslots, nint = p.nint;
@@ -606,7 +671,7 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     // exact layout of this schedule in the matrix's device memory (grown,
     // never shrunk, on a re-plan)
     SpmvBounds b{blocks.size(), longrows.size(), (size_t)nslots};
-    const SpmvLayout lay = spmv_layout(b, elem_size(compute_type), (int64_t)c16.size());
+    const SpmvLayout lay = spmv_layout(b, elem_size(compute_type), (int64_t)c16.size(), p.runs.size());
     mat->planned = 0;
     if (lay.bytes > mat->plan_cap || !mat->d_plan) {
         if (mat->d_plan) {
@@ -632,6 +697,9 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     if (!c16.empty())
         RSP_CHECK_HIP(hipMemcpyAsync(buf + lay.off_cidx, c16.data(), c16.size() * sizeof(uint16_t),
                                      hipMemcpyHostToDevice, h->stream));
+    if (!p.runs.empty())
+        RSP_CHECK_HIP(hipMemcpyAsync(buf + lay.off_runs, p.runs.data(), p.runs.size() * sizeof(int),
+                                     hipMemcpyHostToDevice, h->stream));
     const size_t off_long = lay.off_long, off_part = lay.off_part;
     if (!longrows.empty())
         RSP_CHECK_HIP(hipMemcpyAsync(buf + off_long, longrows.data(),
@@ -654,7 +722,9 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     mat->off_part = off_part;
     mat->off_cbase = lay.off_cbase;
     mat->off_cidx = lay.off_cidx;
+    mat->off_runs = lay.off_runs;
     mat->nnz_c16 = nnz_c16;
+    mat->nnz_staged = p.nnz_staged;
     return RSP_STATUS_SUCCESS;
 }
 
@@ -706,6 +776,7 @@ static rsp_status_t spmv_run(rsp_handle_t h, rsp_operation_t op, const void *alp
     a.nblocks = mat->nblocks;
     a.cbases = (const int *)(plan + mat->off_cbase);
     a.cidx = (const unsigned short *)(plan + mat->off_cidx);
+    a.runs = (const int *)(plan + mat->off_runs);
     a.cmax = mat->cols > 0 ? (int)(mat->cols - 1) : 0;
     a.longrows = (const SpmvLongRow *)(plan + mat->off_long);
     a.nlong = mat->nlong;
@@ -805,11 +876,12 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
     // tickets with single calls of its matrices.
     const int64_t R = spmv_resident_tiles(h, compute_type);
     const bool spread_ok = !(h->spmv_variant & 16), c16_ok = !(h->spmv_variant & 32);
+    const bool stage_ok = !(h->spmv_variant & rsp::kSpmvVariantNoStage);
     rsp_an::hvec<TilePlan> plans((size_t)count);
     // layout: per launch [entries | tiles | tile column bases | long rows |
     // 16-bit column offsets of each matrix | long-row partials and tickets of
     // each matrix (zero)], each 16-B aligned
-    struct Span { int first, count; size_t off_e, off_t, off_c, off_l; rsp_an::hvec<size_t> off_16, off_p; };
+    struct Span { int first, count; size_t off_e, off_t, off_c, off_l; rsp_an::hvec<size_t> off_16, off_p, off_r; };
     rsp_an::hvec<Span> spans;
     size_t bytes = 0;
     auto tile_range = [part](const TilePlan &p, int *t0, int *t1) {
@@ -817,7 +889,7 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
         *t1 = part == 1 ? p.nint : (int)p.blocks.size();
     };
     for (int first = 0; first < count; first += rsp::kSpmvBatchMax) {
-        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, {}, {}};
+        Span sp{first, std::min(rsp::kSpmvBatchMax, count - first), 0, 0, 0, 0, {}, {}, {}};
         rsp_an::hvec<rsp_an::hvec<int>> rps((size_t)sp.count), cis((size_t)sp.count);
         int64_t nt_full = 0, nnz_all = 0;
         for (int q = 0; q < sp.count; q++) {
@@ -825,7 +897,7 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
             rsp_status_t st = download_pattern(h, A, rps[q], cis[q]);
             if (st != RSP_STATUS_SUCCESS) return st;
             make_tile_plan(rps[q].data(), cis[q].data(), (int)A->rows, A->nnz, compute_type, 0,
-                           A->local_cols, c16_ok, plans[first + q], spmv_row_align(h, compute_type));
+                           A->local_cols, c16_ok, plans[first + q], spmv_row_align(h, compute_type), stage_ok);
             int t0, t1;
             tile_range(plans[first + q], &t0, &t1);
             nt_full += t1 - t0;
@@ -838,7 +910,7 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
                 const int64_t share = std::max<int64_t>(1, R * nnz_q / std::max<int64_t>(1, nnz_all));
                 make_tile_plan(rps[q].data(), cis[q].data(), (int)A->rows, A->nnz, compute_type,
                                share, A->local_cols, c16_ok, plans[first + q],
-                               spmv_row_align(h, compute_type));
+                               spmv_row_align(h, compute_type), stage_ok);
             }
         int nt = 0, nl = 0;
         for (int q = 0; q < sp.count; q++) {
@@ -863,6 +935,10 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
         for (int q = 0; q < sp.count; q++) {
             sp.off_16.push_back(bytes);
             bytes += (plans[first + q].c16.size() * sizeof(uint16_t) + 15) & ~(size_t)15;
+        }
+        for (int q = 0; q < sp.count; q++) {
+            sp.off_r.push_back(bytes);
+            bytes += (plans[first + q].runs.size() * sizeof(int) + 15) & ~(size_t)15;
         }
         for (int q = 0; q < sp.count; q++) {
             sp.off_p.push_back(bytes);
@@ -897,6 +973,7 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
             e.y = d_y[sp.first + q];
             e.partials = (void *)((char *)b->d_mem + sp.off_p[q]);  // this member's own
             e.cidx = (const unsigned short *)((char *)b->d_mem + sp.off_16[q]);
+            e.runs = (const int *)((char *)b->d_mem + sp.off_r[q]);
             e.cmax = A->cols > 0 ? (int)(A->cols - 1) : 0;
             e.nnz = A->nnz_s;
             e.vector_ok = ((((uintptr_t)A->colidx) | ((uintptr_t)A->vals)) & 15) == 0;
@@ -904,7 +981,7 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
             a.tiles_at.begin[q] = nt;
             a.longs_at.begin[q] = nl;
             for (int t = t0; t < t1; t++)
-                if (p.cbase[(size_t)t] >= 0) b->entries_16bit += p.blocks[(size_t)t].k1 - p.blocks[(size_t)t].k0;
+                if (p.cbase[(size_t)t] != -1) b->entries_16bit += p.blocks[(size_t)t].k1 - p.blocks[(size_t)t].k0;
             b->tiles += t1 - t0;
             if (t1 > t0) {
                 memcpy(host.data() + sp.off_t + (size_t)nt * sizeof(SpmvBlock), p.blocks.data() + t0,
@@ -917,6 +994,8 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
                        (size_t)nlq * sizeof(SpmvLongRow));
             if (!p.c16.empty())
                 memcpy(host.data() + sp.off_16[q], p.c16.data(), p.c16.size() * sizeof(uint16_t));
+            if (!p.runs.empty())
+                memcpy(host.data() + sp.off_r[q], p.runs.data(), p.runs.size() * sizeof(int));
             nt += t1 - t0;
             nl += nlq;
         }

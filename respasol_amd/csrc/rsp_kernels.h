@@ -59,7 +59,12 @@ struct SpmvTile {
     // rows per tile: fp32 tiles hold twice the entries, so twice the rows
     // (fp32 moderate step 0.077 -> 0.0734 ms with 1024; fp64 unchanged by it)
     static constexpr int kMaxRows = sizeof(T) == 8 ? kSpmvMaxRows : 2 * kSpmvMaxRows;
+    // staged tiles (round 4): the tile's distinct columns, at most kStageSlots
+    // of them, loaded once into the LDS image as contiguous column runs (at
+    // most kStageRuns); each entry then reads its x from LDS
+    static constexpr int kStageSlots = sizeof(T) == 8 ? 1024 : 2048;
 };
+constexpr int kStageRuns = 254;  // run descriptors per staged tile (+1 sentinel <= 256 threads)
 
 struct SpmvArgs {
     int m;
@@ -70,8 +75,13 @@ struct SpmvArgs {
     void *y;
     const SpmvBlock *blocks;
     int nblocks;
-    const int *cbases;            // per tile: column base of its 16-bit offsets, -1 = int32 colidx
-    const unsigned short *cidx;   // 16-bit column offsets (tiles with cbases >= 0)
+    // per tile: >= 0 column base of its 16-bit column offsets; -1 int32 colidx;
+    // <= -2 a staged tile: code = -2 - cbase, its run descriptors at
+    // runs[2 (code >> 8) ..], (code & 255) of them + a sentinel, and its
+    // 16-bit values are LDS slot indices of the tile's distinct columns
+    const int *cbases;
+    const unsigned short *cidx;   // 16-bit column offsets / slot indices (tiles with cbases != -1)
+    const int *runs;              // staged tiles: {first column, first slot} per run, {0, slots} last
     int cmax;                     // n - 1 (clamp for neighbour entries of partial vectors)
     const SpmvLongRow *longrows;
     int nlong;
@@ -99,6 +109,7 @@ struct alignas(16) SpmvBatchEntry {
     void *y;
     void *partials;
     const unsigned short *cidx;  // 16-bit column offsets (SpmvArgs::cidx)
+    const int *runs;             // staged tiles' run descriptors (SpmvArgs::runs)
     int nnz;        // rowptr[m] (as SpmvArgs::nnz)
     int vector_ok;  // colidx/vals 16-B aligned
     int cmax;       // n - 1
@@ -118,6 +129,7 @@ struct SpmvBatchArgs {
                   // bit 8: long rows by the separate fixup kernel
 };
 constexpr int kSpmvVariantFixup = 256;
+constexpr int kSpmvVariantNoStage = 512;  // plan time: no staged tiles (A/B)
 
 // Level schedule of one dependency DAG. Rows are grouped by level
 // (rows[ptr[l] .. ptr[l+1])); `segs` (host) cover the levels in order, each

@@ -206,6 +206,99 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
     }
 }
 
+// LDS-only workgroup barrier: orders LDS traffic and leaves global stores in
+// flight (__syncthreads() waits vmcnt(0), i.e. for the previous tile's y
+// stores to be acknowledged).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// A STAGED tile (round 4; plan: rsp_api.cpp make_tile_plan). Gathering x
+// lane by lane costs the vector-memory path about one TA cycle per lane —
+// the bound of the plain tile (counters) — while a mesh tile's
+// 2-4 k entries read only ~900-1600 distinct columns, in a few contiguous
+// runs. So the tile's distinct columns are loaded once into its LDS image
+// (coalesced loads along each run), and every entry reads its x from there
+// by a 16-bit slot index (stored where the C16 tiles keep column offsets).
+// Sequence: the run descriptors (loaded first, by the caller) go to a table
+// at the END of the LDS image; each thread finds the run of its slots
+// u = tid + 256 k by a binary search in that table (all k together, one LDS
+// round trip per step) and loads x of those columns — while the tile's
+// stream loads are still in flight; x goes to LDS slots [0, U); then the
+// entries' x are read from LDS (slot clamped to U - 1: a partial vector's
+// neighbour entries carry another tile's indices; their products are never
+// read), and after a barrier the products overwrite the image as usual.
+// Same products, same order: the same bits as the gathered tile.
+template <typename T, bool NT, int NTH = kSpmvThreads,
+          int IT = SpmvTile<T>::kSlots / (kSpmvThreads * (16 / sizeof(T)))>
+__device__ __forceinline__ void stream_products_staged(const unsigned short *__restrict__ cidx, int2 rd,
+                                                       int nr, const T *__restrict__ vals,
+                                                       const T *__restrict__ x, int kb, int k1,
+                                                       T *__restrict__ lds) {
+    constexpr int VW = 16 / sizeof(T);
+    constexpr int SMAX = SpmvTile<T>::kStageSlots / NTH;
+    typedef typename VecT<T, VW>::V V;
+    typedef typename VecT<T, VW>::H H;
+    const int tid = threadIdx.x;
+    const int last = (k1 - 1) & ~(VW - 1);
+    H ch[IT];
+    V vv[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = min(kb + (it * NTH + tid) * VW, last);
+        ch[it] = ld<NT>(reinterpret_cast<const H *>(cidx + e));
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int e = min(kb + (it * NTH + tid) * VW, last);
+        vv[it] = ld<NT>(reinterpret_cast<const V *>(vals + e));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int2 *tab = reinterpret_cast<int2 *>(lds + SpmvTile<T>::kSlots) - (nr + 1);
+    if (tid <= nr) tab[tid] = rd;
+    lds_barrier();
+    const int U = tab[nr].y;
+    int us[SMAX], lo[SMAX];
+#pragma unroll
+    for (int k = 0; k < SMAX; ++k) {
+        us[k] = min(k * NTH + tid, U - 1);
+        lo[k] = 0;
+    }
+    for (int n = nr; n > 1;) {  // largest r with tab[r].y <= u (tab[0].y = 0); nr is uniform
+        const int h = n >> 1;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k)
+            if (tab[lo[k] + h].y <= us[k]) lo[k] += h;
+        n -= h;
+    }
+    T xs[SMAX];
+#pragma unroll
+    for (int k = 0; k < SMAX; ++k)
+        if (k * NTH < U) {  // workgroup-uniform
+            const int2 r = tab[lo[k]];
+            xs[k] = x[r.x + (us[k] - r.y)];
+        }
+#pragma unroll
+    for (int k = 0; k < SMAX; ++k)
+        if (k * NTH < U && k * NTH + tid < U) lds[k * NTH + tid] = xs[k];
+    lds_barrier();
+    T xv[IT][VW];
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+        for (int j = 0; j < VW; ++j) xv[it][j] = lds[min((int)ch[it][j], U - 1)];
+    lds_barrier();  // every x read before the products overwrite the image
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        V p;
+#pragma unroll
+        for (int j = 0; j < VW; ++j) p[j] = vv[it][j] * xv[it][j];
+        *reinterpret_cast<V *>(lds + (it * NTH + tid) * VW) = p;
+    }
+}
+
 // Element-wise variant for a tile that touches the end of the arrays (at
 // most one per call) or unaligned arrays.
 template <typename T, int NTH = kSpmvThreads>
@@ -269,14 +362,6 @@ __device__ __forceinline__ void reduce_tile_rows(const T *lds, const unsigned sh
     }
 }
 
-// LDS-only workgroup barrier: orders LDS traffic and leaves global stores in
-// flight (__syncthreads() waits vmcnt(0), i.e. for the previous tile's y
-// stores to be acknowledged).
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 // A long row (or one tile-sized chunk of it) in LDS slots [a, e): thread t
 // sums slots a+t, a+t+256, ... in order, each wave combines its 64 sums with
@@ -340,7 +425,7 @@ __device__ __forceinline__ void longrow_arrive(const SpmvBlock blk, const int *_
 template <typename T, bool NT, bool BETA>
 __device__ __forceinline__ void spmv_tile(
     const SpmvBlock blk, const int *__restrict__ rowptr, const int *__restrict__ colidx,
-    const unsigned short *__restrict__ cidx, int cbase, int cmax,
+    const unsigned short *__restrict__ cidx, const int *__restrict__ runs, int cbase, int cmax,
     const T *__restrict__ vals, const T *__restrict__ x, T *__restrict__ y,
     T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, T *lds,
     T *wsum, unsigned short *rp_lds, int fuse) {
@@ -348,6 +433,16 @@ __device__ __forceinline__ void spmv_tile(
     constexpr int RPQ = (SpmvTile<T>::kMaxRows + kSpmvThreads) / kSpmvThreads;
     const int tid = threadIdx.x;
     const int k0 = blk.k0, k1 = blk.k1;
+    // a staged tile's run descriptors: the first load of the tile, so the x
+    // loads they lead to need not wait for the stream (vmcnt is in order)
+    const bool staged = cbase <= -2;
+    int2 rd = make_int2(0, 0);
+    int nr = 0;
+    if (staged) {  // workgroup-uniform
+        const int code = -2 - cbase;
+        nr = code & 255;
+        if (tid <= nr) rd = reinterpret_cast<const int2 *>(runs)[(code >> 8) + tid];
+    }
     // the tile's row offsets, loaded ahead of the stream and parked in LDS
     // after it, so the reduce never waits on global memory
     const int nrows = blk.r1 - blk.r0;
@@ -392,6 +487,8 @@ __device__ __forceinline__ void spmv_tile(
 #endif
     if (vec && cbase >= 0)
         stream_products<T, NT, true>(colidx, cidx, cbase, cmax, vals, x, kb, k1, lds);
+    else if (vec && staged)
+        stream_products_staged<T, NT>(cidx, rd, nr, vals, x, kb, k1, lds);
     else if (vec)
         stream_products<T, NT>(colidx, cidx, 0, 0, vals, x, kb, k1, lds);
     else
@@ -451,8 +548,8 @@ template <typename T, bool NT, bool BETA>
 __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
     const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
-    const int *__restrict__ cbases, const unsigned short *__restrict__ cidx, int cmax,
-    T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, int fuse) {
+    const int *__restrict__ cbases, const unsigned short *__restrict__ cidx, const int *__restrict__ runs,
+    int cmax, T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ unsigned short rp_lds[SpmvTile<T>::kMaxRows + 2];  // row offsets - kb
@@ -464,7 +561,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     const int t0 = xcd_swizzle(blockIdx.x, nwg) * RSP_PROBE_WALK;
     for (int w = 0; w < RSP_PROBE_WALK && t0 + w < nblocks; ++w) {
         if (w) lds_barrier();
-        spmv_tile<T, NT, BETA>(blocks[t0 + w], rowptr, colidx, cidx, cbases[t0 + w], cmax, vals, x,
+        spmv_tile<T, NT, BETA>(blocks[t0 + w], rowptr, colidx, cidx, runs, cbases[t0 + w], cmax, vals, x,
                                y, partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum,
                                rp_lds, fuse);
     }
@@ -478,7 +575,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
 #if RSP_PROBE_PRIO
     __builtin_amdgcn_s_setprio(RSP_PROBE_PRIO);
 #endif
-    spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, cidx, cbases[b], cmax, vals, x, y,
+    spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, cidx, runs, cbases[b], cmax, vals, x, y,
                            partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds,
                            fuse);
 }
@@ -546,7 +643,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
         }
     const int t = lo + (SWZ ? xcd_swizzle(b - lo, hi - lo) : b - lo);
     const SpmvBatchEntry e = entries[j];
-    spmv_tile<T, NT, BETA>(tiles[t], e.rowptr, e.colidx, e.cidx, cbases[t], e.cmax,
+    spmv_tile<T, NT, BETA>(tiles[t], e.rowptr, e.colidx, e.cidx, e.runs, cbases[t], e.cmax,
                            (const T *)e.vals, (const T *)e.x,
                            (T *)e.y, (T *)e.partials, alpha, beta, BETA, e.nnz, e.vector_ok, lds,
                            wsum, rp_lds, fuse);
@@ -617,7 +714,7 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(RSP_PROBE_WALK ? (a.nblocks + RSP_PROBE_WALK - 1) / (RSP_PROBE_WALK ? RSP_PROBE_WALK : 1)
                                                 : a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
                        (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks, a.cbases,
-                       a.cidx, a.cmax, (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok, fuse);
+                       a.cidx, a.runs, a.cmax, (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok, fuse);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.nlong > 0 && !fuse) {
