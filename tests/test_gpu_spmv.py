@@ -280,12 +280,12 @@ def test_column_offset_tiles(handle):
         check(A, x, dt, handle)
 
 
-@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33, 64, 128, 80, 256, 257, 512])
+@pytest.mark.parametrize("variant", [1, 16, 17, 32, 33, 64, 128, 80, 256, 257, 512, 1024])
 def test_kernel_variants_same_bits(monkeypatch, variant):
     """Every kernel / plan variant (RSP_SPMV_VARIANT: default-policy instead of
     non-temporal loads; small plans not spread over the chip, or every small
     plan spread (bit 9, the round-2 rule); int32 column
-    indices only, no 16-bit offsets) gives the same
+    indices only, no 16-bit offsets; no staged tiles, bit 10) gives the same
     bits as the canonical-order oracle, on matrices with short rows, rows
     just above the 256 threshold and chunked hub rows."""
     monkeypatch.setenv("RSP_SPMV_VARIANT", str(variant))
@@ -297,6 +297,47 @@ def test_kernel_variants_same_bits(monkeypatch, variant):
             x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
             for dt in (torch.float64, torch.float32):
                 check(A, x, dt, h)
+    finally:
+        h.close()
+
+
+@pytest.mark.parametrize("pct", [100, 80, 30])
+def test_staged_tiles_same_bits(monkeypatch, pct):
+    """Staged tiles (a tile's distinct columns loaded once into LDS as column
+    runs, entries reading x by slot index; RSP_SPMV_STAGE_PCT = the largest
+    distinct-column share of a tile's entries that is staged): every row
+    bitwise the canonical-order oracle for mesh / stencil / random-band /
+    circuit structures, odd row lengths (tiles starting inside a 16-B
+    vector), a band just wide enough to hit the run cap, single calls and a
+    batch, fp64 and fp32."""
+    from respasol_amd.sparse import SpmvBatch
+    monkeypatch.setenv("RSP_SPMV_STAGE_PCT", str(pct))
+    h = Handle()
+    try:
+        mats = [csr.surrogate(nm, sc) for nm, sc in (("Serena", 0.02), ("atmosmodd", 0.05), ("Si87H76", 0.05),
+                                                        ("ecology2", 0.05), ("CurlCurl_2", 0.05), ("G2_circuit", 0.2))]
+        rng = np.random.default_rng(3)
+        n = 30000  # 7 entries per row, columns in a +-600 band: many short runs per tile
+        ci = np.sort(np.clip(np.arange(n)[:, None] + rng.integers(-600, 601, (n, 7)), 0, n - 1), axis=1)
+        rows = [np.unique(r) for r in ci]
+        rp = np.zeros(n + 1, np.int32)
+        np.cumsum([len(r) for r in rows], out=rp[1:])
+        cc = np.concatenate(rows).astype(np.int32)
+        mats.append(csr.CsrMatrix(0, n, n, len(cc), rp, cc, rng.uniform(-1, 1, len(cc))))
+        for dt in (torch.float64, torch.float32):
+            xs, ys, ms, refs = [], [], [], []
+            for A in mats:
+                x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+                check(A, x, dt, h)
+                M = SpMat(h, *upload_csr(A.rowptr, A.colidx, A.values, dt), A.n)
+                ms.append(M)
+                xs.append(torch.from_numpy(x.astype(NP[dt])).cuda())
+                ys.append(torch.empty(A.m, dtype=dt, device="cuda"))
+                refs.append(ob.spmv(A.rowptr, A.colidx, A.values.astype(NP[dt]), x.astype(NP[dt]), order="canon"))
+            SpmvBatch(h, ms, xs, ys).run()
+            torch.cuda.synchronize()
+            for r, y in zip(refs, ys):
+                assert same_bits(y.cpu().numpy(), r)
     finally:
         h.close()
 

@@ -142,10 +142,11 @@ def test_batch_own_tiling_same_bits(handle, names, split):
         assert same_bits(r.cpu().numpy(), y.cpu().numpy()), k
 
 
-@pytest.mark.parametrize("variant", [1, 8, 9, 16, 32, 64, 128, 256])
+@pytest.mark.parametrize("variant", [1, 8, 9, 16, 32, 64, 128, 256, 1024])
 def test_batch_variants_same_bits(monkeypatch, variant):
     """Default-policy loads (bit 0), no per-matrix XCD swizzle (bit 3), no
-    spreading (bit 4), int32 column indices only (bit 5)."""
+    spreading (bit 4), int32 column indices only (bit 5), no staged tiles
+    (bit 10)."""
     monkeypatch.setenv("RSP_SPMV_VARIANT", str(variant))
     h = Handle()
     try:
