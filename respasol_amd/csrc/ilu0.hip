@@ -1402,7 +1402,7 @@ __global__ __launch_bounds__(256) void trsv_stream(TrsvArgs a, T alpha) {
     }
 }
 
-template <typename T, int KIND, int G>
+template <typename T, int KIND, int G, bool PAIRS = false>
 __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, int c0, int c1, int base) {
     constexpr int NTH = rsp::kThinThreads;
     constexpr int TPT = rsp::kChunkTerms / NTH;  // terms of a chunk per thread: tid + j NTH
@@ -1812,6 +1812,61 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 a.trace[a.trace_cap / 2 + L] = a.trace_clk ? clock64() : wall_clock64();
         }
     };
+    // The same on K waves with TWO consecutive levels per turn (a.narrow_pairs,
+    // RSP_ILU_NARROW_PAIRS=1): wave w takes levels (q0 + 2 (w + jK), + 1).
+    // The second level of a pair reads the first's y from this wave's own
+    // stores (in-order LDS of one wave, a wavefront fence between), so a
+    // pair pays one counter wait and one release instead of two. Before the
+    // wait the wave loads both levels' row records and the first level's
+    // term groups; the second level's values load with its y. Same terms,
+    // same order, same fma chain: same bits.
+    auto narrow_run_mw2 = [&](const rsp::LevelChunk &ch, int q0, int q1, int K) {
+        const int w = tid >> 6, lane = tid & 63, x0 = ch.x0;
+        const int L0 = ch.l0 + q0;
+        auto row_of = [&](int q) {
+            const int p0 = lptr[q], p1 = lptr[q + 1];
+            return max(p0 - x0 + min(lane, p1 - p0 - 1), 0);
+        };
+        for (int q = q0 + 2 * w; q < q1; q += 2 * K) {
+            const bool has2 = q + 1 < q1;  // wave-uniform
+            const int cr = row_of(q), cr2 = has2 ? row_of(q + 1) : cr;
+            const ThinRow<T> R = lrow[cr], R2 = lrow[cr2];
+            const int g0 = R.g & 0xffff, ng = R.g >> 16;
+            const bool two = __ballot(ng >= 2) != 0;
+            const int gi = ng >= 2 ? g0 + 1 : kPadGroup;
+            const TermIds<G> i1 = lidx[g0];
+            const TermGroup<T, G> v1 = lval[g0];
+            const TermIds<G> j1 = lidx[R2.g & 0xffff];
+            TermIds<G> i2;
+            TermGroup<T, G> v2;
+            if (two) {
+                i2 = lidx[gi];
+                v2 = lval[gi];
+            }
+            const int L = ch.l0 + q;
+            if (L > L0) lds_wait_geq(&lds_done, L, L - 1);
+            T s = group_fma(R.x, v1, i1);
+            if (two) {
+                s = group_fma(s, v2, i2);
+                if (__ballot(ng >= 3))
+                    for (int g = 2; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+            }
+            if constexpr (KIND == 2) s = s / ldg[cr];
+            put(R.out, s);
+            if (has2) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                const int h0 = R2.g & 0xffff, nh = R2.g >> 16;
+                T t = group_fma(R2.x, lval[h0], j1);
+                if (__ballot(nh >= 2))
+                    for (int g = 1; g < nh; ++g) t = group_fma(t, lval[h0 + g], lidx[h0 + g]);
+                if constexpr (KIND == 2) t = t / ldg[cr2];
+                put(R2.out, t);
+            }
+            lds_publish(&lds_done, L + (has2 ? 2 : 1), lane == 0);  // after the y stores
+        }
+    };
     auto levels = [&](const rsp::LevelChunk &ch) {
         const int x0 = ch.x0, nl = ch.l1 - ch.l0;
 #if RSP_THIN_LONG_READLANE
@@ -1825,6 +1880,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 if (KIND != 2 && G == 2 && a.narrow_split) {  // (G = 4: the registers are not there)
                     if constexpr (KIND != 2 && G == 2)
                         if (tid < 64) narrow_run_split(ch, q, qe);
+                } else if (PAIRS && K > 1) {  // (its own instantiation: the registers)
+                    if constexpr (PAIRS)
+                        if (tid < 64 * K) narrow_run_mw2(ch, q, qe, K);
                 } else if (K > 1) {
                     if (tid < 64 * K) narrow_run_mw(ch, q, qe, K);
                 } else if (tid < 64) {
@@ -1999,12 +2057,11 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
             // term groups of 2 for DAGs of short chains (the plan padded them so)
-            if (P.group == 2)
-                hipLaunchKernelGGL((trsv_thin_pf<T, KIND, 2>), dim3(1), dim3(kThinThreads), 0, s, a,
-                                   sg.c0, sg.c1, P.ptr_host[sg.lb]);
-            else
-                hipLaunchKernelGGL((trsv_thin_pf<T, KIND, 4>), dim3(1), dim3(kThinThreads), 0, s, a,
-                                   sg.c0, sg.c1, P.ptr_host[sg.lb]);
+            // (RSP_ILU_NARROW_PAIRS: the two-levels-per-turn narrow runs, L / L^T)
+            const bool pr = KIND != 2 && a.narrow_pairs;
+            auto kern = P.group == 2 ? (pr ? trsv_thin_pf<T, KIND, 2, KIND != 2> : trsv_thin_pf<T, KIND, 2>)
+                                     : (pr ? trsv_thin_pf<T, KIND, 4, KIND != 2> : trsv_thin_pf<T, KIND, 4>);
+            hipLaunchKernelGGL(kern, dim3(1), dim3(kThinThreads), 0, s, a, sg.c0, sg.c1, P.ptr_host[sg.lb]);
             continue;
         }
         if (a.flow && sg.c1 > sg.c0) {  // flow segment: one persistent launch

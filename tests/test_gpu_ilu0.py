@@ -399,6 +399,23 @@ def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, order, nsplit,
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
+@pytest.mark.parametrize("waves,group", [(4, 0), (2, 0), (3, 2), (4, 4)])
+@pytest.mark.parametrize("name,scale", [("dc1", 1.0), ("G2_circuit", 0.5), ("thermomech_TK", 0.5)])
+def test_narrow_runs_two_levels_per_turn(handle, monkeypatch, waves, group, name, scale):
+    """Narrow solve runs with two consecutive levels per wave turn
+    (RSP_ILU_NARROW_PAIRS=1: the second level reads the first's y from the
+    same wave's stores): bitwise equal to the oracle for L and L^T (U keeps
+    the one-level turns), fp64 and fp32, odd and even run lengths."""
+    monkeypatch.setenv("RSP_ILU_NARROW_PAIRS", "1")
+    monkeypatch.setenv("RSP_ILU_NARROW_WAVES", str(waves))
+    if group:
+        monkeypatch.setenv("RSP_ILU_GROUP", str(group))
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float64, handle, x=x)
+    compare(A, torch.float32, handle, x=x, true_lu=True)
+
+
 @pytest.mark.parametrize("flow,wpc,mode", [(0, 8, 0), (1, 4, 0), (1, 8, 0), (1, 16, 0), (1, 4, 1), (1, 16, 1)])
 @pytest.mark.parametrize("name,scale", [("xenon2", 0.3), ("offshore", 0.2), ("cfd2", 0.3), ("ss1", 0.2)])
 def test_flow_segments(handle, monkeypatch, flow, wpc, mode, name, scale):
