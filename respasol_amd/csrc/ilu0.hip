@@ -1813,7 +1813,12 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         }
     };
     // The same on K waves with TWO consecutive levels per turn (a.narrow_pairs,
-    // RSP_ILU_NARROW_PAIRS=1): wave w takes levels (q0 + 2 (w + jK), + 1).
+    // RSP_ILU_NARROW_PAIRS, default on for L / L^T): wave w takes levels
+    // (q0 + 2 (w + jK), + 1). Deep set, same box: solve 15.70 -> 14.95 ms
+    // (dc1 5.19 -> 4.93, matrix-new_3 6.11 -> 5.81, G2_circuit 3.46 -> 3.20;
+    // thermomech_TK 0.95 -> 1.00). (The same for the thin factor's narrow
+    // rounds measured 21.2 -> 26.0 ms — the second level's item preparation
+    // lands on the chain — and was removed.)
     // The second level of a pair reads the first's y from this wave's own
     // stores (in-order LDS of one wave, a wavefront fence between), so a
     // pair pays one counter wait and one release instead of two. Before the

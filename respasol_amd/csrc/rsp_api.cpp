@@ -1323,6 +1323,37 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     };
     rsp_an::hvec<int> dev_rows, long_rows;
     for (int i = 0; i < n; i++) (rp[(size_t)i + 1] - rp[(size_t)i] <= kAnDevRow ? dev_rows : long_rows).push_back(i);
+    // The host level pass needs only the pattern: download it first, check it
+    // (columns in range, rows strictly increasing: the device check below
+    // returns the same verdict), take the diagonal positions from it and run
+    // the level pass on a thread of its own while the device validates,
+    // counts, scans and fills (round 4: the level pass used to wait for all
+    // of that).
+    if (nnz_s > 0) {
+        RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), d_ci, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
+        RSP_CHECK_HIP(hipStreamSynchronize(s));
+    }
+    sub("D2H pattern");
+    {
+        std::atomic<int> bad{0};
+        hp.dpos.resize((size_t)n);
+        rsp_an::parallel_for(n, 1 << 14, [&](long long r0, long long r1) {
+            for (long long i = r0; i < r1; i++) {
+                const int a = rp[(size_t)i], b = rp[(size_t)i + 1];
+                int d = b, prev = -1;
+                for (int p = a; p < b; p++) {
+                    const int c = ci[(size_t)p];
+                    if (c < 0 || c >= n || c <= prev) bad.store(1, std::memory_order_relaxed);
+                    if (d == b && c >= (int)i) d = p;
+                    prev = c;
+                }
+                hp.dpos[(size_t)i] = d;
+            }
+        });
+        if (bad.load()) return RSP_STATUS_INVALID_VALUE;  // a column out of range or a row not increasing
+    }
+    sub("host check + dpos");
+    rsp_an::Task levels([&] { rsp_an::plan_levels(rp.data(), ci.data(), hp); });
     size_t scan_bytes = 0;
     RSP_CHECK_HIP(rsp_k::ilu_an_scan(nullptr, nullptr, nnz_s + 1, nullptr, &scan_bytes, s));
     Arena ar;
@@ -1354,15 +1385,11 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     const int n_c[3] = {(int)dev_rows.size(), 0, 0};
     const int *rows_c[3] = {d_rows, nullptr, nullptr};
     RSP_CHECK_HIP(rsp_k::ilu_an_count(rows_c, n_c, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_cnt, d_scratch, s));
-    hp.dpos.resize((size_t)n);
     hp.hasdiag.resize((size_t)n);
-    if (n > 0) {
-        RSP_CHECK_HIP(hipMemcpyAsync(hp.dpos.data(), f->d_dpos, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (n > 0)
         RSP_CHECK_HIP(hipMemcpyAsync(hp.hasdiag.data(), f->d_hasdiag, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    }
-    if (nnz_s > 0) RSP_CHECK_HIP(hipMemcpyAsync(ci.data(), d_ci, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
-    sub("count kernel + D2H pattern");
+    sub("count kernel + D2H hasdiag");
     // the long rows' counts on the host
     rsp_an::hvec<int> hcnt(long_rows.empty() ? 0 : (size_t)nnz_s);
     rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), hcnt.data(),
@@ -1391,8 +1418,8 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
                                      f->d_upd_l, f->d_upd_u, s));
     RSP_CHECK_HIP(rsp_k::ilu_an_stages(n, kAnDevRow, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, f->d_upd_l,
                                        d_stage, f->d_lord, f->d_lend, f->d_udiv, d_scratch, s));
-    // the level sets on the host while the device fills the update lists
-    rsp_an::plan_levels(rp.data(), ci.data(), hp);
+    // the level sets (host thread, started above) while the device fills the update lists
+    levels.join();
     ph.mark("levels");
     after_levels();  // the solve plans need nothing more: started here
     // the host factor plan reads the update pairs of its thin rows only: those
@@ -1916,7 +1943,7 @@ static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alp
     a.wave_lds = env_int("RSP_ILU_WAVE_LDS", 1);
     a.narrow_waves = std::min(std::max(env_int("RSP_ILU_NARROW_WAVES", 4), 1), rsp::kThinThreads / 64);
     a.narrow_split = env_int("RSP_ILU_NARROW_SPLIT", 0) != 0;  // (default off: slower)
-    a.narrow_pairs = env_int("RSP_ILU_NARROW_PAIRS", 0) != 0;
+    a.narrow_pairs = env_int("RSP_ILU_NARROW_PAIRS", 1) != 0;
     a.flow = env_int("RSP_ILU_FLOW", 1) != 0;
     // every workgroup of a flow launch must be resident at once (an item waits
     // for items of lower index only, and workgroups take items in index

@@ -293,7 +293,8 @@ def test_unsorted_or_duplicate_rows_rejected(handle):
     INVALID_VALUE, never a factor of the wrong pattern."""
     from respasol_amd import RspError
     rp = torch.tensor([0, 2, 4], dtype=torch.int32, device="cuda")
-    for cols in ([1, 0, 0, 1], [0, 0, 0, 1]):  # row 0 unsorted / duplicate column 0
+    # row 0 unsorted / duplicate column 0 / a column past n / a negative column
+    for cols in ([1, 0, 0, 1], [0, 0, 0, 1], [0, 2, 0, 1], [-1, 0, 0, 1]):
         ci = torch.tensor(cols, dtype=torch.int32, device="cuda")
         il = Ilu0(handle, rp, ci)
         with pytest.raises(RspError) as e:
@@ -399,14 +400,14 @@ def test_narrow_runs_on_several_waves(handle, monkeypatch, waves, order, nsplit,
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
-@pytest.mark.parametrize("waves,group", [(4, 0), (2, 0), (3, 2), (4, 4)])
+@pytest.mark.parametrize("waves,group,pairs", [(4, 0, 1), (2, 0, 1), (3, 2, 1), (4, 4, 1), (4, 0, 0), (3, 4, 0)])
 @pytest.mark.parametrize("name,scale", [("dc1", 1.0), ("G2_circuit", 0.5), ("thermomech_TK", 0.5)])
-def test_narrow_runs_two_levels_per_turn(handle, monkeypatch, waves, group, name, scale):
-    """Narrow solve runs with two consecutive levels per wave turn
-    (RSP_ILU_NARROW_PAIRS=1: the second level reads the first's y from the
-    same wave's stores): bitwise equal to the oracle for L and L^T (U keeps
-    the one-level turns), fp64 and fp32, odd and even run lengths."""
-    monkeypatch.setenv("RSP_ILU_NARROW_PAIRS", "1")
+def test_narrow_runs_two_levels_per_turn(handle, monkeypatch, waves, group, pairs, name, scale):
+    """Narrow solve runs with two consecutive levels per wave turn (the
+    default, RSP_ILU_NARROW_PAIRS=1: the second level reads the first's y from
+    the same wave's stores) or one (=0): bitwise equal to the oracle for L and
+    L^T (U keeps the one-level turns), fp64 and fp32, odd and even run lengths."""
+    monkeypatch.setenv("RSP_ILU_NARROW_PAIRS", str(pairs))
     monkeypatch.setenv("RSP_ILU_NARROW_WAVES", str(waves))
     if group:
         monkeypatch.setenv("RSP_ILU_GROUP", str(group))
