@@ -1813,10 +1813,8 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         }
     };
     // The same on K waves with TWO consecutive levels per turn (a.narrow_pairs,
-    // RSP_ILU_NARROW_PAIRS, default on for L / L^T): wave w takes levels
-    // (q0 + 2 (w + jK), + 1). Deep set, same box: solve 15.70 -> 14.95 ms
-    // (dc1 5.19 -> 4.93, matrix-new_3 6.11 -> 5.81, G2_circuit 3.46 -> 3.20;
-    // thermomech_TK 0.95 -> 1.00). (The same for the thin factor's narrow
+    // RSP_ILU_NARROW_PAIRS; L / L^T of DAGs with small levels, see the
+    // launcher): wave w takes levels (q0 + 2 (w + jK), + 1). (The same for the thin factor's narrow
     // rounds measured 21.2 -> 26.0 ms — the second level's item preparation
     // lands on the chain — and was removed.)
     // The second level of a pair reads the first's y from this wave's own
@@ -2062,8 +2060,13 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
         const rsp::LevelSeg sg = P.segs[g];
         if (sg.thin) {
             // term groups of 2 for DAGs of short chains (the plan padded them so)
-            // (RSP_ILU_NARROW_PAIRS: the two-levels-per-turn narrow runs, L / L^T)
-            const bool pr = KIND != 2 && a.narrow_pairs;
+            // the two-levels-per-turn narrow runs (L / L^T): RSP_ILU_NARROW_PAIRS
+            // 1 / 0 forces them; by default (-1) for DAGs of <= 32 rows per
+            // level on average (the deep circuits: config 3, same box, dc1
+            // 5.18 -> 4.94 ms, matrix-new_3 6.09 -> 5.81, G2_circuit 3.45 ->
+            // 3.22; on wider DAGs' narrow runs they cost: parabolic_fem 3.55
+            // -> 3.95, Dubcova3 2.59 -> 2.84, thermomech_TK 0.95 -> 1.00)
+            const bool pr = KIND != 2 && (a.narrow_pairs > 0 || (a.narrow_pairs < 0 && a.n <= 32LL * P.nlev));
             auto kern = P.group == 2 ? (pr ? trsv_thin_pf<T, KIND, 2, KIND != 2> : trsv_thin_pf<T, KIND, 2>)
                                      : (pr ? trsv_thin_pf<T, KIND, 4, KIND != 2> : trsv_thin_pf<T, KIND, 4>);
             hipLaunchKernelGGL(kern, dim3(1), dim3(kThinThreads), 0, s, a, sg.c0, sg.c1, P.ptr_host[sg.lb]);

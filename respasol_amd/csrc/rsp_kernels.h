@@ -380,7 +380,7 @@ struct TrsvArgs {
     int wave_lds;               // fat-level wave rows: chain on LDS broadcast operands (RSP_ILU_WAVE_LDS)
     int narrow_waves;           // thin runs: waves sharing a narrow run, levels round-robin (RSP_ILU_NARROW_WAVES)
     int narrow_split;           // L / L^T narrow runs: one wave, early sums under the late loads (RSP_ILU_NARROW_SPLIT)
-    int narrow_pairs;           // L / L^T narrow runs on K waves, two levels per turn (RSP_ILU_NARROW_PAIRS, default 1)
+    int narrow_pairs;           // L / L^T narrow runs on K waves, two levels per turn (RSP_ILU_NARROW_PAIRS: 1 / 0, -1 auto)
     int flow;                   // run flow segments persistently (RSP_ILU_FLOW, default 1)
     int flow_grid;              // flow launch: 256-thread workgroups (RSP_ILU_FLOW_WPC waves per CU)
     int flow_cus;               // CUs of the device (caps a flow grid)
