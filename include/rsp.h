@@ -278,6 +278,17 @@ rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *level
 rsp_status_t rsp_ilu0_analysis_host(int n, const int *row_offsets, const int *col_ind,
                                     int *levels_lower, int *levels_upper, uint64_t *digest,
                                     double *phase_ms);
+/* Tests (no cuSPARSE counterpart, no device needed): the SpMV schedule
+ * rsp_spmv_buffer_size builds (tiles, 16-bit column offsets, staged tiles'
+ * column runs) for HOST arrays (base 0, m rows, compute type fp64 / fp32),
+ * checked for consistency: every entry of a 16-bit tile decodes to its own
+ * column (cbase + offset, or the staged tile's runs at its slot index), every
+ * staged tile's runs are ascending and within its slot and run caps. Returns
+ * the tile count, the entries read through 16-bit values and, of those, the
+ * entries of staged tiles; INTERNAL_ERROR if a check fails. */
+rsp_status_t rsp_spmv_plan_host(int m, const int *row_offsets, const int *col_ind, int64_t nnz,
+                                rsp_datatype_t compute_type, int64_t *tiles, int64_t *entries_16bit,
+                                int64_t *entries_staged);
 /* The digest of the plan an rsp_ilu0_analysis built (see above); computed
  * only when the environment sets RSP_ILU_DIGEST=1 at analysis time
  * (INVALID_VALUE otherwise). */

@@ -114,6 +114,7 @@ RSP_PROTOS = {
     "rsp_spmv_batch_info": (i32, [vp, vp, vp]),
     "rsp_spmv_plan_info": (i32, [vp, vp, vp]),
     "rsp_ilu0_analysis_host": (i32, [i32, vp, vp, vp, vp, vp, vp]),
+    "rsp_spmv_plan_host": (i32, [i32, vp, vp, C.c_int64, i32, vp, vp, vp]),
     "rsp_ilu0_plan_digest": (i32, [vp, vp]),
 }
 

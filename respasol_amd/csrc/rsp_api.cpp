@@ -1736,6 +1736,47 @@ static rsp_status_t rsp_ilu0_analysis_host_impl(int n, const int *row_offsets, c
     return RSP_STATUS_SUCCESS;
 }
 
+static rsp_status_t rsp_spmv_plan_host_impl(int m, const int *rp, const int *ci, int64_t nnz,
+                                            rsp_datatype_t type, int64_t *tiles, int64_t *e16,
+                                            int64_t *est) {
+    if (m < 0 || (m > 0 && (!rp || !ci)) || !tiles || !e16 || !est) return RSP_STATUS_INVALID_VALUE;
+    if (type != RSP_R_64F && type != RSP_R_32F) return RSP_STATUS_NOT_SUPPORTED;
+    TilePlan p;
+    make_tile_plan(rp, ci, m, nnz, type, 0, -1, true, p);
+    const int ucap = type == RSP_R_64F ? SpmvTile<double>::kStageSlots : SpmvTile<float>::kStageSlots;
+    for (size_t t = 0; t < p.blocks.size(); t++) {
+        const SpmvBlock &b = p.blocks[t];
+        const int cb = p.cbase[t];
+        if (cb == -1) continue;
+        for (int k = b.k0; k < b.k1; k++) {
+            int col;
+            if (cb >= 0) {
+                col = cb + p.c16[(size_t)k];
+            } else {
+                const int code = -2 - cb, nr = code & 255, off = code >> 8;
+                if (nr < 1 || nr > rsp::kStageRuns || (size_t)2 * (off + nr + 1) > p.runs.size())
+                    return RSP_STATUS_INTERNAL_ERROR;
+                const int *r = p.runs.data() + 2 * (size_t)off;
+                const int U = r[2 * nr + 1];
+                if (r[1] != 0 || U > ucap) return RSP_STATUS_INTERNAL_ERROR;
+                for (int j = 1; j <= nr; j++)
+                    if (r[2 * j + 1] <= r[2 * j - 1] || (j < nr && r[2 * j] <= r[2 * j - 2] + (r[2 * j + 1] - r[2 * j - 1]) - 1))
+                        return RSP_STATUS_INTERNAL_ERROR;
+                const int u = p.c16[(size_t)k];
+                if (u >= U) return RSP_STATUS_INTERNAL_ERROR;
+                int j = 0;
+                while (j + 1 < nr && r[2 * (j + 1) + 1] <= u) j++;
+                col = r[2 * j] + (u - r[2 * j + 1]);
+            }
+            if (col != ci[k]) return RSP_STATUS_INTERNAL_ERROR;
+        }
+    }
+    *tiles = (int64_t)p.blocks.size();
+    *e16 = p.nnz_c16;
+    *est = p.nnz_staged;
+    return RSP_STATUS_SUCCESS;
+}
+
 rsp_status_t rsp_ilu0_plan_digest(rsp_ilu0_info_t f, uint64_t *digest) {
     if (!f || !digest || !f->analysed || !f->digest) return RSP_STATUS_INVALID_VALUE;
     *digest = f->digest;
@@ -2119,6 +2160,13 @@ rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f
                             rsp_datatype_t value_type, const void *d_values, const void *d_x,
                             void *d_y) {
     return guarded([&] { return rsp_trsv_upper_impl(h, alpha, f, value_type, d_values, d_x, d_y); }, [] {});
+}
+
+rsp_status_t rsp_spmv_plan_host(int m, const int *row_offsets, const int *col_ind, int64_t nnz,
+                                rsp_datatype_t compute_type, int64_t *tiles, int64_t *entries_16bit,
+                                int64_t *entries_staged) {
+    return guarded([&] { return rsp_spmv_plan_host_impl(m, row_offsets, col_ind, nnz, compute_type, tiles,
+                                                        entries_16bit, entries_staged); }, [] {});
 }
 
 }  // extern "C"

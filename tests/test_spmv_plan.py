@@ -1,0 +1,64 @@
+"""The SpMV schedule on the host (rsp_spmv_plan_host, no device): tiles,
+16-bit column offsets and the staged tiles' column runs (spmv.hip
+stream_products_staged) decode back to every entry's own column; staged
+tiles appear where a tile's distinct columns are few (mesh / stencil) and not
+on random-band matrices; RSP_SPMV_STAGE_PCT moves the cut. The GPU tests
+(tests/test_gpu_spmv.py) hold the kernels on these plans to the oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from respasol_amd import _lib, csr
+
+R64, R32 = 1, 0  # RSP_R_64F / RSP_R_32F (include/rsp.h)
+
+
+def plan(A, dt):
+    rp = np.ascontiguousarray(A.rowptr, np.int32)
+    ci = np.ascontiguousarray(A.colidx, np.int32)
+    t, e16, est = C.c_int64(), C.c_int64(), C.c_int64()
+    st = _lib.rsp.rsp_spmv_plan_host(A.m, rp.ctypes.data, ci.ctypes.data, int(max(A.nnz, A.nnz_stored)), dt,
+                                     C.byref(t), C.byref(e16), C.byref(est))
+    return st, t.value, e16.value, est.value
+
+
+@pytest.mark.parametrize("dt", [R64, R32])
+@pytest.mark.parametrize("name,scale,staged", [("Serena", 0.02, True), ("Hook_1498", 0.02, True),
+                                               ("atmosmodd", 0.05, True), ("ecology2", 0.05, True),
+                                               ("cage13", 1.0, False), ("ASIC_320ks", 0.2, None),
+                                               ("dc1", 0.3, None)])
+def test_plan_decodes(name, scale, staged, dt):
+    A = csr.surrogate(name, scale)
+    st, tiles, e16, est = plan(A, dt)
+    assert st == 0 and tiles > 0 and 0 <= est <= e16 <= A.nnz_stored
+    if staged is True:
+        assert est > 0.5 * A.nnz_stored
+    elif staged is False:
+        assert est == 0
+
+
+def test_stage_share_knob(monkeypatch):
+    A = csr.surrogate("atmosmodd", 0.05)
+    got = []
+    for pct in (0, 30, 80, 100):
+        monkeypatch.setenv("RSP_SPMV_STAGE_PCT", str(pct))
+        st, _, e16, est = plan(A, R64)
+        assert st == 0
+        got.append(est)
+    assert got[0] == 0 and got == sorted(got) and got[-1] > 0
+
+
+def test_plan_odd_rows_and_bands():
+    """Rows of 1-9 entries (tiles starting inside a 16-B vector) in a band
+    wide enough for many short runs per tile, both dtypes."""
+    rng = np.random.default_rng(7)
+    n = 20000
+    rows = [np.unique(np.clip(i + rng.integers(-700, 701, 1 + i % 9), 0, n - 1)) for i in range(n)]
+    rp = np.zeros(n + 1, np.int32)
+    np.cumsum([len(r) for r in rows], out=rp[1:])
+    ci = np.concatenate(rows).astype(np.int32)
+    A = csr.CsrMatrix(0, n, n, len(ci), rp, ci, np.ones(len(ci)))
+    for dt in (R64, R32):
+        st, tiles, e16, est = plan(A, dt)
+        assert st == 0 and tiles > 0 and e16 == len(ci)
