@@ -483,6 +483,42 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
             c += std::max(8, c / 16);
         }
     }
+    // Random-band matrices (round 4): tiles whose columns lie in a band
+    // narrower than 65536 but scattered over it (more runs than a staged
+    // tile's run table holds) are staged by an explicit column LIST instead
+    // (below); that needs at most kStageSlots distinct columns per tile, so
+    // such a matrix is re-packed with tiles of at most kStageSlots entries
+    // (the canonical summation order does not depend on the packing). Judged
+    // on a sample of 64 tiles; not for spread plans (already small tiles).
+    const int ucap = type == RSP_R_64F ? SpmvTile<double>::kStageSlots : SpmvTile<float>::kStageSlots;
+    const bool list_ok = use_stage && use_c16 && type == RSP_R_64F && SpmvTile<double>::kStageList &&
+                         env_int("RSP_SPMV_STAGE_LIST", 1) != 0;
+    if (list_ok && (int64_t)p.blocks.size() == nb && nb > 0) {
+        int64_t band = 0, all = 0;
+        std::vector<int> cols;
+        const size_t step = std::max<size_t>(1, p.blocks.size() / 64);
+        for (size_t t = 0; t < p.blocks.size(); t += step) {
+            const SpmvBlock &bk = p.blocks[t];
+            if (bk.r1 < 0 || bk.k1 <= bk.k0) continue;
+            cols.assign(ci + bk.k0, ci + bk.k1);
+            std::sort(cols.begin(), cols.end());
+            cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+            int R = 1;
+            for (size_t u = 1; u < cols.size(); u++) R += cols[u] != cols[u - 1] + 1;
+            all += bk.k1 - bk.k0;
+            if (cols.back() - cols.front() <= 65535 && R > rsp::kStageRuns && (int)cols.size() > ucap)
+                band += bk.k1 - bk.k0;
+        }
+        if (2 * band > all) {
+            rsp_an::hvec<SpmvBlock> b2;
+            rsp_an::hvec<SpmvLongRow> l2;
+            int s2 = 0;
+            build_spmv_plan(rp, m, std::min(cap, ucap), chunk, b2, l2, &s2, maxrows, align);
+            p.blocks.swap(b2);
+            p.longrows.swap(l2);
+            p.nslots = s2;
+        }
+    }
     // split schedule (rsp_spmat_set_local_cols): tiles reading own columns
     // only first; long-row tiles always in the second part (with the fixup)
     p.nint = 0;
@@ -513,9 +549,9 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
     if (use_c16 && nnz_s > 0 && nnz_s <= nnz_bound) {
         p.c16.assign((size_t)nnz_s, 0);
         const long long nt = (long long)p.blocks.size();
-        const int ucap = type == RSP_R_64F ? SpmvTile<double>::kStageSlots : SpmvTile<float>::kStageSlots;
         const long long pct = std::min(std::max(env_int("RSP_SPMV_STAGE_PCT", 80), 0), 100);
         std::vector<std::vector<int>> truns(use_stage ? (size_t)nt : 0);
+        std::vector<char> tmode(use_stage ? (size_t)nt : 0, 0);  // 1 runs, 2 list
         std::atomic<int64_t> n16{0}, nst{0};
         rsp_an::parallel_for(nt, 64, [&](long long t0, long long t1) {
             std::vector<int> cols;
@@ -538,16 +574,27 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
                     const int U = (int)cols.size();
                     int R = 1;
                     for (int u = 1; u < U; u++) R += cols[(size_t)u] != cols[(size_t)u - 1] + 1;
-                    if (U <= ucap && R <= rsp::kStageRuns && 100LL * U <= pct * len) {
+                    const bool runs_mode = U <= ucap && R <= rsp::kStageRuns && 100LL * U <= pct * len;
+                    const bool list_mode = !runs_mode && list_ok && U <= ucap && R > rsp::kStageRuns;
+                    if (runs_mode || list_mode) {
                         std::vector<int> &r = truns[(size_t)t];
-                        r.reserve(2 * (size_t)(R + 1));
-                        for (int u = 0; u < U; u++)
-                            if (u == 0 || cols[(size_t)u] != cols[(size_t)u - 1] + 1) {
-                                r.push_back(cols[(size_t)u]);
-                                r.push_back(u);
-                            }
-                        r.push_back(0);
-                        r.push_back(U);
+                        tmode[(size_t)t] = runs_mode ? 1 : 2;
+                        if (runs_mode) {
+                            r.reserve(2 * (size_t)(R + 1));
+                            for (int u = 0; u < U; u++)
+                                if (u == 0 || cols[(size_t)u] != cols[(size_t)u - 1] + 1) {
+                                    r.push_back(cols[(size_t)u]);
+                                    r.push_back(u);
+                                }
+                            r.push_back(0);
+                            r.push_back(U);
+                        } else {  // {base column, U}, then the U column offsets as uint16, padded to 8 B
+                            r.assign(2 + 2 * (size_t)((U + 3) / 4), 0);
+                            r[0] = cols[0];
+                            r[1] = U;
+                            uint16_t *o = reinterpret_cast<uint16_t *>(r.data() + 2);
+                            for (int u = 0; u < U; u++) o[u] = (uint16_t)(cols[(size_t)u] - cols[0]);
+                        }
                         for (int k = bk.k0; k < bk.k1; k++)
                             p.c16[(size_t)k] = (uint16_t)(std::lower_bound(cols.begin(), cols.end(), ci[(size_t)k]) -
                                                           cols.begin());
@@ -568,7 +615,8 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
                 const std::vector<int> &r = truns[t];
                 if (r.empty()) continue;
                 const int64_t off = (int64_t)p.runs.size() / 2;
-                const int nr = (int)r.size() / 2 - 1;
+                // runs mode: descriptors + sentinel; list mode: 255 (header {base, U} + offsets)
+                const int nr = tmode[t] == 2 ? 255 : (int)r.size() / 2 - 1;
                 if (off >= (1LL << 22)) {  // (encoding range; never reached on real matrices)
                     p.nnz_c16 -= p.blocks[t].k1 - p.blocks[t].k0;
                     p.nnz_staged -= p.blocks[t].k1 - p.blocks[t].k0;
@@ -1754,6 +1802,21 @@ static rsp_status_t rsp_spmv_plan_host_impl(int m, const int *rp, const int *ci,
                 col = cb + p.c16[(size_t)k];
             } else {
                 const int code = -2 - cb, nr = code & 255, off = code >> 8;
+                if (nr == 255) {  // list mode (fp64): {base, U}, then U uint16 offsets
+                    if (type != RSP_R_64F) return RSP_STATUS_INTERNAL_ERROR;
+                    if ((size_t)2 * off + 2 > p.runs.size()) return RSP_STATUS_INTERNAL_ERROR;
+                    const int *r = p.runs.data() + 2 * (size_t)off;
+                    const int U = r[1];
+                    if (U < 1 || U > ucap || (size_t)2 * off + 2 + 2 * (size_t)((U + 3) / 4) > p.runs.size())
+                        return RSP_STATUS_INTERNAL_ERROR;
+                    const uint16_t *o = reinterpret_cast<const uint16_t *>(r + 2);
+                    for (int u = 1; u < U; u++)
+                        if (o[u] <= o[u - 1]) return RSP_STATUS_INTERNAL_ERROR;
+                    const int u = p.c16[(size_t)k];
+                    if (u >= U) return RSP_STATUS_INTERNAL_ERROR;
+                    if (r[0] + o[u] != ci[k]) return RSP_STATUS_INTERNAL_ERROR;
+                    continue;
+                }
                 if (nr < 1 || nr > rsp::kStageRuns || (size_t)2 * (off + nr + 1) > p.runs.size())
                     return RSP_STATUS_INTERNAL_ERROR;
                 const int *r = p.runs.data() + 2 * (size_t)off;

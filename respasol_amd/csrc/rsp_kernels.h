@@ -63,6 +63,10 @@ struct SpmvTile {
     // of them, loaded once into the LDS image as contiguous column runs (at
     // most kStageRuns); each entry then reads its x from LDS
     static constexpr int kStageSlots = sizeof(T) == 8 ? 1536 : 2048;
+    // list-staged tiles (random-band tiles: too many runs, so an explicit
+    // column list): fp64 only — the list's registers fit under fp64's 64-VGPR
+    // occupancy step but would cost fp32 a wave per SIMD (71 -> 77 VGPRs)
+    static constexpr bool kStageList = sizeof(T) == 8;
 };
 constexpr int kStageRuns = 254;  // run descriptors per staged tile (+1 sentinel <= 256 threads)
 

@@ -237,7 +237,8 @@ __device__ __forceinline__ void lds_barrier() {
 template <typename T, bool NT, int NTH = kSpmvThreads,
           int IT = SpmvTile<T>::kSlots / (kSpmvThreads * (16 / sizeof(T)))>
 __device__ __forceinline__ void stream_products_staged(const unsigned short *__restrict__ cidx, int2 rd,
-                                                       int nr, const T *__restrict__ vals,
+                                                       int nr, const int (&lsl)[SpmvTile<T>::kStageSlots / NTH],
+                                                       const T *__restrict__ vals,
                                                        const T *__restrict__ x, int kb, int k1,
                                                        T *__restrict__ lds) {
     constexpr int VW = 16 / sizeof(T);
@@ -259,38 +260,48 @@ __device__ __forceinline__ void stream_products_staged(const unsigned short *__r
         vv[it] = ld<NT>(reinterpret_cast<const V *>(vals + e));
     }
     __builtin_amdgcn_sched_barrier(0);
-    int2 *tab = reinterpret_cast<int2 *>(lds + SpmvTile<T>::kSlots) - (nr + 1);
-    if (tid <= nr) tab[tid] = rd;
-    lds_barrier();
-    const int U = tab[nr].y;
-    int us[SMAX], lo[SMAX];
-#pragma unroll
-    for (int k = 0; k < SMAX; ++k) {
-        us[k] = min(k * NTH + tid, U - 1);
-        lo[k] = 0;
-    }
-    for (int n = nr; n > 1;) {  // largest r with tab[r].y <= u (tab[0].y = 0); nr is uniform
-        const int h = n >> 1;
-#pragma unroll
-        for (int k = 0; k < SMAX; ++k)
-            if (tab[lo[k] + h].y <= us[k]) lo[k] += h;
-        n -= h;
-    }
     // x through a buffer resource: 32-bit byte offsets instead of 64-bit
     // addresses (fewer VGPRs; num_records covers the whole of x)
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7ffffffc, 0x00020000);
+    auto xload = [&](int col) {
+        if constexpr (sizeof(T) == 8)
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr, col * 8, 0, 0));
+        else
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(xr, col * 4, 0, 0));
+    };
     T xs[SMAX];
+    int U;
+    if (SpmvTile<T>::kStageList && nr == 255) {  // list mode (workgroup-uniform): the slots' columns came with the tile
+        U = rd.y;
 #pragma unroll
-    for (int k = 0; k < SMAX; ++k)
-        if (k * NTH < U) {  // workgroup-uniform
-            const int2 r = tab[lo[k]];
-            const int off = (r.x + (us[k] - r.y)) * (int)sizeof(T);
-            if constexpr (sizeof(T) == 8)
-                xs[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
-            else
-                xs[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
+        for (int k = 0; k < SMAX; ++k)
+            if (k * NTH < U) xs[k] = xload(rd.x + lsl[k]);
+    } else {  // runs mode: the run table at the end of the LDS image, a search per slot
+        int2 *tab = reinterpret_cast<int2 *>(lds + SpmvTile<T>::kSlots) - (nr + 1);
+        if (tid <= nr) tab[tid] = rd;
+        lds_barrier();
+        U = tab[nr].y;
+        int us[SMAX], lo[SMAX];
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            us[k] = min(k * NTH + tid, U - 1);
+            lo[k] = 0;
         }
+        for (int n = nr; n > 1;) {  // largest r with tab[r].y <= u (tab[0].y = 0); nr is uniform
+            const int h = n >> 1;
+#pragma unroll
+            for (int k = 0; k < SMAX; ++k)
+                if (tab[lo[k] + h].y <= us[k]) lo[k] += h;
+            n -= h;
+        }
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k)
+            if (k * NTH < U) {  // workgroup-uniform
+                const int2 r = tab[lo[k]];
+                xs[k] = xload(r.x + (us[k] - r.y));
+            }
+    }
 #pragma unroll
     for (int k = 0; k < SMAX; ++k)
         if (k * NTH < U && k * NTH + tid < U) lds[k * NTH + tid] = xs[k];
@@ -447,12 +458,22 @@ __device__ __forceinline__ void spmv_tile(
     // a staged tile's run descriptors: the first load of the tile, so the x
     // loads they lead to need not wait for the stream (vmcnt is in order)
     const bool staged = cbase <= -2;
+    constexpr int SMAX = SpmvTile<T>::kStageSlots / kSpmvThreads;
     int2 rd = make_int2(0, 0);
     int nr = 0;
+    int lsl[SMAX];  // list mode: this thread's slots' column offsets
     if (staged) {  // workgroup-uniform
         const int code = -2 - cbase;
         nr = code & 255;
-        if (tid <= nr) rd = reinterpret_cast<const int2 *>(runs)[(code >> 8) + tid];
+        if (SpmvTile<T>::kStageList && nr == 255) {  // list mode: {base, U}, then U uint16 column offsets
+            rd = reinterpret_cast<const int2 *>(runs)[code >> 8];
+            const unsigned short *lst = reinterpret_cast<const unsigned short *>(runs + 2 * (code >> 8) + 2);
+#pragma unroll
+            for (int k = 0; k < SMAX; ++k)
+                if (k * kSpmvThreads < rd.y) lsl[k] = lst[min(k * kSpmvThreads + tid, rd.y - 1)];
+        } else if (tid <= nr) {
+            rd = reinterpret_cast<const int2 *>(runs)[(code >> 8) + tid];
+        }
     }
     // the tile's row offsets, loaded ahead of the stream and parked in LDS
     // after it, so the reduce never waits on global memory
@@ -499,7 +520,7 @@ __device__ __forceinline__ void spmv_tile(
     if (vec && cbase >= 0)
         stream_products<T, NT, true>(colidx, cidx, cbase, cmax, vals, x, kb, k1, lds);
     else if (vec && staged)
-        stream_products_staged<T, NT>(cidx, rd, nr, vals, x, kb, k1, lds);
+        stream_products_staged<T, NT>(cidx, rd, nr, lsl, vals, x, kb, k1, lds);
     else if (vec)
         stream_products<T, NT>(colidx, cidx, 0, 0, vals, x, kb, k1, lds);
     else

@@ -1,8 +1,9 @@
 """The SpMV schedule on the host (rsp_spmv_plan_host, no device): tiles,
 16-bit column offsets and the staged tiles' column runs (spmv.hip
 stream_products_staged) decode back to every entry's own column; staged
-tiles appear where a tile's distinct columns are few (mesh / stencil) and not
-on random-band matrices; RSP_SPMV_STAGE_PCT moves the cut. The GPU tests
+tiles appear where a tile's distinct columns are few (mesh / stencil), list
+tiles (column list instead of runs, fp64) on random-band matrices, neither with
+RSP_SPMV_STAGE_LIST=0; RSP_SPMV_STAGE_PCT moves the cut. The GPU tests
 (tests/test_gpu_spmv.py) hold the kernels on these plans to the oracle."""
 import ctypes as C
 
@@ -11,7 +12,7 @@ import pytest
 
 from respasol_amd import _lib, csr
 
-R64, R32 = 1, 0  # RSP_R_64F / RSP_R_32F (include/rsp.h)
+R64, R32 = 0, 1  # RSP_R_64F / RSP_R_32F (include/rsp.h)
 
 
 def plan(A, dt):
@@ -26,16 +27,20 @@ def plan(A, dt):
 @pytest.mark.parametrize("dt", [R64, R32])
 @pytest.mark.parametrize("name,scale,staged", [("Serena", 0.02, True), ("Hook_1498", 0.02, True),
                                                ("atmosmodd", 0.05, True), ("ecology2", 0.05, True),
-                                               ("cage13", 1.0, False), ("ASIC_320ks", 0.2, None),
+                                               ("cage13", 1.0, "list"), ("ASIC_320ks", 0.2, None),
                                                ("dc1", 0.3, None)])
-def test_plan_decodes(name, scale, staged, dt):
+def test_plan_decodes(name, scale, staged, dt, monkeypatch):
     A = csr.surrogate(name, scale)
     st, tiles, e16, est = plan(A, dt)
     assert st == 0 and tiles > 0 and 0 <= est <= e16 <= A.nnz_stored
-    if staged is True:
-        assert est > 0.5 * A.nnz_stored
-    elif staged is False:
+    if staged == "list" and dt == R32:  # list tiles are fp64 only (rsp_kernels.h kStageList)
         assert est == 0
+    elif staged:
+        assert est > 0.5 * A.nnz_stored
+    if staged == "list":
+        monkeypatch.setenv("RSP_SPMV_STAGE_LIST", "0")
+        st, tiles, e16, est = plan(A, dt)
+        assert st == 0 and est == 0
 
 
 def test_stage_share_knob(monkeypatch):
