@@ -342,6 +342,50 @@ def test_staged_tiles_same_bits(monkeypatch, pct):
         h.close()
 
 
+@pytest.mark.parametrize("lst", ["1", "0"])
+def test_list_staged_tiles_same_bits(monkeypatch, lst):
+    """List-staged tiles (fp64 random-band tiles: an explicit column list
+    instead of runs, the matrix re-packed with tiles of <= 1536 entries;
+    RSP_SPMV_STAGE_LIST=0 turns them off): cage13 and Si87H76 at full size,
+    the plan checked on the host to hold list tiles, then single calls and a
+    batch bitwise the canonical-order oracle in both settings (fp32 keeps
+    its plan and is covered by test_staged_tiles_same_bits)."""
+    import ctypes as C
+    from respasol_amd import _lib
+    from respasol_amd.sparse import SpmvBatch
+    monkeypatch.setenv("RSP_SPMV_STAGE_LIST", lst)
+    h = Handle()
+    try:
+        mats = [csr.surrogate(nm, 1.0) for nm in ("cage13", "Si87H76")]
+        dt = torch.float64
+        xs, ys, ms, refs = [], [], [], []
+        for A in mats:
+            rp = np.ascontiguousarray(A.rowptr, np.int32)
+            ci = np.ascontiguousarray(A.colidx, np.int32)
+            t, e16, est = C.c_int64(), C.c_int64(), C.c_int64()
+            assert _lib.rsp.rsp_spmv_plan_host(A.m, rp.ctypes.data, ci.ctypes.data, int(A.nnz_stored), 0,
+                                               C.byref(t), C.byref(e16), C.byref(est)) == 0
+            assert (est.value > 0.5 * A.nnz_stored) if lst == "1" else est.value == 0
+            x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
+            ref = ob.spmv(A.rowptr, A.colidx, A.values, x, order="canon")
+            M = SpMat(h, *upload_csr(A.rowptr, A.colidx, A.values, dt), A.n)
+            xd = torch.from_numpy(x).cuda()
+            y = torch.empty(A.m, dtype=dt, device="cuda")
+            M.spmv(xd, y)
+            torch.cuda.synchronize()
+            assert same_bits(y.cpu().numpy(), ref)
+            ms.append(M)
+            xs.append(xd)
+            ys.append(torch.empty(A.m, dtype=dt, device="cuda"))
+            refs.append(ref)
+        SpmvBatch(h, ms, xs, ys).run()
+        torch.cuda.synchronize()
+        for r, y in zip(refs, ys):
+            assert same_bits(y.cpu().numpy(), r)
+    finally:
+        h.close()
+
+
 def test_shared_workspace_alternating(handle):
     """Several matrices may share one SpMV workspace (cusparseSpMV treats it
     as scratch). The schedule lives in each matrix (built at bufferSize), so
