@@ -365,7 +365,8 @@ def test_list_staged_tiles_same_bits(monkeypatch, lst):
             t, e16, est = C.c_int64(), C.c_int64(), C.c_int64()
             assert _lib.rsp.rsp_spmv_plan_host(A.m, rp.ctypes.data, ci.ctypes.data, int(A.nnz_stored), 0,
                                                C.byref(t), C.byref(e16), C.byref(est)) == 0
-            assert (est.value > 0.5 * A.nnz_stored) if lst == "1" else est.value == 0
+            # (with the lists off a few of Si87H76's tiles still qualify for runs)
+            assert (est.value > 0.5 * A.nnz_stored) if lst == "1" else est.value < 0.1 * A.nnz_stored
             x, _ = csr.dlarnv(1, [0, 0, 0, 1], A.n)
             ref = ob.spmv(A.rowptr, A.colidx, A.values, x, order="canon")
             M = SpMat(h, *upload_csr(A.rowptr, A.colidx, A.values, dt), A.n)
