@@ -513,7 +513,9 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
             rsp_an::hvec<SpmvBlock> b2;
             rsp_an::hvec<SpmvLongRow> l2;
             int s2 = 0;
-            build_spmv_plan(rp, m, std::min(cap, ucap), chunk, b2, l2, &s2, maxrows, align);
+            // RSP_SPMV_LIST_CAP (A/B knob): a smaller tile for the re-packed plan
+            const int lcap = std::min(std::max(env_int("RSP_SPMV_LIST_CAP", ucap), 64), ucap);
+            build_spmv_plan(rp, m, std::min(cap, lcap), chunk, b2, l2, &s2, maxrows, align);
             p.blocks.swap(b2);
             p.longrows.swap(l2);
             p.nslots = s2;
