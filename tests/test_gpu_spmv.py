@@ -346,7 +346,8 @@ def test_staged_tiles_same_bits(monkeypatch, pct):
 def test_list_staged_tiles_same_bits(monkeypatch, lst):
     """List-staged tiles (fp64 random-band tiles: an explicit column list
     instead of runs, the matrix re-packed with tiles of <= 1536 entries;
-    RSP_SPMV_STAGE_LIST=0 turns them off): cage13 and Si87H76 at full size,
+    RSP_SPMV_STAGE_LIST=0 turns them off): cage13 and Si87H76 at full size
+    and a ragged random band (tiles starting inside a 16-B vector),
     the plan checked on the host to hold list tiles, then single calls and a
     batch bitwise the canonical-order oracle in both settings (fp32 keeps
     its plan and is covered by test_staged_tiles_same_bits)."""
@@ -357,6 +358,13 @@ def test_list_staged_tiles_same_bits(monkeypatch, lst):
     h = Handle()
     try:
         mats = [csr.surrogate(nm, 1.0) for nm in ("cage13", "Si87H76")]
+        rng = np.random.default_rng(11)  # ragged rows (1-15 entries) in a +-20000 band
+        n = 60000
+        rows = [np.unique(np.clip(i + rng.integers(-20000, 20001, 1 + i % 15), 0, n - 1)) for i in range(n)]
+        rp = np.zeros(n + 1, np.int32)
+        np.cumsum([len(r) for r in rows], out=rp[1:])
+        cc = np.concatenate(rows).astype(np.int32)
+        mats.append(csr.CsrMatrix(0, n, n, len(cc), rp, cc, rng.uniform(-1, 1, len(cc))))
         dt = torch.float64
         xs, ys, ms, refs = [], [], [], []
         for A in mats:

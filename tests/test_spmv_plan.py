@@ -67,3 +67,25 @@ def test_plan_odd_rows_and_bands():
     for dt in (R64, R32):
         st, tiles, e16, est = plan(A, dt)
         assert st == 0 and tiles > 0 and e16 == len(ci)
+
+
+def test_plan_list_tiles_ragged_band(monkeypatch):
+    """A random band of +-20000 columns with rows of 1-15 entries: every
+    fp64 tile has more runs than the table holds, so the plan goes to list
+    tiles (re-packed, and each list decodes back to the entries' columns);
+    fp32 keeps gathered tiles; RSP_SPMV_STAGE_LIST=0 turns the lists off."""
+    rng = np.random.default_rng(11)
+    n = 60000
+    rows = [np.unique(np.clip(i + rng.integers(-20000, 20001, 1 + i % 15), 0, n - 1)) for i in range(n)]
+    rp = np.zeros(n + 1, np.int32)
+    np.cumsum([len(r) for r in rows], out=rp[1:])
+    ci = np.concatenate(rows).astype(np.int32)
+    A = csr.CsrMatrix(0, n, n, len(ci), rp, ci, np.ones(len(ci)))
+    st, tiles, e16, est = plan(A, R64)
+    assert st == 0 and e16 == len(ci) and est > 0.9 * len(ci)
+    assert tiles >= len(ci) // 1536
+    st, _, _, est32 = plan(A, R32)
+    assert st == 0 and est32 == 0
+    monkeypatch.setenv("RSP_SPMV_STAGE_LIST", "0")
+    st, _, _, est = plan(A, R64)
+    assert st == 0 and est == 0
