@@ -1220,14 +1220,30 @@ static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool
     long long nlo = 0;
     for (int i = 0; i < n; i++) nlo += dpos[(size_t)i] - rp[(size_t)i];
     hp.L.batch = hp.LT.batch = chain_batch(nlo, n);
-    // thin-run term groups: the reference order (default) 2 for DAGs of
-    // short chains (chain_batch), else 4; the split order (RSP_ILU_SPLIT=1)
-    // 2 where a row's two parts are short on average (mean chain <= 5 terms)
-    const int g_dflt = hp.split ? (n > 0 && (double)nlo / n <= 5.0 ? 2 : 4) : (hp.L.batch == 2 ? 2 : 4);
-    for (DagHost *d : {&hp.L, &hp.LT})
-        d->group = env_int("RSP_ILU_GROUP", g_dflt) == 2 ? 2 : 4;
     auto cnt_l = [&](int i) { return dpos[(size_t)i] - rp[(size_t)i]; };
     auto cnt_lt = [&](int i) { return ltp[(size_t)i + 1] - ltp[(size_t)i]; };
+    // thin-run term groups, per DAG. Reference order (default): 2 only where
+    // groups of 4 would save almost no groups (sum ceil(c/2) <= 1.15 sum
+    // ceil(c/4): chains of <= 2 terms, the 2-D grids), else 4 — a circuit's
+    // short mean chain hides hub rows of thousands of terms (config 3, same
+    // box: G2_circuit solve 3.21 -> 2.66 ms, ASIC_320ks 1.52 -> 1.31, ss1
+    // 1.34 -> 1.16 against the round-3 rule of 2 for every DAG of mean chain
+    // <= 2.5; ecology2 / tmt_unsym keep 2: 4.26 / 4.22 against 4.49 / 4.45 ms
+    // with 4; profiles/r04_ilu_group_ab.txt). Split order (RSP_ILU_SPLIT=1):
+    // 2 where a row's two parts are short on average (mean chain <= 5 terms).
+    auto group_of = [&](auto cnt) {
+        if (hp.split) return n > 0 && (double)nlo / n <= 5.0 ? 2 : 4;
+        long long s2 = 0, s4 = 0;
+        for (int i = 0; i < n; i++) {
+            const int c = cnt(i);
+            s2 += (c + 1) / 2;
+            s4 += (c + 3) / 4;
+        }
+        return 100 * s2 <= 115 * s4 ? 2 : 4;
+    };
+    const int g_env = env_int("RSP_ILU_GROUP", 0);
+    hp.L.group = g_env ? (g_env == 2 ? 2 : 4) : group_of(cnt_l);
+    hp.LT.group = g_env ? (g_env == 2 ? 2 : 4) : group_of(cnt_lt);
     // split term order (IluHostPlan::lpos): early terms first
     auto ne_l = [&](int i) { return hp.ne_l[(size_t)i]; };
     auto ne_lt = [&](int i) { return hp.ne_lt[(size_t)i]; };
