@@ -317,7 +317,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
         for (int l = sg.lb; l < sg.le; l++) thin_lev[(size_t)l] = (char)sg.thin;
     // within each level (stable): short rows, then wave rows, then (fat
     // levels) hub rows
-    const int fat_long = env_int("RSP_ILU_FAT_LONG", rsp::kFatLongTerms);
+    const int fat_long = env_int("RSP_ILU_FAT_LONG", rsp::kFatLongDefault);
     const int hub = env_int("RSP_ILU_HUB", rsp::kHubTerms);
     sp.nshort.assign((size_t)std::max(nlev, 1), 0);
     sp.nwave.assign((size_t)std::max(nlev, 1), 0);

@@ -209,7 +209,11 @@ struct LevelPlan {
 };
 constexpr int kLongTerms = 64;       // thin-run solve rows with more terms are done by a whole wave
 constexpr int kHubTerms = 256;       // fat-level solve rows with more terms: a workgroup each (RSP_ILU_HUB)
-constexpr int kFatLongTerms = 8;     // fat-level solve rows with more terms: a wave each (RSP_ILU_FAT_LONG)
+constexpr int kFatLongTerms = 8;     // padded short-row layout: a short row's flat terms (RSP_ILU_FAT_LONG=8)
+// fat-level solve rows with more terms than this: a wave each (RSP_ILU_FAT_LONG; round 4: 8 -> 3,
+// config-3 solve 42.5 -> 41.6 ms, para-10 -19 %, 2cubes_sphere -22 %, profiles/r04_ilu_fatlong_ab.txt;
+// the padded layout needs 8, so it is used only when the knob asks for 8)
+constexpr int kFatLongDefault = 3;
 constexpr int kYWin = 4096;          // LDS y window of a thin solve run (entries, power of 2)
 constexpr int kChunkRows = 1024;     // rows staged per thin-run chunk (<= kYWin)
 constexpr int kChunkTerms = 4096;    // terms staged per thin-run chunk

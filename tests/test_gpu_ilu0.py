@@ -215,15 +215,18 @@ def test_factor_plan_pieces(handle, monkeypatch, piece, name, scale):
     compare(A, torch.float32, handle, x=x)
 
 
-@pytest.mark.parametrize("slot,lds,pad,wlds", [(0, 1, 0, 0), (0, 0, 1, 1), (1, 1, 1, 1), (1, 1, 1, 0)])
+@pytest.mark.parametrize("slot,lds,pad,wlds,flong", [(0, 1, 0, 0, 3), (0, 0, 1, 1, 8), (1, 1, 1, 1, 8),
+                                                     (1, 1, 1, 0, 3), (1, 1, 0, 1, 1)])
 @pytest.mark.parametrize("name,scale", [("FEM_3D_thermal2", 0.1), ("Goodwin_095", 0.1), ("crashbasis", 0.1),
                                         ("ASIC_320ks", 0.1)])
-def test_fat_level_paths(handle, monkeypatch, slot, lds, pad, wlds, name, scale):
+def test_fat_level_paths(handle, monkeypatch, slot, lds, pad, wlds, flong, name, scale):
     """Every level forced fat, through each row kernel: factor rows in the
     slot layout (one round trip for a row's structure), the FacRow + LDS
     kernel and the global-memory path; solve short rows with padded flat terms
-    (values loaded with the task) or unpadded; wave rows chained on LDS
-    broadcast operands or on readlanes — the same bits."""
+    (values loaded with the task; the padded layout needs the 8-term short-row
+    cut) or unpadded, rows past 1 / 3 (default) / 8 terms a wave each; wave
+    rows chained on LDS broadcast operands or on readlanes — the same bits."""
+    monkeypatch.setenv("RSP_ILU_FAT_LONG", str(flong))
     monkeypatch.setenv("RSP_ILU_WAVE_LDS", str(wlds))
     monkeypatch.setenv("RSP_ILU_FAT_SLOT", str(slot))
     monkeypatch.setenv("RSP_ILU_FAT_LDS", str(lds))
@@ -351,7 +354,7 @@ def test_device_analysis_same_plan_as_host(handle, monkeypatch, name, scale):
 
 @pytest.mark.parametrize("knobs", [{"RSP_ILU_THIN_SOLVE": "0"}, {"RSP_ILU_THIN_SOLVE": "1"},
                                    {"RSP_ILU_GROUP": "2"}, {"RSP_ILU_FAT_PAD": "0"},
-                                   {"RSP_ILU_THIN_TERMS": "64"}])
+                                   {"RSP_ILU_THIN_TERMS": "64"}, {"RSP_ILU_FAT_LONG": "8"}])
 @pytest.mark.parametrize("name,scale", [("dc1", 0.3), ("stomach", 0.05), ("ecology2", 0.05)])
 def test_device_solve_terms_same_plan_under_schedule_knobs(handle, monkeypatch, knobs, name, scale):
     """The device-built per-term solve plan equals the host's whatever the
