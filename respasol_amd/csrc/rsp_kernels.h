@@ -235,7 +235,10 @@ constexpr int kRndItems = 2048;
 constexpr int kRndPairs = 4096;
 constexpr int kRndStaged = 4096;
 constexpr int kRndRounds = 2048;
-constexpr int kRndLevelItems = 2048;
+// hub levels (a row past the slot layout, so no flow launch) run thin up to this many positions
+// (round 4: 2048 -> 32768, config-3 factor 58.8 -> 57.2 ms: dc1 7.38 -> 7.02, ASIC_320ks 2.46 -> 1.92,
+// ss1 1.86 -> 1.47; larger gains nothing; profiles/r04_ilu_factor_ab.txt)
+constexpr int kRndLevelItems = 1 << 15;
 constexpr int kRndFlowItems = 1024;  // ... kRndFlowItems if the level could run in a flow launch
 constexpr int kRndItemPairs = 1024;
 constexpr int kRndLevelStart = 1 << 15;  // rounds[]: this round opens a level (or a chunk)
