@@ -5,6 +5,14 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload big|moderate|NAME]
     torchrun --nproc-per-node N ... bench.py --gpus N ...      (N > 1, RCCL)
 
+With --gpus N > 1 and no WORLD_SIZE in the environment (a plain `python
+bench.py --gpus N`), bench.py launches the N ranks itself: N child processes
+(one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+MASTER_PORT set), spawned before anything loads the HIP runtime; the parent
+relays rank 0's JSON line and exits non-zero if any rank fails. Under
+torchrun the ranks come from the environment; --gpus must equal WORLD_SIZE,
+and with the nccl backend every rank needs a GPU of its own.
+
 Workload (default "big"): one step = one fp64 y = A x over EACH of the 15
 "big" SuiteSparse matrices (BASELINE config 4; seeded surrogates of the same
 m / stored nnz / structure, since no .mtx data exists offline). With N > 1
@@ -32,19 +40,130 @@ import argparse
 import glob
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from respasol_amd import csr  # noqa: E402
-from respasol_amd.dist import HaloExchange, HaloSlice, RowPartitionedSpmv, remap_columns  # noqa: E402
-from respasol_amd.sparse import Handle, SpMat, SpmvBatch, upload_csr  # noqa: E402
+# product modules (they map librsp.so) and torch: imported by _import_product()
+# once this process is known to be a rank, never in the launcher parent
+np = torch = dist = csr = None
+HaloExchange = HaloSlice = RowPartitionedSpmv = remap_columns = None
+Handle = SpMat = SpmvBatch = upload_csr = None
+
+
+def _import_product():
+    global np, torch, dist, csr, HaloExchange, HaloSlice, RowPartitionedSpmv, remap_columns
+    global Handle, SpMat, SpmvBatch, upload_csr
+    import numpy as np_
+    import torch as torch_
+    import torch.distributed as dist_
+    from respasol_amd import csr as csr_
+    from respasol_amd import dist as rd
+    from respasol_amd import sparse as sp
+    np, torch, dist, csr = np_, torch_, dist_, csr_
+    HaloExchange, HaloSlice, RowPartitionedSpmv, remap_columns = (rd.HaloExchange, rd.HaloSlice,
+                                                                  rd.RowPartitionedSpmv, rd.remap_columns)
+    Handle, SpMat, SpmvBatch, upload_csr = sp.Handle, sp.SpMat, sp.SpmvBatch, sp.upload_csr
+
+
+# ---------------------------------------------------------------- launcher
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, base_env, port, addr="127.0.0.1"):
+    """The environment of each of the n ranks a single-node launch starts (the
+    variables torch.distributed.run sets that bench.py and init_process_group
+    read)."""
+    envs = []
+    for r in range(n):
+        e = dict(base_env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                  "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "NODE_RANK": "0",
+                  "MASTER_ADDR": addr, "MASTER_PORT": str(port),
+                  "HSA_ENABLE_IPC_MODE_LEGACY": base_env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+                  "PYTHONUNBUFFERED": "1"})
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n, child_argv, base_env=None, timeout=None, out=None):
+    """Start n rank processes (child_argv each, environments from rank_envs),
+    relay rank 0's stdout to `out` (default sys.stdout; the other ranks'
+    stdout goes to stderr), wait for all of them. If one fails, the others are
+    terminated. Returns the exit code: 0 only if every rank exited 0."""
+    base_env = dict(os.environ if base_env is None else base_env)
+    out = sys.stdout if out is None else out
+    procs = []
+    for r, env in enumerate(rank_envs(n, base_env, free_port())):
+        procs.append(subprocess.Popen(child_argv, env=env, stdout=subprocess.PIPE if r == 0 else 2,
+                                      start_new_session=True, text=True))
+    # rank 0's stdout is drained on a thread, so a full pipe never blocks it
+    import threading
+
+    def pump():
+        for line in procs[0].stdout:
+            out.write(line)
+            out.flush()
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    t0 = time.time()
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0:
+                print(f"bench.py launcher: rank {r} exited with {c}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                rc = rc or (c if c > 0 else 1)
+                for q in live:
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        if timeout is not None and time.time() - t0 > timeout and live:
+            print("bench.py launcher: time limit reached; stopping the ranks", file=sys.stderr, flush=True)
+            for q in live:
+                try:
+                    os.killpg(procs[q].pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+            rc = rc or 124
+            timeout = None
+        time.sleep(0.05)
+    th.join(timeout=10)
+    return rc
+
+
+def visible_gpus():
+    """GPUs this process could use, counted without initialising the HIP
+    runtime (torch.cuda.device_count() does not on this image)."""
+    import torch as torch_
+    return int(torch_.cuda.device_count())
+
+
+def check_world(args, world, n_visible):
+    """None if this rank may run, else the reason it must not: --gpus must
+    equal the launched world, and the nccl backend needs one GPU per rank."""
+    if args.gpus != world:
+        return (f"--gpus {args.gpus} but WORLD_SIZE is {world}: the JSON line would name the wrong "
+                f"number of GPUs")
+    if world > 1 and args.dist_backend == "nccl" and n_visible < world:
+        return (f"--gpus {world} with the nccl backend needs {world} GPUs, {n_visible} visible "
+                f"(use --dist-backend gloo only to rehearse N > 1 ranks sharing one GPU)")
+    return None
+
 
 METRIC = "CSR SpMV GFLOP/s + achieved HBM GB/s (fp64 vs fp32), SuiteSparse set, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -377,7 +496,7 @@ class Workload:
         return float(tot[0]), float(tot[1])
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -410,11 +529,33 @@ def main():
                     help="skip the Serena-only step (BASELINE config 5) reported beside the big set")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
-    args = ap.parse_args()
+    ap.add_argument("--launch-timeout", type=float, default=0.0,
+                    help="launcher mode: stop every rank after this many seconds (0: no limit)")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # plain `python bench.py --gpus N`: launch the N ranks here, before
+        # anything in this process touches the GPU
+        why = check_world(args, args.gpus, visible_gpus())
+        if why:
+            print(f"bench.py: {why}", file=sys.stderr, flush=True)
+            sys.exit(2)
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                              timeout=args.launch_timeout or None))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    why = check_world(args, world, visible_gpus())
+    if why:
+        print(f"bench.py (rank {rank}): {why}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    _import_product()
     dev = local % max(torch.cuda.device_count(), 1)  # == local on a full node
     torch.cuda.set_device(dev)
     device = torch.device("cuda", dev)

@@ -2006,6 +2006,7 @@ template <typename T, int B>
 static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
     const LevelPlan &P = a.plan;
     int fr = 0;  // next flow run (sorted by level)
+    int flow_launched = 0;
     if (a.flow && a.nfruns > 0) {  // the flow rows' upper values become kNotYet (ilu0_flow_prep)
         const int nitems = a.fruns[a.nfruns - 1].c1;
         hipLaunchKernelGGL((ilu0_flow_prep<T>), dim3((nitems + 3) / 4), dim3(256), 0, s, a, nitems);
@@ -2023,6 +2024,7 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
                 const int grid = flow_grid<ilu0_flow<T>>(a.flow_grid, a.flow_cus, r.c1 - r.c0);
                 const unsigned long long base = flow_claims(a.fc, r.c1 - r.c0, grid);
                 hipLaunchKernelGGL((ilu0_flow<T>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, base);
+                ++flow_launched;
                 l = r.le - 1;
                 continue;
             }
@@ -2045,6 +2047,10 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
                                    dim3(64 * kIluWaves), 0, s, a, off, cnt);
         }
     }
+    // ilu0_flow_prep tagged the upper values of EVERY flow run's rows; only the
+    // run's own launch restores them. A run the level walk skipped would leave
+    // its rows tagged (a corrupt factor reported as success): fail the call.
+    if (a.flow && flow_launched != a.nfruns) return hipErrorLaunchFailure;
     return hipGetLastError();
 }
 

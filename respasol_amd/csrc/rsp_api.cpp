@@ -552,6 +552,7 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
         p.c16.assign((size_t)nnz_s, 0);
         const long long nt = (long long)p.blocks.size();
         const long long pct = std::min(std::max(env_int("RSP_SPMV_STAGE_PCT", 80), 0), 100);
+        const int64_t xelem = type == RSP_R_64F ? 8 : 4;
         std::vector<std::vector<int>> truns(use_stage ? (size_t)nt : 0);
         std::vector<char> tmode(use_stage ? (size_t)nt : 0, 0);  // 1 runs, 2 list
         std::atomic<int64_t> n16{0}, nst{0};
@@ -569,7 +570,11 @@ static void make_tile_plan(const int *rp, const int *ci, int m, int64_t nnz_boun
                 if (hi - lo > 65535) continue;
                 const int len = bk.k1 - bk.k0;
                 c16n += len;
-                if (use_stage && bk.r1 >= 0) {  // (long-row chunks keep the offsets)
+                // staged x loads use 32-bit byte offsets into a buffer resource of
+                // 0x7ffffffc bytes (spmv.hip stream_products_staged): a tile whose
+                // columns reach past that keeps the plain 16-bit offsets
+                const bool x_in_rsrc = ((int64_t)hi + 1) * xelem <= (int64_t)0x7ffffffc;
+                if (use_stage && bk.r1 >= 0 && x_in_rsrc) {  // (long-row chunks keep the offsets)
                     cols.assign(ci + bk.k0, ci + bk.k1);
                     std::sort(cols.begin(), cols.end());
                     cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
@@ -2062,13 +2067,15 @@ static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alp
 
 // A solve call of kind `which` (RSP_TRSV_*): its generation (status word
 // 2 + which; generations restart with the factor's wrap-around below 2^30).
-static void trsv_begin(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp::TrsvArgs &a) {
+static hipError_t trsv_begin(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp::TrsvArgs &a) {
     int &g = f->solve_gen[which];
     if (g >= (1 << 30)) {  // wrap: no stale give-up may match a new generation
-        (void)hipMemsetD32Async(f->d_zero + 2 + which, 0, 1, h->stream);
+        const hipError_t e = hipMemsetD32Async(f->d_zero + 2 + which, 0, 1, h->stream);
+        if (e != hipSuccess) return e;
         g = 0;
     }
     a.fc = flow_ctl(f, 2 + which, ++g);
+    return hipSuccess;
 }
 
 static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op, const void *alpha,
@@ -2094,7 +2101,7 @@ static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op,
     hipError_t e;
     const bool f64 = value_type == RSP_R_64F, ftz = h->ftz != 0;
     if (op != RSP_OPERATION_NON_TRANSPOSE && op != RSP_OPERATION_TRANSPOSE) return RSP_STATUS_INVALID_VALUE;
-    trsv_begin(h, f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, a);
+    RSP_CHECK_HIP(trsv_begin(h, f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, a));
     if (op == RSP_OPERATION_NON_TRANSPOSE) {
         e = f64 ? rsp_k::trsv_lower_n_f64(a, h->stream)
                 : (ftz ? rsp_k_ftz::trsv_lower_n_f32(a, h->stream) : rsp_k::trsv_lower_n_f32(a, h->stream));
@@ -2138,7 +2145,7 @@ static rsp_status_t rsp_trsv_upper_impl(rsp_handle_t h, const void *alpha, rsp_i
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
     a.plan = level_plan(f->U, f->U.segs, f->U.batch);
     a.sval = f->d_usval;
-    trsv_begin(h, f, RSP_TRSV_U, a);
+    RSP_CHECK_HIP(trsv_begin(h, f, RSP_TRSV_U, a));
     hipError_t e;
     if (value_type == RSP_R_64F)
         e = rsp_k::trsv_upper_f64(a, h->stream);

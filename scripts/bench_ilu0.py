@@ -62,8 +62,8 @@ def run_one(h, A, dt, ftz, reps):
     rv, _, rzp = ob.ilu0(A.rowptr, A.colidx, A.values.astype(npdt), ftz=ftz)
     t_cf = (time.perf_counter() - t0) * 1e3
     # the CPU time is the reference's own sequential solves (L column
-    # ascending, L^T column sweep); the parity check uses the split order the
-    # MI355X plans follow (untimed)
+    # ascending, L^T column sweep); the parity check (untimed) follows the
+    # plan's order, which is the reference's order unless RSP_ILU_SPLIT=1
     t0 = time.perf_counter()
     cz = ob.trsv("lower_n_ref", A.rowptr, A.colidx, rv, np.ones(A.n, npdt), ftz=ftz)
     ob.trsv("lower_t_ref", A.rowptr, A.colidx, rv, cz, ftz=ftz)

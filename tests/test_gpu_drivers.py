@@ -3,6 +3,7 @@ GPU/spmv.cu:202-207,260 and GPU/ilu0.cu:221-226,312-317, results checked
 against the oracle; plus the multi-partition SpMV on one GPU (the N>1
 data path without the collective: every rank's slice computed by the HIP
 kernel on the padded x must reassemble the single-GPU y bitwise)."""
+import json
 import os
 import re
 import subprocess
@@ -82,6 +83,31 @@ def test_spmv_driver_ngpu_rccl():
     r = subprocess.run([os.path.join(BIN, "test_spmv"), "surrogate:Serena@0.01", f"--ngpu={n + 1}"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "GPU(s) visible" in r.stderr
+
+
+def _bench(*args, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    return subprocess.run(["python3", os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def test_bench_launches_n_ranks_itself():
+    """`python bench.py --gpus 2` (no torchrun: the driver's scaling command)
+    starts two ranks itself. On a one-GPU box the rehearsal backend (gloo)
+    lets both ranks share cuda:0; the line must name 2 GPUs, the row-partitioned
+    step's y must pass the oracle check, and with the product backend (nccl =
+    RCCL) and too few GPUs bench.py must exit non-zero without a line."""
+    r = _bench("--gpus", "2", "--dist-backend", "gloo", "--workload", "Serena", "--steps", "3",
+               "--warmup", "1", "--ramp-ms", "20", "--no-cpu", "--fp32-reps", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["parity_check"] == "ok" and d["value"] > 0
+    assert "row-partition x2" == d["config"]["parallelism"] and "gloo" in d["config"]["collective"]
+    if torch.cuda.device_count() < 2:
+        r = _bench("--gpus", "2", "--workload", "Serena", "--steps", "3", "--no-cpu", timeout=120)
+        assert r.returncode != 0 and not r.stdout.strip() and "nccl" in r.stderr
 
 
 def test_ilu0_driver_reference_format():

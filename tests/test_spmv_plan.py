@@ -89,3 +89,22 @@ def test_plan_list_tiles_ragged_band(monkeypatch):
     monkeypatch.setenv("RSP_SPMV_STAGE_LIST", "0")
     st, _, _, est = plan(A, R64)
     assert st == 0 and est == 0
+
+
+@pytest.mark.parametrize("shift,staged64,staged32", [(0, True, True), (300_000_000, False, True),
+                                                    (600_000_000, False, False)])
+def test_plan_no_staging_past_the_x_resource(shift, staged64, staged32):
+    """Staged tiles load x through a buffer resource of 0x7ffffffc bytes with
+    32-bit byte offsets (spmv.hip stream_products_staged): a tile whose
+    columns reach past 0x7ffffffc / sizeof(T) (268 435 455 fp64, 536 870 910
+    fp32) must not be staged; it keeps the plain 16-bit column offsets."""
+    n = 20000
+    rows = [np.arange(max(0, i - 3), min(n, i + 4)) + shift for i in range(n)]
+    rp = np.zeros(n + 1, np.int32)
+    np.cumsum([len(r) for r in rows], out=rp[1:])
+    ci = np.concatenate(rows).astype(np.int32)
+    A = csr.CsrMatrix(0, n, shift + n, len(ci), rp, ci, np.ones(len(ci)))
+    for dt, want in ((R64, staged64), (R32, staged32)):
+        st, tiles, e16, est = plan(A, dt)
+        assert st == 0 and e16 == len(ci)
+        assert (est > 0.9 * len(ci)) if want else est == 0
