@@ -1402,24 +1402,65 @@ __global__ __launch_bounds__(256) void trsv_stream(TrsvArgs a, T alpha) {
     }
 }
 
-template <typename T, int KIND, int G, bool PAIRS = false>
+// The LDS layout of trsv_thin_pf (byte offsets into its one LDS object).
+template <typename T, int KIND, int G, bool PF, bool PF2>
+struct ThinLay {
+    static constexpr int al(int v, int a) { return (v + a - 1) / a * a; }
+    static constexpr int idx = 0;
+    static constexpr int val = al(idx + (rsp::kChunkTerms / G + 1) * (int)sizeof(TermIds<G>), 32);
+    static constexpr int yb = al(val + (rsp::kChunkTerms / G + 1) * (int)sizeof(TermGroup<T, G>), 16);
+    static constexpr int row = al(yb + (rsp::kYWin + 1 + rsp::kChunkTerms) * (int)sizeof(T), 16);
+    static constexpr int rowi = row + rsp::kChunkRows * (int)sizeof(ThinRow<T>);
+    static constexpr int ptr = rowi + 4 * rsp::kChunkRows;
+    static constexpr int ns = ptr + 4 * (rsp::kChunkRows + 1);
+    static constexpr int vw = ns + 4 * rsp::kChunkRows;
+    static constexpr int gl = al(vw + (PF ? 4 * rsp::kChunkRows : 4), 8);
+    static constexpr int dg = al(gl + (PF2 ? 8 * rsp::kChunkRows : 8), 8);
+    static constexpr int done = dg + (int)sizeof(T) * (KIND == 2 ? rsp::kChunkRows : 1);
+    static constexpr int egr = done + 4;
+    static constexpr int bytes = al(egr + rsp::kChunkRows, 16);
+};
+
+// NM: how narrow runs (levels of <= 64 short rows) are computed — 0 on
+// a.narrow_waves waves, levels round-robin (or one wave); 1 the same with two
+// levels per wave turn (narrow_run_mw2); 2 one wave with every term group of
+// the next level prefetched (narrow_run_pf, L / L^T only); 3 the same with the
+// rows' group offsets and the level words precomputed per chunk (PF2). Each
+// is its own instantiation (their registers).
+template <typename T, int KIND, int G, int NM = 0>
 __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, int c0, int c1, int base) {
+    constexpr bool PAIRS = NM == 1, PF = (NM == 2 || NM == 3) && KIND != 2, PF2 = NM == 3 && KIND != 2;
     constexpr int NTH = rsp::kThinThreads;
     constexpr int TPT = rsp::kChunkTerms / NTH;  // terms of a chunk per thread: tid + j NTH
     static_assert(TPT * NTH == rsp::kChunkTerms && G <= rsp::kGroup, "chunk terms per thread");
     static_assert(rsp::kChunkRows <= NTH, "one row of a chunk per thread");
     constexpr int kZero = rsp::kYWin, kStaged = rsp::kYWin + 1;
-    __shared__ T ybuf[rsp::kYWin + 1 + rsp::kChunkTerms];
     // + one pad group (values 0, y from the zero slot) after the chunk's groups
     constexpr int kPadGroup = rsp::kChunkTerms / G;
-    __shared__ TermGroup<T, G> lval[rsp::kChunkTerms / G + 1];
-    __shared__ TermIds<G> lidx[rsp::kChunkTerms / G + 1];
-    __shared__ ThinRow<T> lrow[rsp::kChunkRows];
-    __shared__ int lrowi[rsp::kChunkRows];
-    __shared__ unsigned char legr[rsp::kChunkRows];  // per row: its early term groups (split order)
-    __shared__ T ldg[KIND == 2 ? rsp::kChunkRows : 1];  // u_ii: U solve only
-    __shared__ int lptr[rsp::kChunkRows + 1], lns[rsp::kChunkRows];
-    __shared__ int lds_done;  // multi-wave narrow runs: absolute levels completed
+    // The workgroup's LDS is ONE object with a fixed layout, so the arrays the
+    // narrow loops index per term sit where an LDS instruction's 16-bit offset
+    // field can add their base: the term groups' y indices (lidx) at 0, their
+    // values (lval) next, the y buffer (ybuf: window | zero slot | staged y)
+    // after them; then the row records and the per-level arrays.
+    using Lay = ThinLay<T, KIND, G, PF, PF2>;
+    static_assert(Lay::yb < 65536 && Lay::val < 65536 && Lay::bytes <= 163840, "LDS layout");
+    __shared__ __attribute__((aligned(32))) char lds_arena[Lay::bytes];
+    T *const ybuf = (T *)(lds_arena + Lay::yb);
+    TermGroup<T, G> *const lval = (TermGroup<T, G> *)(lds_arena + Lay::val);
+    TermIds<G> *const lidx = (TermIds<G> *)(lds_arena + Lay::idx);
+    ThinRow<T> *const lrow = (ThinRow<T> *)(lds_arena + Lay::row);
+    int *const lrowi = (int *)(lds_arena + Lay::rowi);
+    unsigned char *const legr = (unsigned char *)(lds_arena + Lay::egr);  // per row: its early term groups (split order)
+    T *const ldg = (T *)(lds_arena + Lay::dg);  // u_ii: U solve only
+    int *const lptr = (int *)(lds_arena + Lay::ptr);
+    int *const lns = (int *)(lds_arena + Lay::ns);
+    int &lds_done = *(int *)(lds_arena + Lay::done);  // multi-wave narrow runs: absolute levels completed
+    // PF narrow runs: per narrow level of the chunk, its first row (chunk-relative)
+    // | rows - 1 << 10 | largest group count << 16
+    int *const lvw = (int *)(lds_arena + Lay::vw);
+    // PF2: per row of a narrow level, the LDS byte addresses of its first 4 / 2
+    // term groups' y indices (the pad group past the row's own), 16 bits each
+    uint2 *const lgl = (uint2 *)(lds_arena + Lay::gl);
     const int tid = threadIdx.x;
     if (tid == 0) lds_done = INT_MIN;  // ordered before any use by the first chunk's barriers
     const T *sval = (const T *)a.sval, *sx = (const T *)a.sx, *sdg = (const T *)a.sdg;
@@ -1870,8 +1911,273 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             lds_publish(&lds_done, L + (has2 ? 2 : 1), lane == 0);  // after the y stores
         }
     };
+    // Narrow run on ONE wave with every term group of the next level
+    // prefetched (PF; L / L^T; round 5). In the other narrow loops a level
+    // whose rows have more than two term groups reads the third and later
+    // groups' y indices inside the level (an index load, then its y load: two
+    // dependent LDS round trips per group on the critical path), and the
+    // multi-wave forms add a counter release / poll / acquire per level or
+    // pair. Here a level's critical path is ONE LDS round trip: right after
+    // level q-1's y stores the wave issues the y loads of ALL of level q's
+    // groups (up to NGP; the y indices were loaded during level q-1), then
+    // the fma chain, then the y stores. Everything else — level q+1's y
+    // indices (before the chain) and term values (after the stores), the row
+    // records of level q+2 — is issued in the shadow of that round trip. One
+    // wave's LDS accesses are performed in order (the fences below are
+    // wavefront scope), so no counter and no barrier orders the levels.
+    // Groups past a row's own read the pad group (exact no-op fmas); lanes past
+    // a level's rows repeat its last row (same value to the same slot); level
+    // words past the run repeat its last level (loaded, never used). Rows of
+    // more than NGP groups take their remaining groups inside the level.
+    // Same terms, same order, same fma chain as every other solve path: same bits.
+    auto narrow_run_pf = [&](int q0, int q1) {  // wave 0
+        constexpr int NGP = 8 / G;  // groups prefetched per level (8 terms)
+        const int lane = tid;
+        struct Lv {
+            ThinRow<T> R;
+            int ng;  // the level's largest group count (wave-uniform)
+        };
+        auto word = [&](int q) { return lvw[min(q, q1 - 1)]; };
+        auto rec = [&](int wv) {  // this lane's row of the level with word wv
+            const int w = __builtin_amdgcn_readfirstlane(wv);
+            Lv v;
+            v.R = lrow[(w & 1023) + min(lane, (w >> 10) & 63)];
+            v.ng = w >> 16;
+            return v;
+        };
+        auto grp = [&](const ThinRow<T> &R, int g) { return g < (R.g >> 16) ? (R.g & 0xffff) + g : kPadGroup; };
+        TermIds<G> ic[NGP];
+        TermGroup<T, G> vc[NGP];
+        int gc[NGP];
+        auto ids = [&](const ThinRow<T> &R) {
+#pragma unroll
+            for (int g = 0; g < NGP; ++g) {
+                gc[g] = grp(R, g);
+                ic[g] = lidx[gc[g]];
+            }
+        };
+        auto values = [&] {
+#pragma unroll
+            for (int g = 0; g < NGP; ++g) vc[g] = lval[gc[g]];
+        };
+        // Level q: c its records, n level q+1's, m <- level q+2's (from its word
+        // wm, loaded one level earlier), wn <- level q+3's word. NG = the
+        // level's group count, a compile-time constant per branch (NGP + 1:
+        // more than NGP), so each branch is straight-line code.
+        auto body = [&](const Lv &c, const Lv &n, Lv &m, const int &wm, int &wn, int q) {
+            auto run = [&](auto ngc) {
+                constexpr int NG = decltype(ngc)::value;
+                constexpr int NL = NG < NGP ? NG : NGP;
+                T yv[NL > 0 ? NL : 1][G];
+#pragma unroll
+                for (int g = 0; g < NL; ++g)
+#pragma unroll
+                    for (int j = 0; j < G; ++j) yv[g][j] = yb(ic[g].v[j]);
+                __builtin_amdgcn_sched_barrier(0);  // level q's y loads first: the chain waits for them only
+                ids(n.R);  // level q+1's y indices (ic is free once these y loads are issued)
+                m = rec(wm);
+                wn = word(q + 3);
+                __builtin_amdgcn_sched_barrier(0);
+                T s = c.R.x;
+#pragma unroll
+                for (int g = 0; g < NL; ++g)
+#pragma unroll
+                    for (int j = 0; j < G; ++j) s = fma_t(-vc[g].v[j], yv[g][j], s);
+                if constexpr (NG > NGP) {
+                    for (int g = NGP; g < c.ng; ++g) {  // rows of more groups (uniform bound)
+                        const int gi = grp(c.R, g);
+                        s = group_fma(s, lval[gi], lidx[gi]);
+                    }
+                }
+                put(c.R.out, s);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                values();  // level q+1's term values (needed after its y loads)
+            };
+            static_assert(NGP == 4 || NGP == 2, "prefetch depth");
+            switch (c.ng) {
+                case 0: run(std::integral_constant<int, 0>()); break;
+                case 1: run(std::integral_constant<int, 1>()); break;
+                case 2: run(std::integral_constant<int, 2>()); break;
+                case 3:
+                    if constexpr (NGP >= 3) {
+                        run(std::integral_constant<int, NGP >= 3 ? 3 : NGP + 1>());
+                        break;
+                    }
+                    [[fallthrough]];
+                case 4:
+                    if constexpr (NGP >= 4) {
+                        run(std::integral_constant<int, NGP >= 4 ? 4 : NGP + 1>());
+                        break;
+                    }
+                    [[fallthrough]];
+                default: run(std::integral_constant<int, NGP + 1>()); break;
+            }
+        };
+        Lv L0 = rec(word(q0)), L1 = rec(word(q0 + 1)), L2;
+        int W0 = word(q0 + 2), W1, W2;
+        ids(L0.R);
+        values();
+        // drain the prologue (see narrow_run: a pending load at the loop head
+        // makes the compiler wait at the head of every level)
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        for (int q = q0;; q += 3) {  // unrolled by the records' rotation (no register copies)
+            body(L0, L1, L2, W0, W1, q);
+            if (q + 1 >= q1) break;
+            body(L1, L2, L0, W1, W2, q + 1);
+            if (q + 2 >= q1) break;
+            body(L2, L0, L1, W2, W0, q + 2);
+            if (q + 3 >= q1) break;
+        }
+    };
+    // PF2 (round 5): narrow_run_pf with the per-level and per-row work of the
+    // loop moved to the chunk's marking pass (below): each row of a narrow
+    // level carries the LDS addresses of its first NGP term groups' y indices
+    // (lgl; the pad group past the row's own groups), so a group's y indices
+    // and values are one address extraction and one load each; and the level
+    // words of 64 consecutive levels sit in one VGPR (lane l = level qb + l),
+    // read with v_readlane instead of a load per level. Same terms, same
+    // order, same fma chain: same bits.
+    auto narrow_run_pf2 = [&](int x0, int q0, int q1) {  // wave 0
+        constexpr int NGP = 8 / G;
+        constexpr int VS = (int)(sizeof(TermGroup<T, G>) / sizeof(TermIds<G>));  // lval / lidx entry size
+        const int lane = tid;
+        struct Lv {
+            T x;
+            int out;
+            uint2 gl;  // group y-index addresses, 16 bits each
+            int ng;    // the level's largest group count (wave-uniform)
+        };
+        // the words of levels [qb, qb + 64) in wv, [qb + 64, qb + 128) in wv2;
+        // qb advances by 63 levels (21 turns of the 3-level loop below)
+        int qb = q0;
+        auto words = [&] {
+            return make_int2(lvw[min(qb + lane, q1 - 1)], lvw[min(qb + 64 + lane, q1 - 1)]);
+        };
+        int2 wv = words();
+        auto rec = [&](int q) {
+            const int i = q - qb;  // 0 .. 65
+            const int w0 = __builtin_amdgcn_readlane(wv.x, i), w1 = __builtin_amdgcn_readlane(wv.y, i - 64);
+            const int w = i < 64 ? w0 : w1;
+            const int r = (w & 1023) + min(lane, (w >> 10) & 63);
+            const ThinRow<T> R = lrow[r];
+            Lv v;
+            v.x = R.x;
+            v.out = R.out;
+            v.gl = lgl[r];
+            v.ng = w >> 16;
+            return v;
+        };
+        auto gaddr = [&](const uint2 &gl, int g) {
+            const unsigned u = (g >> 1) ? gl.y : gl.x;
+            return (g & 1) ? (int)(u >> 16) : (int)(u & 0xffff);
+        };
+        TermIds<G> ic[NGP];
+        TermGroup<T, G> vc[NGP];
+        int ga[NGP];
+        auto ids = [&](const Lv &n) {
+#pragma unroll
+            for (int g = 0; g < NGP; ++g) {
+                ga[g] = gaddr(n.gl, g);
+                ic[g] = *(const TermIds<G> *)(lds_arena + ga[g]);
+            }
+        };
+        auto values = [&] {
+#pragma unroll
+            for (int g = 0; g < NGP; ++g) vc[g] = *(const TermGroup<T, G> *)(lds_arena + Lay::val + VS * ga[g]);
+        };
+        auto body = [&](const Lv &c, const Lv &n, Lv &m, int q) {
+            auto run = [&](auto ngc) {
+                constexpr int NG = decltype(ngc)::value;
+                constexpr int NL = NG < NGP ? NG : NGP;
+                T yv[NL > 0 ? NL : 1][G];
+#pragma unroll
+                for (int g = 0; g < NL; ++g)
+#pragma unroll
+                    for (int j = 0; j < G; ++j) yv[g][j] = yb(ic[g].v[j]);
+                __builtin_amdgcn_sched_barrier(0);  // level q's y loads first: the chain waits for them only
+                ids(n);
+                m = rec(q + 2);
+                __builtin_amdgcn_sched_barrier(0);
+                T s = c.x;
+#pragma unroll
+                for (int g = 0; g < NL; ++g)
+#pragma unroll
+                    for (int j = 0; j < G; ++j) s = fma_t(-vc[g].v[j], yv[g][j], s);
+                if constexpr (NG > NGP) {  // rows of more groups (uniform bound): their groups past NGP
+                    // the row from its y window slot (the window outlasts a chunk's rows)
+                    const int gr = lrow[(c.out / (int)sizeof(T) - (x0 - base)) & (rsp::kYWin - 1)].g;
+                    for (int g = NGP; g < c.ng; ++g) {
+                        const int gi = g < (gr >> 16) ? (gr & 0xffff) + g : kPadGroup;
+                        s = group_fma(s, lval[gi], lidx[gi]);
+                    }
+                }
+                put(c.out, s);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                values();  // level q+1's term values (needed after its y loads)
+            };
+            switch (c.ng) {
+                case 0: run(std::integral_constant<int, 0>()); break;
+                case 1: run(std::integral_constant<int, 1>()); break;
+                case 2: run(std::integral_constant<int, 2>()); break;
+                case 3:
+                    if constexpr (NGP >= 3) {
+                        run(std::integral_constant<int, NGP >= 3 ? 3 : NGP + 1>());
+                        break;
+                    }
+                    [[fallthrough]];
+                case 4:
+                    if constexpr (NGP >= 4) {
+                        run(std::integral_constant<int, NGP >= 4 ? 4 : NGP + 1>());
+                        break;
+                    }
+                    [[fallthrough]];
+                default: run(std::integral_constant<int, NGP + 1>()); break;
+            }
+        };
+        Lv L0 = rec(q0), L1 = rec(q0 + 1), L2;
+        ids(L0);
+        values();
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): drain the prologue (see narrow_run)
+        for (int q = q0;; q += 3) {
+            if (q - qb >= 63) {  // wave-uniform, every 21 turns: the next words
+                qb += 63;
+                wv = words();
+            }
+            body(L0, L1, L2, q);
+            if (q + 1 >= q1) break;
+            body(L1, L2, L0, q + 1);
+            if (q + 2 >= q1) break;
+            body(L2, L0, L1, q + 2);
+            if (q + 3 >= q1) break;
+        }
+    };
     auto levels = [&](const rsp::LevelChunk &ch) {
         const int x0 = ch.x0, nl = ch.l1 - ch.l0;
+        if constexpr (PF) {  // the narrow levels' words (narrow_run_pf): one thread per level
+            for (int q = tid; q < nl; q += NTH) {
+                const int p0 = lptr[q], cnt = lptr[q + 1] - p0;
+                if (cnt <= 64 && lns[q] == cnt) {
+                    int ngm = 0;
+                    for (int r = 0; r < cnt; ++r) ngm = max(ngm, lrow[p0 - x0 + r].g >> 16);
+                    lvw[q] = (p0 - x0) | (cnt - 1) << 10 | ngm << 16;
+                }
+            }
+            if constexpr (PF2) {  // every row: its first 8 / G groups' y-index addresses (pad past its own)
+                if (tid < ch.x1 - x0) {
+                    const int gr = lrow[tid].g, g0 = gr & 0xffff, ng = gr >> 16;
+                    unsigned o[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        o[g] = (unsigned)((g < ng ? g0 + g : kPadGroup) * (int)sizeof(TermIds<G>) + Lay::idx);
+                    lgl[tid] = make_uint2(o[0] | o[1] << 16, o[2] | o[3] << 16);
+                }
+            }
+            lds_barrier();
+        }
 #if RSP_THIN_LONG_READLANE
         auto vat = [&](int k) { return lval[k / G].v[k % G]; };
         auto yat = [&](int k) { return yb(lidx[k / G].v[k % G]); };
@@ -1880,7 +2186,11 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             if (narrow(q)) {
                 const int qe = run_end(q, nl);
                 const int K = min(a.narrow_waves, (int)(blockDim.x >> 6));  // waves of this launch
-                if (KIND != 2 && G == 2 && a.narrow_split) {  // (G = 4: the registers are not there)
+                if constexpr (PF2) {
+                    if (tid < 64) narrow_run_pf2(x0, q, qe);
+                } else if constexpr (PF) {
+                    if (tid < 64) narrow_run_pf(q, qe);
+                } else if (KIND != 2 && G == 2 && a.narrow_split) {  // (G = 4: the registers are not there)
                     if constexpr (KIND != 2 && G == 2)
                         if (tid < 64) narrow_run_split(ch, q, qe);
                 } else if (PAIRS && K > 1) {  // (its own instantiation: the registers)
@@ -2073,8 +2383,16 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             // 3.22; on wider DAGs' narrow runs they cost: parabolic_fem 3.55
             // -> 3.95, Dubcova3 2.59 -> 2.84, thermomech_TK 0.95 -> 1.00)
             const bool pr = KIND != 2 && (a.narrow_pairs > 0 || (a.narrow_pairs < 0 && a.n <= 32LL * P.nlev));
-            auto kern = P.group == 2 ? (pr ? trsv_thin_pf<T, KIND, 2, KIND != 2> : trsv_thin_pf<T, KIND, 2>)
-                                     : (pr ? trsv_thin_pf<T, KIND, 4, KIND != 2> : trsv_thin_pf<T, KIND, 4>);
+            // the one-wave prefetching narrow runs (L / L^T): RSP_ILU_NARROW_PF 1 / 0
+            // (2: the precomputed-address form)
+            const bool pf = KIND != 2 && a.narrow_pf > 0, pf2 = pf && a.narrow_pf == 2;
+            constexpr int NP = KIND != 2 ? 1 : 0, NF = KIND != 2 ? 2 : 0, NF2 = KIND != 2 ? 3 : 0;
+            auto kern = P.group == 2 ? (pf2 ? trsv_thin_pf<T, KIND, 2, NF2>
+                                        : pf ? trsv_thin_pf<T, KIND, 2, NF>
+                                             : pr ? trsv_thin_pf<T, KIND, 2, NP> : trsv_thin_pf<T, KIND, 2>)
+                                     : (pf2 ? trsv_thin_pf<T, KIND, 4, NF2>
+                                        : pf ? trsv_thin_pf<T, KIND, 4, NF>
+                                             : pr ? trsv_thin_pf<T, KIND, 4, NP> : trsv_thin_pf<T, KIND, 4>);
             hipLaunchKernelGGL(kern, dim3(1), dim3(kThinThreads), 0, s, a, sg.c0, sg.c1, P.ptr_host[sg.lb]);
             continue;
         }
