@@ -1403,7 +1403,7 @@ __global__ __launch_bounds__(256) void trsv_stream(TrsvArgs a, T alpha) {
 }
 
 // The LDS layout of trsv_thin_pf (byte offsets into its one LDS object).
-template <typename T, int KIND, int G, bool PF, bool PF2>
+template <typename T, int KIND, int G>
 struct ThinLay {
     static constexpr int al(int v, int a) { return (v + a - 1) / a * a; }
     static constexpr int idx = 0;
@@ -1413,27 +1413,34 @@ struct ThinLay {
     static constexpr int rowi = row + rsp::kChunkRows * (int)sizeof(ThinRow<T>);
     static constexpr int ptr = rowi + 4 * rsp::kChunkRows;
     static constexpr int ns = ptr + 4 * (rsp::kChunkRows + 1);
-    static constexpr int vw = ns + 4 * rsp::kChunkRows;
-    static constexpr int gl = al(vw + (PF ? 4 * rsp::kChunkRows : 4), 8);
-    static constexpr int dg = al(gl + (PF2 ? 8 * rsp::kChunkRows : 8), 8);
+    static constexpr int dg = al(ns + 4 * rsp::kChunkRows, 8);
     static constexpr int done = dg + (int)sizeof(T) * (KIND == 2 ? rsp::kChunkRows : 1);
     static constexpr int egr = done + 4;
     static constexpr int bytes = al(egr + rsp::kChunkRows, 16);
 };
 
-// NM: how narrow runs (levels of <= 64 short rows) are computed — 0 on
-// a.narrow_waves waves, levels round-robin (or one wave); 1 the same with two
-// levels per wave turn (narrow_run_mw2); 2 one wave with every term group of
-// the next level prefetched (narrow_run_pf, L / L^T only); 3 the same with the
-// rows' group offsets and the level words precomputed per chunk (PF2). Each
-// is its own instantiation (their registers).
-template <typename T, int KIND, int G, int NM = 0>
+// PAIRS: narrow runs (levels of <= 64 short rows) on a.narrow_waves waves
+// with two consecutive levels per wave turn (narrow_run_mw2), else one level
+// per turn (narrow_run_mw; one wave: narrow_run). Its own instantiation (the
+// registers).
+// LW (round 5): the first LW waves never load the next chunk; the loader
+// threads are the other kThinThreads - 64 LW (a thread stages rows lt + r NL
+// and terms lt + j NL). The narrow waves then hold none of the chunk
+// prefetch's registers, which gives narrow_run_mw2 the room to prepare every
+// term group of up to three per level before its wait (G = 2): config-3 deep
+// set, same box, interleaved x2 (profiles/r05_ilu_loaders_ab.txt): dc1 solve
+// 4.77 -> 4.46 ms, G2_circuit 2.58 -> 2.33, matrix-new_3 5.60 -> 5.24; the
+// split alone (without the extra groups) measured equal, and on DAGs that do
+// not take the pair loop it cost (thermomech_TK 1.01 -> 1.05): LW = 4 with
+// PAIRS only.
+template <typename T, int KIND, int G, bool PAIRS = false, int LW = 0>
 __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, int c0, int c1, int base) {
-    constexpr bool PAIRS = NM == 1, PF = (NM == 2 || NM == 3) && KIND != 2, PF2 = NM == 3 && KIND != 2;
     constexpr int NTH = rsp::kThinThreads;
-    constexpr int TPT = rsp::kChunkTerms / NTH;  // terms of a chunk per thread: tid + j NTH
-    static_assert(TPT * NTH == rsp::kChunkTerms && G <= rsp::kGroup, "chunk terms per thread");
-    static_assert(rsp::kChunkRows <= NTH, "one row of a chunk per thread");
+    constexpr int NL = NTH - 64 * LW;                     // loader threads: lt = tid - 64 LW >= 0
+    constexpr int TPT = (rsp::kChunkTerms + NL - 1) / NL;  // terms of a chunk per loader: lt + j NL
+    constexpr int RPT = (rsp::kChunkRows + NL - 1) / NL;   // rows (and level pointers) per loader: lt + r NL
+    static_assert(NL > 0 && G <= rsp::kGroup, "chunk loaders");
+    static_assert(NTH >= rsp::kThinSolveRows, "one pass over a thin level's short rows");
     constexpr int kZero = rsp::kYWin, kStaged = rsp::kYWin + 1;
     // + one pad group (values 0, y from the zero slot) after the chunk's groups
     constexpr int kPadGroup = rsp::kChunkTerms / G;
@@ -1442,7 +1449,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     // field can add their base: the term groups' y indices (lidx) at 0, their
     // values (lval) next, the y buffer (ybuf: window | zero slot | staged y)
     // after them; then the row records and the per-level arrays.
-    using Lay = ThinLay<T, KIND, G, PF, PF2>;
+    using Lay = ThinLay<T, KIND, G>;
     static_assert(Lay::yb < 65536 && Lay::val < 65536 && Lay::bytes <= 163840, "LDS layout");
     __shared__ __attribute__((aligned(32))) char lds_arena[Lay::bytes];
     T *const ybuf = (T *)(lds_arena + Lay::yb);
@@ -1455,13 +1462,8 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     int *const lptr = (int *)(lds_arena + Lay::ptr);
     int *const lns = (int *)(lds_arena + Lay::ns);
     int &lds_done = *(int *)(lds_arena + Lay::done);  // multi-wave narrow runs: absolute levels completed
-    // PF narrow runs: per narrow level of the chunk, its first row (chunk-relative)
-    // | rows - 1 << 10 | largest group count << 16
-    int *const lvw = (int *)(lds_arena + Lay::vw);
-    // PF2: per row of a narrow level, the LDS byte addresses of its first 4 / 2
-    // term groups' y indices (the pad group past the row's own), 16 bits each
-    uint2 *const lgl = (uint2 *)(lds_arena + Lay::gl);
     const int tid = threadIdx.x;
+    const int lt = tid - 64 * LW;  // loader index (< 0: a narrow-run wave that never loads)
     if (tid == 0) lds_done = INT_MIN;  // ordered before any use by the first chunk's barriers
     const T *sval = (const T *)a.sval, *sx = (const T *)a.sx, *sdg = (const T *)a.sdg;
     T *y = (T *)a.y;
@@ -1471,13 +1473,13 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         lval[kPadGroup].v[tid] = T(0);
         lidx[kPadGroup].v[tid] = kZero * (int)sizeof(T);
     }
-    struct Pre {  // this thread's share of a chunk: row tid, terms tid + j NTH (all streams)
-        rsp::ThinRowPlan r;
-        T xv, dg, v[TPT];
+    struct Pre {  // this loader's share of a chunk: rows lt + r NL, terms lt + j NL (all streams)
+        rsp::ThinRowPlan r[RPT];
+        T xv[RPT], dg[RPT], v[TPT];
         int id[TPT];
-        int lp, ln, lpe;
+        int lp[RPT], ln[RPT], lpe;
     };
-    struct Stg {  // staged terms tid + j NTH of a chunk
+    struct Stg {  // staged terms lt + j NL of a chunk
         int slot[TPT], j[TPT];
     };
     struct StgY {  // ... and their y
@@ -1489,22 +1491,30 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     // bandwidth, and a chunk of short rows fills a fraction of its term slots.
     auto load_pre = [&](const rsp::LevelChunk &ch) {
         Pre p;
-        const int x = ch.x0 + tid, nl = ch.l1 - ch.l0;
-        if (x < ch.x1) {
-            p.r = a.plan.trow[x];
-            p.xv = sx[x];
-            p.dg = KIND == 2 ? sdg[x] : T(0);
+        const int nl = ch.l1 - ch.l0;
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) {
+            const int x = ch.x0 + lt + rr * NL;
+            if (lt >= 0 && x < ch.x1) {
+                p.r[rr] = a.plan.trow[x];
+                p.xv[rr] = sx[x];
+                p.dg[rr] = KIND == 2 ? sdg[x] : T(0);
+            }
         }
 #pragma unroll
         for (int j = 0; j < TPT; ++j) {
-            const int k = ch.k0 + tid + j * NTH;
-            if (k < ch.k1) {
+            const int k = ch.k0 + lt + j * NL;
+            if (lt >= 0 && k < ch.k1) {
                 p.v[j] = sval[k];
                 p.id[j] = a.plan.sid[k];
             }
         }
-        p.lp = ptr[ch.l0 + min(tid, nl)];
-        p.ln = a.plan.nshort[ch.l0 + min(tid, max(nl - 1, 0))];
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr)
+            if (lt >= 0) {
+                p.lp[rr] = ptr[ch.l0 + min(lt + rr * NL, nl)];
+                p.ln[rr] = a.plan.nshort[ch.l0 + min(lt + rr * NL, max(nl - 1, 0))];
+            }
         p.lpe = ptr[ch.l1];
         return p;
     };
@@ -1512,20 +1522,22 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         Stg q;
         const int el = max(ch.st1 - 1, 0);
 #pragma unroll
-        for (int j = 0; j < TPT; ++j) {
-            const rsp::StagedTerm t = a.plan.stg[max(min(ch.st0 + tid + j * NTH, el), 0)];
-            q.slot[j] = t.slot;
-            q.j[j] = t.j;
-        }
+        for (int j = 0; j < TPT; ++j)
+            if (lt >= 0) {
+                const rsp::StagedTerm t = a.plan.stg[max(min(ch.st0 + lt + j * NL, el), 0)];
+                q.slot[j] = t.slot;
+                q.j[j] = t.j;
+            }
         return q;
     };
     auto load_stgy = [&](const Stg &q) {
         StgY w;
 #pragma unroll
-        for (int j = 0; j < TPT; ++j) {
-            w.slot[j] = q.slot[j];
-            w.y[j] = y[q.j[j]];
-        }
+        for (int j = 0; j < TPT; ++j)
+            if (lt >= 0) {
+                w.slot[j] = q.slot[j];
+                w.y[j] = y[q.j[j]];
+            }
         return w;
     };
     // Chunk switch. The levels write y to the LDS window only; the previous
@@ -1547,32 +1559,47 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         // this chunk's prefetch loads: workgroup-scope release / acquire
         __syncthreads();
         mark(c, 1);
-        const bool flush = tid < px1 - px0;
-        const int fi = lrowi[tid];  // read before this thread restages its slot
-        const T fv = ybuf[(px0 + tid - base) & (rsp::kYWin - 1)];
-        if (tid < ch.x1 - ch.x0) {
-            ThinRow<T> r;
-            r.x = p.xv;
-            r.g = p.r.g;
-            r.out = (p.r.out & 0xffff) * (int)sizeof(T);
-            lrow[tid] = r;
-            legr[tid] = (unsigned char)(p.r.out >> 16);  // early groups (split order)
-            lrowi[tid] = p.r.i;
-            if constexpr (KIND == 2) ldg[tid] = p.dg;
+        int fi[RPT];
+        T fv[RPT];
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) {  // read before this thread restages its slots
+            const int t = min(max(lt, 0) + rr * NL, rsp::kChunkRows - 1);
+            fi[rr] = lrowi[t];
+            fv[rr] = ybuf[(px0 + t - base) & (rsp::kYWin - 1)];
+        }
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) {
+            const int t = lt + rr * NL;
+            if (lt >= 0 && t < ch.x1 - ch.x0) {
+                ThinRow<T> r;
+                r.x = p.xv[rr];
+                r.g = p.r[rr].g;
+                r.out = (p.r[rr].out & 0xffff) * (int)sizeof(T);
+                lrow[t] = r;
+                legr[t] = (unsigned char)(p.r[rr].out >> 16);  // early groups (split order)
+                lrowi[t] = p.r[rr].i;
+                if constexpr (KIND == 2) ldg[t] = p.dg[rr];
+            }
         }
 #pragma unroll
         for (int j = 0; j < TPT; ++j)
-            if (tid + j * NTH < nk) {
-                ((T *)lval)[tid + j * NTH] = p.v[j];
-                ((int *)lidx)[tid + j * NTH] = p.id[j] * (int)sizeof(T);
+            if (lt >= 0 && lt + j * NL < nk) {
+                ((T *)lval)[lt + j * NL] = p.v[j];
+                ((int *)lidx)[lt + j * NL] = p.id[j] * (int)sizeof(T);
             }
 #pragma unroll
         for (int j = 0; j < TPT; ++j)
-            if (tid + j * NTH < ns) ybuf[kStaged + w.slot[j]] = w.y[j];
-        if (tid <= nl) lptr[tid] = p.lp;
-        if (tid < nl) lns[tid] = p.ln;
-        if (tid == 0 && nl == NTH) lptr[NTH] = p.lpe;
-        if (flush) y[fi] = fv;  // after the last use of the prefetched registers
+            if (lt >= 0 && lt + j * NL < ns) ybuf[kStaged + w.slot[j]] = w.y[j];
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr) {
+            const int t = lt + rr * NL;
+            if (lt >= 0 && t <= nl) lptr[t] = p.lp[rr];
+            if (lt >= 0 && t < nl) lns[t] = p.ln[rr];
+        }
+        if (lt == 0 && nl == rsp::kChunkRows) lptr[rsp::kChunkRows] = p.lpe;
+#pragma unroll
+        for (int rr = 0; rr < RPT; ++rr)  // after the last use of the prefetched registers
+            if (lt >= 0 && lt + rr * NL < px1 - px0) y[fi[rr]] = fv[rr];
         lds_barrier();
         mark(c, 2);
     };
@@ -1887,13 +1914,46 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 i2 = lidx[gi];
                 v2 = lval[gi];
             }
+            // LW > 0 (the narrow waves hold no chunk prefetch, so the registers
+            // are there): the third group of the first level and the second and
+            // third of the second are prepared before the wait as well, so those
+            // groups' y loads join the level's first round trip
+            const int h0 = R2.g & 0xffff, nh = R2.g >> 16;
+            constexpr bool MORE = LW > 0 && G == 2;
+            const bool three = MORE && __ballot(ng >= 3) != 0, two2 = MORE && has2 && __ballot(nh >= 2) != 0;
+            const bool three2 = MORE && has2 && __ballot(nh >= 3) != 0;
+            TermIds<G> i3, j2, j3;
+            if (three) i3 = lidx[ng >= 3 ? g0 + 2 : kPadGroup];
+            if (two2) j2 = lidx[nh >= 2 ? h0 + 1 : kPadGroup];
+            if (three2) j3 = lidx[nh >= 3 ? h0 + 2 : kPadGroup];
             const int L = ch.l0 + q;
             if (L > L0) lds_wait_geq(&lds_done, L, L - 1);
-            T s = group_fma(R.x, v1, i1);
-            if (two) {
-                s = group_fma(s, v2, i2);
-                if (__ballot(ng >= 3))
-                    for (int g = 2; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+            T s;
+            if (three) {  // groups 0-2 in one round trip
+                T ya[3][G];
+#pragma unroll
+                for (int j = 0; j < G; ++j) {
+                    ya[0][j] = yb(i1.v[j]);
+                    ya[1][j] = yb(i2.v[j]);
+                    ya[2][j] = yb(i3.v[j]);
+                }
+                const TermGroup<T, G> v3 = lval[ng >= 3 ? g0 + 2 : kPadGroup];
+                s = R.x;
+#pragma unroll
+                for (int j = 0; j < G; ++j) s = fma_t(-v1.v[j], ya[0][j], s);
+#pragma unroll
+                for (int j = 0; j < G; ++j) s = fma_t(-v2.v[j], ya[1][j], s);
+#pragma unroll
+                for (int j = 0; j < G; ++j) s = fma_t(-v3.v[j], ya[2][j], s);
+                if (__ballot(ng >= 4))
+                    for (int g = 3; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+            } else {
+                s = group_fma(R.x, v1, i1);
+                if (two) {
+                    s = group_fma(s, v2, i2);
+                    if (!MORE && __ballot(ng >= 3))
+                        for (int g = 2; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
+                }
             }
             if constexpr (KIND == 2) s = s / ldg[cr];
             put(R.out, s);
@@ -1901,283 +1961,48 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-                const int h0 = R2.g & 0xffff, nh = R2.g >> 16;
-                T t = group_fma(R2.x, lval[h0], j1);
-                if (__ballot(nh >= 2))
-                    for (int g = 1; g < nh; ++g) t = group_fma(t, lval[h0 + g], lidx[h0 + g]);
+                T t;
+                if (two2) {  // groups 0-1 (or 0-2) in one round trip
+                    T yb0[G], yb1[G], yb2[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        yb0[j] = yb(j1.v[j]);
+                        yb1[j] = yb(j2.v[j]);
+                        if (three2) yb2[j] = yb(j3.v[j]);
+                    }
+                    const TermGroup<T, G> w0 = lval[h0], w1 = lval[nh >= 2 ? h0 + 1 : kPadGroup];
+                    TermGroup<T, G> w2;
+                    if (three2) w2 = lval[nh >= 3 ? h0 + 2 : kPadGroup];
+                    t = R2.x;
+#pragma unroll
+                    for (int j = 0; j < G; ++j) t = fma_t(-w0.v[j], yb0[j], t);
+#pragma unroll
+                    for (int j = 0; j < G; ++j) t = fma_t(-w1.v[j], yb1[j], t);
+                    if (three2) {
+#pragma unroll
+                        for (int j = 0; j < G; ++j) t = fma_t(-w2.v[j], yb2[j], t);
+                    }
+                    const int gn = three2 ? 3 : 2;
+                    if (__ballot(nh > gn))
+                        for (int g = gn; g < nh; ++g) t = group_fma(t, lval[h0 + g], lidx[h0 + g]);
+                } else {
+                    t = group_fma(R2.x, lval[h0], j1);
+                    if (__ballot(nh >= 2))
+                        for (int g = 1; g < nh; ++g) t = group_fma(t, lval[h0 + g], lidx[h0 + g]);
+                }
                 if constexpr (KIND == 2) t = t / ldg[cr2];
                 put(R2.out, t);
             }
             lds_publish(&lds_done, L + (has2 ? 2 : 1), lane == 0);  // after the y stores
+            if (a.trace && lane == 0 && L + 1 < a.trace_cap / 2)  // diagnostics: pair end stamps
+                a.trace[a.trace_cap / 2 + L + 1] = a.trace_clk ? clock64() : wall_clock64();
         }
     };
-    // Narrow run on ONE wave with every term group of the next level
-    // prefetched (PF; L / L^T; round 5). In the other narrow loops a level
-    // whose rows have more than two term groups reads the third and later
-    // groups' y indices inside the level (an index load, then its y load: two
-    // dependent LDS round trips per group on the critical path), and the
-    // multi-wave forms add a counter release / poll / acquire per level or
-    // pair. Here a level's critical path is ONE LDS round trip: right after
-    // level q-1's y stores the wave issues the y loads of ALL of level q's
-    // groups (up to NGP; the y indices were loaded during level q-1), then
-    // the fma chain, then the y stores. Everything else — level q+1's y
-    // indices (before the chain) and term values (after the stores), the row
-    // records of level q+2 — is issued in the shadow of that round trip. One
-    // wave's LDS accesses are performed in order (the fences below are
-    // wavefront scope), so no counter and no barrier orders the levels.
-    // Groups past a row's own read the pad group (exact no-op fmas); lanes past
-    // a level's rows repeat its last row (same value to the same slot); level
-    // words past the run repeat its last level (loaded, never used). Rows of
-    // more than NGP groups take their remaining groups inside the level.
-    // Same terms, same order, same fma chain as every other solve path: same bits.
-    auto narrow_run_pf = [&](int q0, int q1) {  // wave 0
-        constexpr int NGP = 8 / G;  // groups prefetched per level (8 terms)
-        const int lane = tid;
-        struct Lv {
-            ThinRow<T> R;
-            int ng;  // the level's largest group count (wave-uniform)
-        };
-        auto word = [&](int q) { return lvw[min(q, q1 - 1)]; };
-        auto rec = [&](int wv) {  // this lane's row of the level with word wv
-            const int w = __builtin_amdgcn_readfirstlane(wv);
-            Lv v;
-            v.R = lrow[(w & 1023) + min(lane, (w >> 10) & 63)];
-            v.ng = w >> 16;
-            return v;
-        };
-        auto grp = [&](const ThinRow<T> &R, int g) { return g < (R.g >> 16) ? (R.g & 0xffff) + g : kPadGroup; };
-        TermIds<G> ic[NGP];
-        TermGroup<T, G> vc[NGP];
-        int gc[NGP];
-        auto ids = [&](const ThinRow<T> &R) {
-#pragma unroll
-            for (int g = 0; g < NGP; ++g) {
-                gc[g] = grp(R, g);
-                ic[g] = lidx[gc[g]];
-            }
-        };
-        auto values = [&] {
-#pragma unroll
-            for (int g = 0; g < NGP; ++g) vc[g] = lval[gc[g]];
-        };
-        // Level q: c its records, n level q+1's, m <- level q+2's (from its word
-        // wm, loaded one level earlier), wn <- level q+3's word. NG = the
-        // level's group count, a compile-time constant per branch (NGP + 1:
-        // more than NGP), so each branch is straight-line code.
-        auto body = [&](const Lv &c, const Lv &n, Lv &m, const int &wm, int &wn, int q) {
-            auto run = [&](auto ngc) {
-                constexpr int NG = decltype(ngc)::value;
-                constexpr int NL = NG < NGP ? NG : NGP;
-                T yv[NL > 0 ? NL : 1][G];
-#pragma unroll
-                for (int g = 0; g < NL; ++g)
-#pragma unroll
-                    for (int j = 0; j < G; ++j) yv[g][j] = yb(ic[g].v[j]);
-                __builtin_amdgcn_sched_barrier(0);  // level q's y loads first: the chain waits for them only
-                ids(n.R);  // level q+1's y indices (ic is free once these y loads are issued)
-                m = rec(wm);
-                wn = word(q + 3);
-                __builtin_amdgcn_sched_barrier(0);
-                T s = c.R.x;
-#pragma unroll
-                for (int g = 0; g < NL; ++g)
-#pragma unroll
-                    for (int j = 0; j < G; ++j) s = fma_t(-vc[g].v[j], yv[g][j], s);
-                if constexpr (NG > NGP) {
-                    for (int g = NGP; g < c.ng; ++g) {  // rows of more groups (uniform bound)
-                        const int gi = grp(c.R, g);
-                        s = group_fma(s, lval[gi], lidx[gi]);
-                    }
-                }
-                put(c.R.out, s);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-                values();  // level q+1's term values (needed after its y loads)
-            };
-            static_assert(NGP == 4 || NGP == 2, "prefetch depth");
-            switch (c.ng) {
-                case 0: run(std::integral_constant<int, 0>()); break;
-                case 1: run(std::integral_constant<int, 1>()); break;
-                case 2: run(std::integral_constant<int, 2>()); break;
-                case 3:
-                    if constexpr (NGP >= 3) {
-                        run(std::integral_constant<int, NGP >= 3 ? 3 : NGP + 1>());
-                        break;
-                    }
-                    [[fallthrough]];
-                case 4:
-                    if constexpr (NGP >= 4) {
-                        run(std::integral_constant<int, NGP >= 4 ? 4 : NGP + 1>());
-                        break;
-                    }
-                    [[fallthrough]];
-                default: run(std::integral_constant<int, NGP + 1>()); break;
-            }
-        };
-        Lv L0 = rec(word(q0)), L1 = rec(word(q0 + 1)), L2;
-        int W0 = word(q0 + 2), W1, W2;
-        ids(L0.R);
-        values();
-        // drain the prologue (see narrow_run: a pending load at the loop head
-        // makes the compiler wait at the head of every level)
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        for (int q = q0;; q += 3) {  // unrolled by the records' rotation (no register copies)
-            body(L0, L1, L2, W0, W1, q);
-            if (q + 1 >= q1) break;
-            body(L1, L2, L0, W1, W2, q + 1);
-            if (q + 2 >= q1) break;
-            body(L2, L0, L1, W2, W0, q + 2);
-            if (q + 3 >= q1) break;
-        }
-    };
-    // PF2 (round 5): narrow_run_pf with the per-level and per-row work of the
-    // loop moved to the chunk's marking pass (below): each row of a narrow
-    // level carries the LDS addresses of its first NGP term groups' y indices
-    // (lgl; the pad group past the row's own groups), so a group's y indices
-    // and values are one address extraction and one load each; and the level
-    // words of 64 consecutive levels sit in one VGPR (lane l = level qb + l),
-    // read with v_readlane instead of a load per level. Same terms, same
-    // order, same fma chain: same bits.
-    auto narrow_run_pf2 = [&](int x0, int q0, int q1) {  // wave 0
-        constexpr int NGP = 8 / G;
-        constexpr int VS = (int)(sizeof(TermGroup<T, G>) / sizeof(TermIds<G>));  // lval / lidx entry size
-        const int lane = tid;
-        struct Lv {
-            T x;
-            int out;
-            uint2 gl;  // group y-index addresses, 16 bits each
-            int ng;    // the level's largest group count (wave-uniform)
-        };
-        // the words of levels [qb, qb + 64) in wv, [qb + 64, qb + 128) in wv2;
-        // qb advances by 63 levels (21 turns of the 3-level loop below)
-        int qb = q0;
-        auto words = [&] {
-            return make_int2(lvw[min(qb + lane, q1 - 1)], lvw[min(qb + 64 + lane, q1 - 1)]);
-        };
-        int2 wv = words();
-        auto rec = [&](int q) {
-            const int i = q - qb;  // 0 .. 65
-            const int w0 = __builtin_amdgcn_readlane(wv.x, i), w1 = __builtin_amdgcn_readlane(wv.y, i - 64);
-            const int w = i < 64 ? w0 : w1;
-            const int r = (w & 1023) + min(lane, (w >> 10) & 63);
-            const ThinRow<T> R = lrow[r];
-            Lv v;
-            v.x = R.x;
-            v.out = R.out;
-            v.gl = lgl[r];
-            v.ng = w >> 16;
-            return v;
-        };
-        auto gaddr = [&](const uint2 &gl, int g) {
-            const unsigned u = (g >> 1) ? gl.y : gl.x;
-            return (g & 1) ? (int)(u >> 16) : (int)(u & 0xffff);
-        };
-        TermIds<G> ic[NGP];
-        TermGroup<T, G> vc[NGP];
-        int ga[NGP];
-        auto ids = [&](const Lv &n) {
-#pragma unroll
-            for (int g = 0; g < NGP; ++g) {
-                ga[g] = gaddr(n.gl, g);
-                ic[g] = *(const TermIds<G> *)(lds_arena + ga[g]);
-            }
-        };
-        auto values = [&] {
-#pragma unroll
-            for (int g = 0; g < NGP; ++g) vc[g] = *(const TermGroup<T, G> *)(lds_arena + Lay::val + VS * ga[g]);
-        };
-        auto body = [&](const Lv &c, const Lv &n, Lv &m, int q) {
-            auto run = [&](auto ngc) {
-                constexpr int NG = decltype(ngc)::value;
-                constexpr int NL = NG < NGP ? NG : NGP;
-                T yv[NL > 0 ? NL : 1][G];
-#pragma unroll
-                for (int g = 0; g < NL; ++g)
-#pragma unroll
-                    for (int j = 0; j < G; ++j) yv[g][j] = yb(ic[g].v[j]);
-                __builtin_amdgcn_sched_barrier(0);  // level q's y loads first: the chain waits for them only
-                ids(n);
-                m = rec(q + 2);
-                __builtin_amdgcn_sched_barrier(0);
-                T s = c.x;
-#pragma unroll
-                for (int g = 0; g < NL; ++g)
-#pragma unroll
-                    for (int j = 0; j < G; ++j) s = fma_t(-vc[g].v[j], yv[g][j], s);
-                if constexpr (NG > NGP) {  // rows of more groups (uniform bound): their groups past NGP
-                    // the row from its y window slot (the window outlasts a chunk's rows)
-                    const int gr = lrow[(c.out / (int)sizeof(T) - (x0 - base)) & (rsp::kYWin - 1)].g;
-                    for (int g = NGP; g < c.ng; ++g) {
-                        const int gi = g < (gr >> 16) ? (gr & 0xffff) + g : kPadGroup;
-                        s = group_fma(s, lval[gi], lidx[gi]);
-                    }
-                }
-                put(c.out, s);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-                values();  // level q+1's term values (needed after its y loads)
-            };
-            switch (c.ng) {
-                case 0: run(std::integral_constant<int, 0>()); break;
-                case 1: run(std::integral_constant<int, 1>()); break;
-                case 2: run(std::integral_constant<int, 2>()); break;
-                case 3:
-                    if constexpr (NGP >= 3) {
-                        run(std::integral_constant<int, NGP >= 3 ? 3 : NGP + 1>());
-                        break;
-                    }
-                    [[fallthrough]];
-                case 4:
-                    if constexpr (NGP >= 4) {
-                        run(std::integral_constant<int, NGP >= 4 ? 4 : NGP + 1>());
-                        break;
-                    }
-                    [[fallthrough]];
-                default: run(std::integral_constant<int, NGP + 1>()); break;
-            }
-        };
-        Lv L0 = rec(q0), L1 = rec(q0 + 1), L2;
-        ids(L0);
-        values();
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): drain the prologue (see narrow_run)
-        for (int q = q0;; q += 3) {
-            if (q - qb >= 63) {  // wave-uniform, every 21 turns: the next words
-                qb += 63;
-                wv = words();
-            }
-            body(L0, L1, L2, q);
-            if (q + 1 >= q1) break;
-            body(L1, L2, L0, q + 1);
-            if (q + 2 >= q1) break;
-            body(L2, L0, L1, q + 2);
-            if (q + 3 >= q1) break;
-        }
-    };
-    auto levels = [&](const rsp::LevelChunk &ch) {
+    // NAR: this thread may compute narrow runs (the loaders of LW > 0 never
+    // do: their instance of levels() leaves that code, and its registers, out)
+    auto levels = [&](const rsp::LevelChunk &ch, auto nar) {
+        constexpr bool NAR = decltype(nar)::value;
         const int x0 = ch.x0, nl = ch.l1 - ch.l0;
-        if constexpr (PF) {  // the narrow levels' words (narrow_run_pf): one thread per level
-            for (int q = tid; q < nl; q += NTH) {
-                const int p0 = lptr[q], cnt = lptr[q + 1] - p0;
-                if (cnt <= 64 && lns[q] == cnt) {
-                    int ngm = 0;
-                    for (int r = 0; r < cnt; ++r) ngm = max(ngm, lrow[p0 - x0 + r].g >> 16);
-                    lvw[q] = (p0 - x0) | (cnt - 1) << 10 | ngm << 16;
-                }
-            }
-            if constexpr (PF2) {  // every row: its first 8 / G groups' y-index addresses (pad past its own)
-                if (tid < ch.x1 - x0) {
-                    const int gr = lrow[tid].g, g0 = gr & 0xffff, ng = gr >> 16;
-                    unsigned o[4];
-#pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                        o[g] = (unsigned)((g < ng ? g0 + g : kPadGroup) * (int)sizeof(TermIds<G>) + Lay::idx);
-                    lgl[tid] = make_uint2(o[0] | o[1] << 16, o[2] | o[3] << 16);
-                }
-            }
-            lds_barrier();
-        }
 #if RSP_THIN_LONG_READLANE
         auto vat = [&](int k) { return lval[k / G].v[k % G]; };
         auto yat = [&](int k) { return yb(lidx[k / G].v[k % G]); };
@@ -2185,12 +2010,9 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
         for (int q = 0; q < nl;) {
             if (narrow(q)) {
                 const int qe = run_end(q, nl);
-                const int K = min(a.narrow_waves, (int)(blockDim.x >> 6));  // waves of this launch
-                if constexpr (PF2) {
-                    if (tid < 64) narrow_run_pf2(x0, q, qe);
-                } else if constexpr (PF) {
-                    if (tid < 64) narrow_run_pf(q, qe);
-                } else if (KIND != 2 && G == 2 && a.narrow_split) {  // (G = 4: the registers are not there)
+                if constexpr (NAR) {
+                const int K = min(a.narrow_waves, LW > 0 ? LW : (int)(blockDim.x >> 6));  // waves of this launch
+                if (KIND != 2 && G == 2 && a.narrow_split) {  // (G = 4: the registers are not there)
                     if constexpr (KIND != 2 && G == 2)
                         if (tid < 64) narrow_run_split(ch, q, qe);
                 } else if (PAIRS && K > 1) {  // (its own instantiation: the registers)
@@ -2204,16 +2026,17 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                     else
                         narrow_run(ch, q, qe, std::false_type());
                 }
+                }
                 lds_barrier();
                 q = qe;
                 continue;
             }
             const int l = ch.l0 + q;
             const int lp = lptr[q], off = lp - x0, cnt = lptr[q + 1] - lp, ns = lns[q];
-            if (tid < ns) {
-                const ThinRow<T> r = lrow[off + tid];
+            for (int t = tid; t < ns; t += NTH) {  // (one pass: ns <= kThinSolveRows <= NTH)
+                const ThinRow<T> r = lrow[off + t];
                 T s = row_value(r);
-                if constexpr (KIND == 2) s = s / ldg[off + tid];
+                if constexpr (KIND == 2) s = s / ldg[off + t];
                 put(r.out, s);
             }
             for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
@@ -2259,31 +2082,47 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     // and the staged-term list of chunk c+2. Streams have no dependent loads,
     // so one chunk of lead hides them.
     const int cl = c1 - 1;
-    rsp::LevelChunk rc = chunk(c0), rn = chunk(min(c0 + 1, cl));
-    Pre p = load_pre(rc);
-    StgY w = load_stgy(load_stg(rc));
-    Stg sn = load_stg(rn);
     int px0 = 0, px1 = 0;  // the chunk to flush at the next switch
-    for (int c = c0; c < c1; ++c) {
-        stage(c, px0, px1, rc, p, w);
-        const rsp::LevelChunk cur = rc;
-        if (c + 1 < c1) {
-            const rsp::LevelChunk r2 = chunk(min(c + 2, cl));
-            p = load_pre(rn);                           // chunk c+1's streams
-            if (rn.st1 > rn.st0) w = load_stgy(sn);     // ... and its staged y
-            if (r2.st1 > r2.st0) sn = load_stg(r2);     // chunk c+2's staged terms
-            rc = rn;
-            rn = r2;
+    if (LW == 0 || lt >= 0) {  // the loaders (every thread when LW == 0)
+        rsp::LevelChunk rc = chunk(c0), rn = chunk(min(c0 + 1, cl));
+        Pre p = load_pre(rc);
+        StgY w = load_stgy(load_stg(rc));
+        Stg sn = load_stg(rn);
+        for (int c = c0; c < c1; ++c) {
+            stage(c, px0, px1, rc, p, w);
+            const rsp::LevelChunk cur = rc;
+            if (c + 1 < c1) {
+                const rsp::LevelChunk r2 = chunk(min(c + 2, cl));
+                p = load_pre(rn);                           // chunk c+1's streams
+                if (rn.st1 > rn.st0) w = load_stgy(sn);     // ... and its staged y
+                if (r2.st1 > r2.st0) sn = load_stg(r2);     // chunk c+2's staged terms
+                rc = rn;
+                rn = r2;
+            }
+            mark_by(c, 4, 0);  // diagnostics: prefetch issued (wave 0 / last wave)
+            mark_by(c, 5, NTH - 64);
+            levels(cur, std::integral_constant<bool, LW == 0>());
+            mark(c, 3);
+            px0 = cur.x0;
+            px1 = cur.x1;
         }
-        mark_by(c, 4, 0);  // diagnostics: prefetch issued (wave 0 / last wave)
-        mark_by(c, 5, NTH - 64);
-        levels(cur);
-        mark(c, 3);
-        px0 = cur.x0;
-        px1 = cur.x1;
+    } else {  // the first LW waves: the same barriers, no prefetch (so none of its registers)
+        for (int c = c0; c < c1; ++c) {
+            const rsp::LevelChunk cur = chunk(c);
+            mark(c, 0);
+            __syncthreads();  // stage(): the loaders restage the chunk between these two
+            mark(c, 1);
+            lds_barrier();
+            mark(c, 2);
+            mark_by(c, 4, 0);
+            levels(cur, std::true_type());
+            mark(c, 3);
+            px0 = cur.x0;
+            px1 = cur.x1;
+        }
     }
     // the last chunk's rows (its levels ended with a barrier)
-    if (tid < px1 - px0) y[lrowi[tid]] = ybuf[(px0 + tid - base) & (rsp::kYWin - 1)];
+    for (int t = tid; t < px1 - px0; t += NTH) y[lrowi[t]] = ybuf[(px0 + t - base) & (rsp::kYWin - 1)];
 }
 
 // --------------------------------------------------------------- launchers
@@ -2383,16 +2222,13 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             // 3.22; on wider DAGs' narrow runs they cost: parabolic_fem 3.55
             // -> 3.95, Dubcova3 2.59 -> 2.84, thermomech_TK 0.95 -> 1.00)
             const bool pr = KIND != 2 && (a.narrow_pairs > 0 || (a.narrow_pairs < 0 && a.n <= 32LL * P.nlev));
-            // the one-wave prefetching narrow runs (L / L^T): RSP_ILU_NARROW_PF 1 / 0
-            // (2: the precomputed-address form)
-            const bool pf = KIND != 2 && a.narrow_pf > 0, pf2 = pf && a.narrow_pf == 2;
-            constexpr int NP = KIND != 2 ? 1 : 0, NF = KIND != 2 ? 2 : 0, NF2 = KIND != 2 ? 3 : 0;
-            auto kern = P.group == 2 ? (pf2 ? trsv_thin_pf<T, KIND, 2, NF2>
-                                        : pf ? trsv_thin_pf<T, KIND, 2, NF>
-                                             : pr ? trsv_thin_pf<T, KIND, 2, NP> : trsv_thin_pf<T, KIND, 2>)
-                                     : (pf2 ? trsv_thin_pf<T, KIND, 4, NF2>
-                                        : pf ? trsv_thin_pf<T, KIND, 4, NF>
-                                             : pr ? trsv_thin_pf<T, KIND, 4, NP> : trsv_thin_pf<T, KIND, 4>);
+            // the pair loop's waves never load the next chunk (LW = 4;
+            // RSP_ILU_LOADERS=0 turns that off)
+            const bool ldr = pr && a.loaders != 0;
+            auto kern = P.group == 2 ? (pr ? (ldr ? trsv_thin_pf<T, KIND, 2, KIND != 2, 4> : trsv_thin_pf<T, KIND, 2, KIND != 2>)
+                                           : trsv_thin_pf<T, KIND, 2>)
+                                     : (pr ? (ldr ? trsv_thin_pf<T, KIND, 4, KIND != 2, 4> : trsv_thin_pf<T, KIND, 4, KIND != 2>)
+                                           : trsv_thin_pf<T, KIND, 4>);
             hipLaunchKernelGGL(kern, dim3(1), dim3(kThinThreads), 0, s, a, sg.c0, sg.c1, P.ptr_host[sg.lb]);
             continue;
         }

@@ -2055,7 +2055,7 @@ static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alp
     a.narrow_waves = std::min(std::max(env_int("RSP_ILU_NARROW_WAVES", 4), 1), rsp::kThinThreads / 64);
     a.narrow_split = env_int("RSP_ILU_NARROW_SPLIT", 0) != 0;  // (default off: slower)
     a.narrow_pairs = env_int("RSP_ILU_NARROW_PAIRS", -1);  // -1: by the DAG's level width (launcher)
-    a.narrow_pf = env_int("RSP_ILU_NARROW_PF", 0);
+    a.loaders = env_int("RSP_ILU_LOADERS", 1);
     a.flow = env_int("RSP_ILU_FLOW", 1) != 0;
     // every workgroup of a flow launch must be resident at once (an item waits
     // for items of lower index only, and workgroups take items in index

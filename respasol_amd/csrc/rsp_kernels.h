@@ -392,7 +392,7 @@ struct TrsvArgs {
     int narrow_waves;           // thin runs: waves sharing a narrow run, levels round-robin (RSP_ILU_NARROW_WAVES)
     int narrow_split;           // L / L^T narrow runs: one wave, early sums under the late loads (RSP_ILU_NARROW_SPLIT)
     int narrow_pairs;           // L / L^T narrow runs on K waves, two levels per turn (RSP_ILU_NARROW_PAIRS: 1 / 0, -1 auto)
-    int narrow_pf;              // L / L^T narrow runs on one wave, next level's term groups prefetched (RSP_ILU_NARROW_PF)
+    int loaders;                // thin runs with the pair loop: its waves never load the next chunk (RSP_ILU_LOADERS)
     int flow;                   // run flow segments persistently (RSP_ILU_FLOW, default 1)
     int flow_grid;              // flow launch: 256-thread workgroups (RSP_ILU_FLOW_WPC waves per CU)
     int flow_cus;               // CUs of the device (caps a flow grid)

@@ -40,42 +40,8 @@
 #define RSP_KNS rsp_k
 #endif
 
-// Diagnostic builds only (scripts/spmv_probe.py, never the shipped library):
-// 1 = every gather hits the first 32 KiB of x (gather cost removed),
-// 2 = no row reduce (one LDS read per thread stands in for it),
-// 3 = 1 + 2, 4 = the tile's loads only (no gather, LDS or reduce).
-#ifndef RSP_PROBE
-#define RSP_PROBE 0
-#endif
-#ifndef RSP_PROBE_Y
-#define RSP_PROBE_Y 0  // with RSP_PROBE 4: also store y (one element per row)
-#endif
-#ifndef RSP_PROBE_NOSWIZZLE
-#define RSP_PROBE_NOSWIZZLE 0  // plain blockIdx -> tile order (A/B)
-#endif
-#ifndef RSP_PROBE_PRIO
-#define RSP_PROBE_PRIO 0  // s_setprio at kernel entry (A/B)
-#endif
 #ifndef RSP_NT_Y
-#define RSP_NT_Y -1  // y stores: 1 non-temporal, 0 plain, -1 (shipped) non-temporal for fp64 only
-#endif
-#ifndef RSP_PROBE_LDS
-#define RSP_PROBE_LDS 0  // with RSP_PROBE 4: also an LDS write + barrier
-#endif
-#ifndef RSP_GATHER_POL
-#define RSP_GATHER_POL 0  // x gathers as buffer loads with a cache policy (A/B)
-#endif
-#ifndef RSP_PROBE_NOY
-#define RSP_PROBE_NOY 0  // the short-row y stores kept behind a never-taken test (their cost)
-#endif
-#ifndef RSP_PROBE_YSMALL
-#define RSP_PROBE_YSMALL 0  // the short-row y stores aimed at an L2-resident 1024-entry window
-#endif
-#ifndef RSP_SPMV_MINBLK
-#define RSP_SPMV_MINBLK 1  // __launch_bounds__ min blocks per CU (A/B: 8 caps the tiles at 64 VGPRs)
-#endif
-#ifndef RSP_PROBE_WALK
-#define RSP_PROBE_WALK 0  // spmv_tiles: each workgroup walks this many consecutive tiles
+#define RSP_NT_Y -1  // y stores: 1 non-temporal, 0 plain, -1 (shipped) non-temporal for fp64 only (A/B)
 #endif
 
 namespace RSP_KNS {
@@ -168,17 +134,7 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
     // keep the scheduler from splitting the load and gather bursts: two
     // memory round trips per tile, not one per vector
     __builtin_amdgcn_sched_barrier(0);
-#if RSP_PROBE_PRIO
-    __builtin_amdgcn_s_setprio(0);  // loads issued: back to normal priority
-#endif
     T xv[IT][VW];
-#if RSP_GATHER_POL
-    // diagnostic builds: x gathers as buffer loads with a cache policy
-    // (1 sc0, 2 nt, 3 sc1, 4 none) — scripts/spmv_probe.py gp1..gp4
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7ffffff0, 0x00020000);
-    constexpr int kAux = RSP_GATHER_POL == 1 ? 1 : RSP_GATHER_POL == 2 ? 2 : RSP_GATHER_POL == 3 ? 16 : 0;
-#endif
 #pragma unroll
     for (int it = 0; it < IT; ++it)
 #pragma unroll
@@ -188,14 +144,7 @@ __device__ __forceinline__ void stream_products(const int *__restrict__ colidx,
                 c = min(cbase + (int)ch[it][j], cmax);
             else
                 c = ci[it][j];
-#if RSP_GATHER_POL
-            if constexpr (sizeof(T) == 8)
-                xv[it][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr, c * 8, 0, kAux));
-            else
-                xv[it][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(xr, c * 4, 0, kAux));
-#else
-            xv[it][j] = x[(RSP_PROBE == 1 || RSP_PROBE == 3) ? (c & 4095) : c];
-#endif
+            xv[it][j] = x[c];
         }
     __builtin_amdgcn_sched_barrier(0);
     // every slot (it*256 + tid)*VW lies inside the tile's LDS image, so the
@@ -402,6 +351,10 @@ __device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
     return (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
 }
 
+#ifdef RSP_SPMV_PROBE_LOADS
+#include "spmv_probe.h"
+#endif
+
 // One tile: stream -> gathers -> products in LDS -> canonical reduce -> y.
 // BETA: beta != 0 (y is read); the beta == 0 form issues no y loads, so its
 // y stores never wait on anything.
@@ -486,34 +439,9 @@ __device__ __forceinline__ void spmv_tile(
     // vectors may be used unless the tile reaches the last, partial vector
     const bool vec = vector_ok && k1 > k0 && k1 <= (nnz & ~(VW - 1));
     const int kb = vec ? (k0 & ~(VW - 1)) : k0;
-#if RSP_PROBE == 4
-    if (vec) {  // diagnostic: the tile's colidx/vals stream alone
-        typedef typename VecT<T, VW>::V V;
-        typedef typename VecT<T, VW>::I I;
-        constexpr int IT = SpmvTile<T>::kSlots / (kSpmvThreads * VW);
-        const int last = (k1 - 1) & ~(VW - 1);
-        T acc = T(0);
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int e = min(kb + (it * kSpmvThreads + tid) * VW, last);
-            const I c = ld<NT>(reinterpret_cast<const I *>(colidx + e));
-            const V v = ld<NT>(reinterpret_cast<const V *>(vals + e));
-#pragma unroll
-            for (int j = 0; j < VW; ++j) acc += v[j] + T(c[j]);
-        }
-#if RSP_PROBE_Y
-#if RSP_NT_Y > 0
-        if (blk.r1 > 0 && tid < nrows) __builtin_nontemporal_store(acc, y + blk.r0 + tid);
-#else
-        if (blk.r1 > 0 && tid < nrows) y[blk.r0 + tid] = acc;  // + the y stream
-#endif
-#endif
-#if RSP_PROBE_LDS
-        lds[tid] = acc;  // + an LDS write and a workgroup barrier
-        __syncthreads();
-        acc = lds[(tid + 1) & (kSpmvThreads - 1)];
-#endif
-        if (acc == T(-12345.0)) y[blk.r0] = acc + T(rpv[0]);  // keeps every load live
+#ifdef RSP_SPMV_PROBE_LOADS  // diagnostic builds only (make probe; scripts/spmv_probe.py loadsonly)
+    if (vec) {
+        probe_tile_loads<T, NT>(colidx, vals, y, blk, kb, k1, rpv[0]);
         return;
     }
 #endif
@@ -549,26 +477,17 @@ __device__ __forceinline__ void spmv_tile(
     }
 
     const int r0 = blk.r0;
-    if (RSP_PROBE == 2 || RSP_PROBE == 3) {
-        if (tid < nrows) y[r0 + tid] = lds[tid];
-        return;
-    }
     reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, 0, [&](int rr, T sum) {
         T out = alpha * sum;
-        if (RSP_PROBE_NOY && out != T(-12345.0)) return;
         if (BETA) out += beta * y[r0 + rr];
         // fp64: non-temporal y stores (the y lines leave L2 as a stream;
         // -3 % per pass on the big set, where plain y write-back costs ~16 %
         // of the time for ~4 % of the bytes); fp32: plain stores (nt +2 %)
         constexpr bool kNtY = RSP_NT_Y > 0 || (RSP_NT_Y < 0 && sizeof(T) == 8);
-#if RSP_PROBE_YSMALL
-        y[(r0 + rr) & 1023] = out;
-#else
         if constexpr (kNtY)
             __builtin_nontemporal_store(out, y + r0 + rr);
         else
             y[r0 + rr] = out;
-#endif
     });
 }
 
@@ -577,7 +496,7 @@ __device__ __forceinline__ void spmv_tile(
 // -18 %), all of a workgroup's tiles loaded up front (-4 %), a software-
 // pipelined persistent kernel (-29 %), one-wave tiles (-1 %).
 template <typename T, bool NT, bool BETA>
-__global__ __launch_bounds__(kSpmvThreads, RSP_SPMV_MINBLK) void spmv_tiles(
+__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     const int *__restrict__ rowptr, const int *__restrict__ colidx, const T *__restrict__ vals,
     const T *__restrict__ x, T *__restrict__ y, const SpmvBlock *__restrict__ blocks, int nblocks,
     const int *__restrict__ cbases, const unsigned short *__restrict__ cidx, const int *__restrict__ runs,
@@ -585,28 +504,7 @@ __global__ __launch_bounds__(kSpmvThreads, RSP_SPMV_MINBLK) void spmv_tiles(
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
     __shared__ unsigned short rp_lds[SpmvTile<T>::kMaxRows + 2];  // row offsets - kb
-#if RSP_PROBE_WALK
-    // diagnostic: tiles [W t, W t + W) of the swizzled workgroup t in turn,
-    // an LDS-only barrier between them (the previous tile's y stores stay in
-    // flight under the next tile's stream)
-    const int nwg = (nblocks + RSP_PROBE_WALK - 1) / RSP_PROBE_WALK;
-    const int t0 = xcd_swizzle(blockIdx.x, nwg) * RSP_PROBE_WALK;
-    for (int w = 0; w < RSP_PROBE_WALK && t0 + w < nblocks; ++w) {
-        if (w) lds_barrier();
-        spmv_tile<T, NT, BETA>(blocks[t0 + w], rowptr, colidx, cidx, runs, cbases[t0 + w], cmax, vals, x,
-                               y, partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum,
-                               rp_lds, fuse);
-    }
-    return;
-#endif
-#if RSP_PROBE_NOSWIZZLE
-    const int b = blockIdx.x;
-#else
     const int b = xcd_swizzle(blockIdx.x, nblocks);
-#endif
-#if RSP_PROBE_PRIO
-    __builtin_amdgcn_s_setprio(RSP_PROBE_PRIO);
-#endif
     spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, cidx, runs, cbases[b], cmax, vals, x, y,
                            partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds,
                            fuse);
@@ -651,7 +549,7 @@ __global__ __launch_bounds__(64) void spmv_longrow_fixup(const SpmvLongRow *__re
 // One launch instead of one per matrix removes the per-kernel ramp and drain
 // (~5 us each on the big set, more than the whole SpMV of a small slice).
 template <typename T, bool NT, bool BETA, bool SWZ>
-__global__ __launch_bounds__(kSpmvThreads, RSP_SPMV_MINBLK) void spmv_tiles_batch(
+__global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     const SpmvBatchEntry *__restrict__ entries, const SpmvBlock *__restrict__ tiles,
     const int *__restrict__ cbases, SpmvBatchTable at, T alpha, T beta, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
@@ -743,8 +641,7 @@ static hipError_t launch_spmv(const SpmvArgs &a, hipStream_t s) {
     // variant bit 0 restores default-policy loads for A/B runs
     auto kern = (a.variant & 1) ? (bnz ? spmv_tiles<T, false, true> : spmv_tiles<T, false, false>)
                                 : (bnz ? spmv_tiles<T, true, true> : spmv_tiles<T, true, false>);
-    hipLaunchKernelGGL(kern, dim3(RSP_PROBE_WALK ? (a.nblocks + RSP_PROBE_WALK - 1) / (RSP_PROBE_WALK ? RSP_PROBE_WALK : 1)
-                                                : a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
+    hipLaunchKernelGGL(kern, dim3(a.nblocks), dim3(kSpmvThreads), 0, s, a.rowptr, a.colidx,
                        (const T *)a.vals, (const T *)a.x, (T *)a.y, a.blocks, a.nblocks, a.cbases,
                        a.cidx, a.runs, a.cmax, (T *)a.partials, alpha, beta, bnz, a.nnz, a.vector_ok, fuse);
     hipError_t e = hipGetLastError();

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 4 session 2: the full GPU test suite, the driver's bench command, the
+# Round session: the full GPU test suite, the driver's bench command, the
 # config-2 bench and the config-3 ILU bench. Each step has its own limit.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/${1:-r04f}
+O=gpurun_out/${1:-r05f}
 mkdir -p "$O"
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > "$O/pytest_gpu.txt" 2>&1
