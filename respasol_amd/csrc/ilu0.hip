@@ -1440,7 +1440,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
     constexpr int TPT = (rsp::kChunkTerms + NL - 1) / NL;  // terms of a chunk per loader: lt + j NL
     constexpr int RPT = (rsp::kChunkRows + NL - 1) / NL;   // rows (and level pointers) per loader: lt + r NL
     static_assert(NL > 0 && G <= rsp::kGroup, "chunk loaders");
-    static_assert(NTH >= rsp::kThinSolveRows, "one pass over a thin level's short rows");
+    static_assert(NTH >= rsp::kChunkRows, "a thin level's short rows: one per thread");
     constexpr int kZero = rsp::kYWin, kStaged = rsp::kYWin + 1;
     // + one pad group (values 0, y from the zero slot) after the chunk's groups
     constexpr int kPadGroup = rsp::kChunkTerms / G;
@@ -2033,10 +2033,10 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             }
             const int l = ch.l0 + q;
             const int lp = lptr[q], off = lp - x0, cnt = lptr[q + 1] - lp, ns = lns[q];
-            for (int t = tid; t < ns; t += NTH) {  // (one pass: ns <= kThinSolveRows <= NTH)
-                const ThinRow<T> r = lrow[off + t];
+            if (tid < ns) {  // (ns <= kChunkRows <= NTH)
+                const ThinRow<T> r = lrow[off + tid];
                 T s = row_value(r);
-                if constexpr (KIND == 2) s = s / ldg[off + t];
+                if constexpr (KIND == 2) s = s / ldg[off + tid];
                 put(r.out, s);
             }
             for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
