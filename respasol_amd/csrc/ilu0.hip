@@ -57,6 +57,7 @@ using rsp::TrsvArgs;
 __device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+
 // s - sum_p v_p y_p as a serial fma chain over p = p0 .. p1-1, ascending.
 // The operands of B consecutive terms are loaded together (clamped,
 // unpredicated) so the loads of a batch overlap instead of serialising

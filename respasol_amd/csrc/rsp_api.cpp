@@ -1002,6 +1002,36 @@ static rsp_status_t rsp_spmv_batch_create_impl(rsp_handle_t h, int count, const 
         }
         spans.push_back(sp);
     }
+    // Layout invariant (the round-4 fault was a zero-fill that reached the
+    // entries and tiles of a later launch): every region of every launch lies
+    // inside the allocation, after the previous one, and overlaps no other;
+    // in particular each member's partials and tickets (zeros of the image,
+    // written by nothing else here) are its own.
+    {
+        size_t end = 0;
+        auto region = [&](size_t off, size_t len) {
+            const bool ok = off >= end && off + len <= bytes;
+            end = off + len;
+            return ok;
+        };
+        for (const Span &sp : spans) {
+            int nt = 0, nl = 0;
+            for (int q = 0; q < sp.count; q++) {
+                int t0, t1;
+                tile_range(plans[sp.first + q], &t0, &t1);
+                nt += t1 - t0;
+                nl += part == 1 ? 0 : (int)plans[sp.first + q].longrows.size();
+            }
+            bool ok = region(sp.off_e, (size_t)sp.count * sizeof(rsp::SpmvBatchEntry)) &&
+                      region(sp.off_t, (size_t)nt * sizeof(SpmvBlock)) && region(sp.off_c, (size_t)nt * sizeof(int)) &&
+                      region(sp.off_l, (size_t)nl * sizeof(SpmvLongRow));
+            for (int q = 0; ok && q < sp.count; q++) ok = region(sp.off_16[q], plans[sp.first + q].c16.size() * 2);
+            for (int q = 0; ok && q < sp.count; q++) ok = region(sp.off_r[q], plans[sp.first + q].runs.size() * 4);
+            for (int q = 0; ok && q < sp.count; q++)
+                ok = region(sp.off_p[q], (size_t)plans[sp.first + q].nslots * 2 * elem_size(compute_type));
+            if (!ok) return RSP_STATUS_INTERNAL_ERROR;
+        }
+    }
     if (bytes > 0) RSP_CHECK_HIP(hipMalloc(&b->d_mem, bytes));
     rsp_an::hvec<unsigned char> host(bytes);
     for (const Span &sp : spans) {
