@@ -219,7 +219,14 @@ __device__ __forceinline__ void lds_barrier() {
 #define RSP_POLL_SLEEP 1
 #endif
 __device__ __forceinline__ void lds_wait_geq(int *p, int want, int near) {
-#if RSP_POLL_MODE == 3
+#if RSP_POLL_MODE == 4
+    // sleep between polls; the publishing wave's s_wakeup (lds_publish) ends
+    // the sleep at once, so a waiting wave neither polls the LDS continuously
+    // (its reads queue beside the working wave's) nor sleeps past the hand-off
+    for (int it = 0; it < (1 << 26) && __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want;
+         ++it)
+        __builtin_amdgcn_s_sleep(RSP_POLL_SLEEP);
+#elif RSP_POLL_MODE == 3
     for (int it = 0; it < (1 << 26); ++it) {
         const int c = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -252,6 +259,9 @@ __device__ __forceinline__ void lds_publish(int *p, int v, bool leader) {
     if (leader) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #else
     if (leader) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+#if RSP_POLL_MODE == 4
+    asm volatile("s_wakeup" ::: "memory");  // the waves sleeping in lds_wait_geq
 #endif
 }
 

@@ -358,43 +358,60 @@ __device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
 // One tile: stream -> gathers -> products in LDS -> canonical reduce -> y.
 // BETA: beta != 0 (y is read); the beta == 0 form issues no y loads, so its
 // y stores never wait on anything.
-// A chunk of a long row (one lane): publish the chunk's partial, take a
-// ticket; the chunk that arrives last adds the row's partials in chunk order
-// (the fixup kernel's order: 0 + p0 + p1 + ...) and writes y. Partials and
-// tickets are agent-scope atomics; the ticket add is a release and the last
-// arriver issues an acquire fence before reading the partials, so the
-// ordering holds under the HIP memory model for chunks on any XCD (gfx950:
-// an L2 write-back before the add, an L2 invalidate in the last arriver).
-// No wait, no spin: the last arriver is told by the value its own add
-// returned. It resets the ticket.
+// A chunk of a long row (wave 0 of its tile): publish the chunk's partial,
+// take a ticket; the chunk that arrives last adds the row's partials in chunk
+// order (the fixup kernel's order: 0 + p0 + p1 + ...) and writes y. No wait,
+// no spin: the last arriver is told by the value its own add returned; it
+// resets the ticket. The hand-off is the write-through form of
+// MI355X_MICROARCH.md §Workgroup dispatch (valid forms; cdna_hip_programming.md
+// split-K recipe, "equally valid and cheaper"): the partial is an agent-scope
+// (sc1, write-through) store, drained by the storing lane's s_waitcnt vmcnt(0)
+// before its relaxed agent-scope ticket add, and the last arriver reads EVERY
+// partial with agent-scope (sc1) loads — so neither an L2 write-back
+// (release) nor an L1 invalidate (acquire) is on the row's path (round 5;
+// they were ~1.7 us each). The last arriver's lanes load the partials in
+// parallel (lane c: partial c), one memory round trip instead of one per
+// chunk, and the in-order sum runs on shuffles.
 template <typename T>
 __device__ __forceinline__ void longrow_arrive(const SpmvBlock blk, const int *__restrict__ rowptr,
                                                T *partials, T *__restrict__ y, T t, T alpha, T beta,
                                                bool beta_nz) {
     typedef typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type U;
     constexpr int C = SpmvTile<T>::kChunk;
+    const int lane = threadIdx.x & 63;
     const int slot = -(blk.r1 + 1);
     const int rs = rowptr[blk.r0], re = rowptr[blk.r0 + 1];
     const int first = slot - (blk.k0 - rs) / C;
     const int n = (re - rs + C - 1) / C;
-    U *pv = reinterpret_cast<U *>(partials);
-    unsigned int *ticket = reinterpret_cast<unsigned int *>(partials + 2 * first + 1);
-    __hip_atomic_store(pv + 2 * slot, __builtin_bit_cast(U, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // release: this chunk's partial is visible device-wide before its ticket
-    // moves; the last arriver's acquire fence then orders its partial reads
-    // after every other chunk's release (the standard last-block pattern)
-    const unsigned int arrived =
-        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived != (unsigned int)(n - 1)) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // global-address-space pointers: global_ (not flat_) instructions, the
+    // form the hand-off is measured for (the batched kernel's entry pointers
+    // are generic)
+    typedef __attribute__((address_space(1))) U GU;
+    typedef __attribute__((address_space(1))) unsigned int GI;
+    GU *pv = (GU *)reinterpret_cast<U *>(partials);
+    GI *ticket = (GI *)reinterpret_cast<unsigned int *>(partials + 2 * first + 1);
+    unsigned int arrived = 0;
+    if (lane == 0) {
+        __hip_atomic_store(pv + 2 * slot, __builtin_bit_cast(U, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial has left this CU before the ticket moves
+        arrived = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    arrived = (unsigned int)__builtin_amdgcn_readfirstlane((int)arrived);
+    if (arrived != (unsigned int)(n - 1)) return;  // wave-uniform
     T s = T(0);
-    for (int c = 0; c < n; ++c)
-        s += __builtin_bit_cast(T, __hip_atomic_load(pv + 2 * (first + c), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT));
-    T out = alpha * s;
-    if (beta_nz) out += beta * y[blk.r0];
-    y[blk.r0] = out;
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const T p = c0 + lane < n ? __builtin_bit_cast(T, __hip_atomic_load(pv + 2 * (first + c0 + lane),
+                                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                  : T(0);
+        const int cn = min(64, n - c0);
+        for (int c = 0; c < cn; ++c) s += __shfl(p, c, 64);
+    }
+    if (lane == 0) {
+        T out = alpha * s;
+        if (beta_nz) out += beta * y[blk.r0];
+        y[blk.r0] = out;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 template <typename T, bool NT, bool BETA>
@@ -462,13 +479,13 @@ __device__ __forceinline__ void spmv_tile(
 
     if (blk.r1 < 0) {  // a long row: written whole, or a chunk partial for the fixup
         const T t = reduce_long(lds, k0 - kb, k1 - kb, wsum);
-        if (tid == 0) {
+        if (blk.r1 != rsp::kSpmvWholeRow && fuse) {
+            if (tid < 64) longrow_arrive<T>(blk, rowptr, partials, y, t, alpha, beta, BETA);
+        } else if (tid == 0) {
             if (blk.r1 == rsp::kSpmvWholeRow) {
                 T out = alpha * t;
                 if (BETA) out += beta * y[blk.r0];
                 y[blk.r0] = out;
-            } else if (fuse) {
-                longrow_arrive<T>(blk, rowptr, partials, y, t, alpha, beta, BETA);
             } else {
                 partials[2 * -(blk.r1 + 1)] = t;
             }
