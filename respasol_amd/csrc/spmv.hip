@@ -296,13 +296,19 @@ __device__ __forceinline__ void reduce_rows(const T *lds, const unsigned short *
 #pragma unroll
         for (int t = 0; t < NA; ++t) acc[t] = T(0);
         if (active) {
-            const int a1 = rp_lds[rr + 1] - kb;
+            // branch-free: every step issues its NA loads together (clamped
+            // into the row) and adds a product or +0 (exact: a partial that
+            // starts at +0 is never -0). A predicated load per product made the
+            // compiler wait on each one, so a 256-entry row in a tile of short
+            // rows held its workgroup ~8 us (scripts/percall_probe.py).
+            const int a1 = rp_lds[rr + 1] - kb, last = a1 - 1;
             for (int base = rp_lds[rr] - kb + lane; base < a1; base += 8) {
+                T v[NA];
 #pragma unroll
-                for (int t = 0; t < NA; ++t) {
-                    const int k = base + t * L;  // partial (lane + t*L) of the row
-                    if (k < a1) acc[t] += lds[k];
-                }
+                for (int t = 0; t < NA; ++t) v[t] = lds[min(base + t * L, last)];
+#pragma unroll
+                for (int t = 0; t < NA; ++t)  // partial (lane + t*L) of the row
+                    acc[t] += base + t * L < a1 ? v[t] : T(0);
             }
         }
         // tree stages whose pair offset (4, 2, 1) is a multiple of L: local
