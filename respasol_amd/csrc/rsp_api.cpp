@@ -673,27 +673,6 @@ static int64_t spmv_resident_tiles(rsp_handle_t h, rsp_datatype_t t) {
     return (int64_t)rsp_k::spmv_tiles_per_cu((int)elem_size(t)) * h->num_cus;
 }
 
-// Whether a matrix's gathers are scattered (circuit-like): a row longer than
-// a tile, or more than 2 % of the entries of a sample of rows (every
-// m / 65536-th) more than 32768 columns off the diagonal. Only those gain from
-// being spread over every resident slot: their tiles wait on random x reads
-// and more of them in flight hide that; a local (stencil / FEM) matrix's
-// small tiles only add workgroups. Per call, 20 back-to-back calls of one
-// matrix (profiles/r03_spread_ab.txt): thermomech_TK 7.1 -> 6.0 us, cfd2
-// 8.4 -> 7.3, parabolic_fem 9.9 -> 8.4 unspread; G2_circuit 15.2 -> 11.3,
-// matrix-new_3 15.8 -> 12.9, ss1 18.8 -> 15.3 spread.
-static bool spmv_scattered(const int *rp, const int *ci, int m, int tile_cap) {
-    const int step = std::max(1, m / 65536);
-    int64_t far = 0, seen = 0;
-    for (int i = 0; i < m; i++) {
-        if (rp[i + 1] - rp[i] > tile_cap) return true;
-        if (i % step) continue;
-        for (int q = rp[i]; q < rp[i + 1]; q++) far += std::llabs((long long)ci[q] - i) > 32768;
-        seen += rp[i + 1] - rp[i];
-    }
-    return far * 50 > seen;
-}
-
 // Build the schedule of `mat` for `compute_type` into the matrix's own device
 // memory (host-blocking; see struct rsp_spmat).
 static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t compute_type) {
@@ -701,17 +680,17 @@ static rsp_status_t spmv_plan(rsp_handle_t h, rsp_spmat_t mat, rsp_datatype_t co
     rsp_an::hvec<int> rp, ci;
     rsp_status_t st = download_pattern(h, mat, rp, ci);
     if (st != RSP_STATUS_SUCCESS) return st;
-    const int chunk = chunk_cap(compute_type);
-    // A scattered matrix (spmv_scattered) with fewer tiles than the chip
-    // holds resident workgroups (R) leaves slots idle and runs each tile
-    // latency-bound: spread it over up to R smaller tiles (plans of >= 2
-    // waves are left alone, they lost 1 % this way); a local one keeps full
-    // tiles. A batch re-plans its members itself (rsp_spmv_batch_create).
-    // Tiling never changes the result (canonical summation order).
-    // RSP_SPMV_VARIANT bit 4 turns spreading off, bit 9 spreads every small
-    // matrix (round-2 rule), bit 5 keeps every tile on the int32 indices.
-    const bool spread = !(h->spmv_variant & 16) &&
-                        ((h->spmv_variant & 512) || spmv_scattered(rp.data(), ci.data(), m, chunk));
+    // Full tiles for every matrix. Rounds 3-4 spread a scattered (circuit)
+    // matrix with fewer tiles than resident slots over up to that many small
+    // tiles; once the row reduce stopped stalling on 33-256-entry rows (round
+    // 5: branch-free steps, heavy rows eight lanes each) the full tiles are
+    // faster per call: dc1 8.75 -> 7.02 us, G2_circuit 8.13 -> 6.10, ASIC_320ks
+    // 11.77 -> 9.22, ss1 8.49 -> 6.61, matrix-new_3 9.10 -> 6.71
+    // (profiles/r05_heavy_rows_ab.txt). RSP_SPMV_VARIANT bit 9 still spreads
+    // every small matrix (A/B), bit 5 keeps every tile on the int32 indices.
+    // A batch re-plans its members itself (rsp_spmv_batch_create). Tiling
+    // never changes the result (canonical summation order).
+    const bool spread = (h->spmv_variant & 512) != 0;
     TilePlan p;
     make_tile_plan(rp.data(), ci.data(), m, mat->nnz, compute_type,
                    spread ? spmv_resident_tiles(h, compute_type) : 0,

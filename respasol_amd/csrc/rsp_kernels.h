@@ -46,6 +46,7 @@ constexpr int kSpmvIter = RSP_SPMV_ITER;  // vectors per thread per tile
 #endif
 constexpr int kSpmvMaxRows = RSP_SPMV_MAXROWS;  // rows per tile (row offsets staged in LDS)
 constexpr int kSpmvLongRow = 256;   // rows longer than this get the 256-thread tree
+constexpr int kSpmvHeavyMax = 128;  // rows of > 32 entries a tile can hold (<= 4093 / 33)
 constexpr int kSpmvWholeRow = -2147483647 - 1;  // SpmvBlock::r1 marker (INT_MIN)
 template <typename T>
 struct SpmvTile {
@@ -68,6 +69,8 @@ struct SpmvTile {
     // occupancy step but would cost fp32 a wave per SIMD (71 -> 77 VGPRs)
     static constexpr bool kStageList = sizeof(T) == 8;
 };
+static_assert(SpmvTile<float>::kMaxNnz / 33 < kSpmvHeavyMax && SpmvTile<double>::kMaxNnz / 33 < kSpmvHeavyMax,
+              "every > 32-entry row of a tile fits the heavy-row list");
 constexpr int kStageRuns = 254;  // run descriptors per staged tile (+1 sentinel <= 256 threads)
 
 struct SpmvArgs {
@@ -94,7 +97,8 @@ struct SpmvArgs {
     int nnz;        // rowptr[m]: tiles touching the last partial vector go scalar
     int vector_ok;  // colidx/vals 16-B aligned -> vector loads
     int variant;    // bit 0: default-policy (not non-temporal) vals/colidx loads;
-                    // bit 4 (plan time): no spreading of sub-wave plans;
+                    // bit 4 (plan time): no spreading of a batch's small launches;
+                    // bit 9 (plan time): spread single-matrix plans (round-2 rule, A/B);
                     // bit 8: long rows by the separate fixup kernel
 };
 

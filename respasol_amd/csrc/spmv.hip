@@ -47,6 +47,7 @@
 namespace RSP_KNS {
 
 using rsp::kSpmvThreads;
+using rsp::kSpmvHeavyMax;
 using rsp::SpmvArgs;
 using rsp::SpmvBlock;
 using rsp::SpmvLongRow;
@@ -282,33 +283,41 @@ __device__ __forceinline__ void stream_products_scalar(const int *__restrict__ c
 }
 
 // Rows [0, nrows) of a tile, L lanes per row, canonical 8-way order; the
-// row sum goes to sink(row, sum) (lane 0 of the row's group).
+// row sum goes to sink(row, sum) (lane 0 of the row's group). A row longer
+// than `heavy` entries (heavy > 0) is not summed here but listed in
+// hl[0 .. *hn) for reduce_heavy_rows.
 template <typename T, int L, int NTH, typename Sink>
 __device__ __forceinline__ void reduce_rows(const T *lds, const unsigned short *rp_lds, int nrows, int kb,
-                                            Sink sink) {
+                                            int heavy, int *hl, int *hn, Sink sink) {
     constexpr int NA = 8 / L;                  // partials held per lane
     constexpr int NG = NTH / L;                // row groups per pass
     const int tid = threadIdx.x;
     const int g = tid / L, lane = tid & (L - 1);
     for (int rr = g; rr - g < nrows; rr += NG) {  // same trip count for all groups
-        const bool active = rr < nrows;
+        bool active = rr < nrows;
         T acc[NA];
 #pragma unroll
         for (int t = 0; t < NA; ++t) acc[t] = T(0);
         if (active) {
-            // branch-free: every step issues its NA loads together (clamped
-            // into the row) and adds a product or +0 (exact: a partial that
-            // starts at +0 is never -0). A predicated load per product made the
-            // compiler wait on each one, so a 256-entry row in a tile of short
-            // rows held its workgroup ~8 us (scripts/percall_probe.py).
-            const int a1 = rp_lds[rr + 1] - kb, last = a1 - 1;
-            for (int base = rp_lds[rr] - kb + lane; base < a1; base += 8) {
-                T v[NA];
+            const int a0 = rp_lds[rr] - kb, a1 = rp_lds[rr + 1] - kb, last = a1 - 1;
+            if (heavy > 0 && a1 - a0 > heavy) {
+                active = false;
+                if (lane == 0) hl[atomicAdd(hn, 1)] = rr;
+            } else {
+                // branch-free: every step issues its NA loads together
+                // (clamped into the row) and adds a product or +0 (exact: a
+                // partial that starts at +0 is never -0). A predicated load
+                // per product made the compiler wait on each one, so a
+                // 256-entry row in a tile of short rows held its workgroup
+                // ~8 us (scripts/percall_probe.py).
+                for (int base = a0 + lane; base < a1; base += 8) {
+                    T v[NA];
 #pragma unroll
-                for (int t = 0; t < NA; ++t) v[t] = lds[min(base + t * L, last)];
+                    for (int t = 0; t < NA; ++t) v[t] = lds[min(base + t * L, last)];
 #pragma unroll
-                for (int t = 0; t < NA; ++t)  // partial (lane + t*L) of the row
-                    acc[t] += base + t * L < a1 ? v[t] : T(0);
+                    for (int t = 0; t < NA; ++t)  // partial (lane + t*L) of the row
+                        acc[t] += base + t * L < a1 ? v[t] : T(0);
+                }
             }
         }
         // tree stages whose pair offset (4, 2, 1) is a multiple of L: local
@@ -324,21 +333,56 @@ __device__ __forceinline__ void reduce_rows(const T *lds, const unsigned short *
     }
 }
 
-// lanes per row: power of two <= 8 such that each lane still sums >= 4
-// products of an average row and the groups fit the workgroup
-template <typename T, int NTH = kSpmvThreads, typename Sink>
-__device__ __forceinline__ void reduce_tile_rows(const T *lds, const unsigned short *rp_lds, int nrows,
-                                                 int nnzt, int kb, Sink sink) {
-    int L = 1;
-    while (L < 8 && 2 * L * nrows <= NTH && 8 * L * nrows <= nnzt) L <<= 1;
-    switch (L) {
-        case 1: reduce_rows<T, 1, NTH>(lds, rp_lds, nrows, kb, sink); break;
-        case 2: reduce_rows<T, 2, NTH>(lds, rp_lds, nrows, kb, sink); break;
-        case 4: reduce_rows<T, 4, NTH>(lds, rp_lds, nrows, kb, sink); break;
-        default: reduce_rows<T, 8, NTH>(lds, rp_lds, nrows, kb, sink); break;
+// The rows listed by reduce_rows (hl[0 .. hn)): eight lanes per row, lane j
+// summing partial j (products j, j+8, ... in order) four steps per round
+// (32 products, loads issued together), then the canonical tree over the
+// eight lanes — the same bits as any L. A tile's few 33–256-entry rows no
+// longer run one lane's 8-partial loop each while the rest of the tile idles.
+template <typename T, int NTH, typename Sink>
+__device__ __forceinline__ void reduce_heavy_rows(const T *lds, const unsigned short *rp_lds, int kb,
+                                                  const int *hl, int hn, Sink sink) {
+    constexpr int NG = NTH / 8;
+    const int tid = threadIdx.x;
+    const int g = tid >> 3, lane = tid & 7;
+    for (int h = g; h - g < hn; h += NG) {  // same trip count for all groups
+        const bool active = h < hn;
+        T acc = T(0);
+        const int rr = active ? hl[h] : 0;
+        if (active) {
+            const int a1 = rp_lds[rr + 1] - kb, last = a1 - 1;
+            for (int base = rp_lds[rr] - kb + lane; base < a1; base += 32) {
+                T v[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) v[t] = lds[min(base + 8 * t, last)];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc += base + 8 * t < a1 ? v[t] : T(0);
+            }
+        }
+#pragma unroll
+        for (int off = 4; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+        if (active && lane == 0) sink(rr, acc);
     }
 }
 
+// lanes per row: power of two <= 8 such that each lane still sums >= 4
+// products of an average row and the groups fit the workgroup; with L < 8,
+// rows longer than 32 L entries go to reduce_heavy_rows after a barrier
+// (hl: kSpmvHeavyMax ints of LDS, *hn zeroed before the tile's first barrier)
+template <typename T, int NTH = kSpmvThreads, typename Sink>
+__device__ __forceinline__ void reduce_tile_rows(const T *lds, const unsigned short *rp_lds, int nrows,
+                                                 int nnzt, int kb, int *hl, int *hn, Sink sink) {
+    int L = 1;
+    while (L < 8 && 2 * L * nrows <= NTH && 8 * L * nrows <= nnzt) L <<= 1;
+    switch (L) {
+        case 1: reduce_rows<T, 1, NTH>(lds, rp_lds, nrows, kb, 32, hl, hn, sink); break;
+        case 2: reduce_rows<T, 2, NTH>(lds, rp_lds, nrows, kb, 64, hl, hn, sink); break;
+        case 4: reduce_rows<T, 4, NTH>(lds, rp_lds, nrows, kb, 128, hl, hn, sink); break;
+        default: reduce_rows<T, 8, NTH>(lds, rp_lds, nrows, kb, 0, hl, hn, sink); return;
+    }
+    lds_barrier();
+    const int n = *hn;  // workgroup-uniform
+    if (n > 0) reduce_heavy_rows<T, NTH>(lds, rp_lds, kb, hl, n, sink);
+}
 
 // A long row (or one tile-sized chunk of it) in LDS slots [a, e): thread t
 // sums slots a+t, a+t+256, ... in order, each wave combines its 64 sums with
@@ -426,7 +470,7 @@ __device__ __forceinline__ void spmv_tile(
     const unsigned short *__restrict__ cidx, const int *__restrict__ runs, int cbase, int cmax,
     const T *__restrict__ vals, const T *__restrict__ x, T *__restrict__ y,
     T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, T *lds,
-    T *wsum, unsigned short *rp_lds, int fuse) {
+    T *wsum, unsigned short *rp_lds, int *hl, int fuse) {
     constexpr int VW = 16 / sizeof(T);
     constexpr int RPQ = (SpmvTile<T>::kMaxRows + kSpmvThreads) / kSpmvThreads;
     const int tid = threadIdx.x;
@@ -481,6 +525,7 @@ __device__ __forceinline__ void spmv_tile(
         const int i = tid + q * kSpmvThreads;
         if (i <= nrows) rp_lds[i] = (unsigned short)(rpv[q] - kb);  // < kSlots + kVec
     }
+    if (tid == 0) hl[0] = 0;  // the tile's heavy-row count (reduce_tile_rows)
     lds_barrier();
 
     if (blk.r1 < 0) {  // a long row: written whole, or a chunk partial for the fixup
@@ -500,7 +545,7 @@ __device__ __forceinline__ void spmv_tile(
     }
 
     const int r0 = blk.r0;
-    reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, 0, [&](int rr, T sum) {
+    reduce_tile_rows<T>(lds, rp_lds, nrows, k1 - k0, 0, hl + 1, hl, [&](int rr, T sum) {
         T out = alpha * sum;
         if (BETA) out += beta * y[r0 + rr];
         // fp64: non-temporal y stores (the y lines leave L2 as a stream;
@@ -526,10 +571,11 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles(
     int cmax, T *partials, T alpha, T beta, int beta_nonzero, int nnz, int vector_ok, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
+    __shared__ int hl[1 + kSpmvHeavyMax];  // heavy rows of the tile: count, list
     __shared__ unsigned short rp_lds[SpmvTile<T>::kMaxRows + 2];  // row offsets - kb
     const int b = xcd_swizzle(blockIdx.x, nblocks);
     spmv_tile<T, NT, BETA>(blocks[b], rowptr, colidx, cidx, runs, cbases[b], cmax, vals, x, y,
-                           partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds,
+                           partials, alpha, beta, beta_nonzero, nnz, vector_ok, lds, wsum, rp_lds, hl,
                            fuse);
 }
 
@@ -577,6 +623,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     const int *__restrict__ cbases, SpmvBatchTable at, T alpha, T beta, int fuse) {
     __shared__ __attribute__((aligned(16))) T lds[SpmvTile<T>::kSlots];
     __shared__ T wsum[kSpmvThreads / 64];
+    __shared__ int hl[1 + kSpmvHeavyMax];  // heavy rows of the tile: count, list
     __shared__ unsigned short rp_lds[SpmvTile<T>::kMaxRows + 2];  // row offsets - kb
     const int b = blockIdx.x;
     // lo / hi selected inside the compare chain on the kernel arguments
@@ -599,7 +646,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_tiles_batch(
     spmv_tile<T, NT, BETA>(tiles[t], e.rowptr, e.colidx, e.cidx, e.runs, cbases[t], e.cmax,
                            (const T *)e.vals, (const T *)e.x,
                            (T *)e.y, (T *)e.partials, alpha, beta, BETA, e.nnz, e.vector_ok, lds,
-                           wsum, rp_lds, fuse);
+                           wsum, rp_lds, hl, fuse);
 }
 
 template <typename T>

@@ -137,8 +137,9 @@ def spmv_bound(rowptr, colidx, vals, x, eps):
     """|dy_i| <= (len_i + 2) * eps * sum_j |a_ij x_j|."""
     rp = np.asarray(rowptr, np.int64)
     lens = np.diff(rp)
-    absprod = np.abs(np.asarray(vals, np.float64)) * np.abs(np.asarray(x, np.float64)[colidx])
-    rowsum = np.add.reduceat(absprod, rp[:-1]) if absprod.size else np.zeros(len(lens))
+    absprod = np.abs(np.asarray(vals, np.float64)[:rp[-1]]) * np.abs(np.asarray(x, np.float64)[colidx[:rp[-1]]])
+    # a trailing 0 keeps reduceat's indices in range when the last rows are empty
+    rowsum = np.add.reduceat(np.append(absprod, 0.0), rp[:-1]) if len(lens) else np.zeros(0)
     rowsum = np.where(lens > 0, rowsum, 0.0)
     return (lens + 2) * eps * rowsum
 

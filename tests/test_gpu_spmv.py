@@ -144,6 +144,29 @@ def test_long_row_tickets_repeat(handle):
         assert same_bits(mat.spmv(xd).cpu().numpy(), canon)
 
 
+@pytest.mark.parametrize("pattern", ["random_mix", "alt_1_33", "alt_1_65", "alt_3_129", "alt_2_256"])
+def test_heavy_rows_in_short_row_tiles(handle, pattern):
+    """Rows of 33-256 entries packed into tiles of short rows are summed by
+    the tile's second, eight-lanes-per-row pass (reduce_heavy_rows): the same
+    canonical bits as every other row, with up to ~120 such rows in one fp32
+    tile (alternating 1- and 33-entry rows) and at every lanes-per-row width."""
+    rng = np.random.default_rng(sum(map(ord, pattern)))
+    n = 30000
+    if pattern == "random_mix":
+        lens = np.where(rng.random(n) < 0.1, rng.integers(17, 257, n), rng.choice([0, 1, 2, 3, 5, 8], n))
+    else:
+        a, b = (int(t) for t in pattern.split("_")[1:])
+        lens = np.where(np.arange(n) % 2 == 0, a, b)
+    cols = [np.sort(rng.choice(n, int(k), replace=False)).astype(np.int32) for k in lens]
+    rp = np.zeros(n + 1, np.int32)
+    np.cumsum(lens, out=rp[1:])
+    ci = np.concatenate(cols)
+    A = csr.CsrMatrix(0, n, n, len(ci), rp, ci, rng.uniform(-1, 1, len(ci)))
+    x = rng.uniform(-1, 1, n)
+    for dt in (torch.float64, torch.float32):
+        check(A, x, dt, handle)
+
+
 def test_single_dense_row_and_column(handle):
     n = 10000
     rows = [np.arange(n, dtype=np.int32)]  # row 0 dense
