@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variants", default="orig,short,band,shortband")
+    ap.add_argument("--floor", action="store_true",
+                    help="also time a one-element kernel and device copies of 4-64 MB the same way")
     ap.add_argument("--spmv-variants", default="0", help="RSP_SPMV_VARIANT per handle (16: no spreading)")
     args = ap.parse_args()
     hs = {}
@@ -77,6 +79,27 @@ def main():
         hs[v] = Handle()
     kinds = args.variants.split(",")
     rows = []
+    if args.floor:
+        def timed(fn):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ts = []
+            for _ in range(args.rounds):
+                fn()
+                e0.record()
+                for _ in range(args.reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3 / args.reps)
+            return statistics.median(ts)
+        one = torch.zeros(1, device="cuda")
+        print(f"floor one-element add_   {timed(lambda: one.add_(1.0)):7.2f} us", flush=True)
+        for mb in (4, 8, 16, 32, 64):
+            src = torch.empty(mb << 19, dtype=torch.uint8, device="cuda")  # read mb/2 + write mb/2
+            dst = torch.empty_like(src)
+            t = timed(lambda: dst.copy_(src))
+            print(f"floor copy {mb:3d} MB moved   {t:7.2f} us {mb * (1 << 20) / t / 1e6:6.2f} TB/s", flush=True)
+            del src, dst
     for name in args.names.split(","):
         A = csr.surrogate(name)
         x = torch.from_numpy(csr.dlarnv(1, [0, 0, 0, 1], A.n)[0]).cuda()
