@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 4: staged-tile tuning A/B on the bench step (batched, big set; then the
+# Env-knob A/B on the bench step (batched, big set; then the
 # moderate set): "name:ENV=... " specs, interleaved rounds.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/${1:-r4tune}; shift
+O=gpurun_out/${1:-benchab}; shift
 mkdir -p "$O"
 export TMPDIR=/tmp
 for wl in ${WORKLOADS:-big}; do

@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$PWD
-O=$ROOT/gpurun_out/${1:-r4pc}
+O=$ROOT/gpurun_out/${1:-percall}
 mkdir -p "$O"
 export TMPDIR=/tmp
 cd /tmp

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round 4 profiling session 1: the headline roofline evidence (fp64 + fp32),
+# Profiling session (tag argument): the headline roofline evidence (fp64 + fp32),
 # the moderate-set HBM traffic and the random-band counters.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$PWD
 export TMPDIR=/tmp
-T=${1:-r04}
-bash scripts/profile_round.sh $T || exit 1
+T=${1:-r05}
+[ "${SKIP_ROUND:-0}" = 1 ] || bash scripts/profile_round.sh $T || exit 1
 O=$ROOT/gpurun_out/${T}m
 mkdir -p "$O"
 cd /tmp
