@@ -1076,15 +1076,18 @@ rsp_status_t plan_validate(int n, const int *rpp, const int *cip, IluHostPlan &h
 static void split_terms(const int *rp, const int *ci, IluHostPlan &hp) {
     const int n = hp.n;
     const hvec<int> &dpos = hp.dpos, &lv = hp.lev_l, &lvt = hp.lev_lt;
+    if (!hp.split) {  // the reference's order: every term "late", none moved. Left
+        // empty (identity order, no early terms: the consumers treat an empty
+        // lpos / ne as that) instead of materialised: the fill was 1-4 ms of
+        // the level phase on the 1 M-row patterns (round 5)
+        hp.lpos.clear();
+        hp.ne_l.clear();
+        hp.ne_lt.clear();
+        return;
+    }
     hp.lpos.assign((size_t)std::max(hp.nnz_s, 1), 0);
     hp.ne_l.assign((size_t)std::max(n, 1), 0);
     hp.ne_lt.assign((size_t)std::max(n, 1), 0);
-    if (!hp.split) {  // the reference's order: every term "late", none moved
-        pfor(std::max(hp.nnz_s, 1), 1 << 16, [&](long long a, long long b) {
-            for (long long p = a; p < b; p++) hp.lpos[(size_t)p] = (int)p;
-        });
-        return;
-    }
     parallel_rows(n, [&](int r0, int r1) {
         hvec<int> late, late_c;
         for (int i = r0; i < r1; i++) {
@@ -1133,6 +1136,8 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
     // the L^T levels; each level set then grouped (counting sort).
     // levels of the lower DAG (factor + L solve): the longest path ending at
     // each row (each row needs its producers')
+    const double t0 = now_ms();
+    double t_l = 0, t_lt = 0, t_tr = 0;  // diagnostics (RSP_ILU_TIMING >= 3): each pass's wall time
     Task tl([&] {
         hvec<int> &lv = hp.lev_l;
         lv.assign((size_t)n, 0);
@@ -1144,6 +1149,7 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
             nl = std::max(nl, l + 1);
         }
         group_levels(lv, nl, hp.L.ptr, hp.L.rows);
+        t_l = now_ms() - t0;
     });
     // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
     Task tt([&] {
@@ -1158,27 +1164,70 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
             }
         }
         group_levels(lvt, nlt, hp.LT.ptr, hp.LT.rows);
+        t_lt = now_ms() - t0;
     });
-    // transposed strict lower: row k lists (j, pos) for l_jk, j descending
+    // transposed strict lower: row k lists (j, pos) for l_jk, j descending.
+    // Rows in parallel: counts and slots by relaxed atomics, then each
+    // column's slots sorted by j (descending; one entry per j, so the order
+    // is unique whatever the interleaving). Round 5: the sequential form was
+    // the level phase's longest pass (tmt_unsym 9.4 ms against 4.4 / 4.6 ms
+    // for the two level passes).
     hvec<int> &ltp = hp.ltp, &lts = hp.lts, &ltc = hp.ltc;
     ltp.assign((size_t)n + 1, 0);
-    for (int j = 0; j < n; j++)
-        for (int p = rp[j]; p < dpos[(size_t)j]; p++) ltp[(size_t)ci[p] + 1]++;
+    parallel_rows(n, [&](int r0, int r1) {
+        for (int j = r0; j < r1; j++)
+            for (int p = rp[j]; p < dpos[(size_t)j]; p++) __atomic_fetch_add(&ltp[(size_t)ci[p] + 1], 1, __ATOMIC_RELAXED);
+    });
     for (int k = 0; k < n; k++) ltp[(size_t)k + 1] += ltp[(size_t)k];
     lts.resize((size_t)ltp[(size_t)n]);
     ltc.resize((size_t)ltp[(size_t)n]);
     {
         hvec<int> fill(ltp.begin(), ltp.end() - 1);
-        for (int j = n - 1; j >= 0; j--)
-            for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
-                const int slot = fill[(size_t)ci[p]]++;
-                lts[(size_t)slot] = p;
-                ltc[(size_t)slot] = j;
-            }
+        parallel_rows(n, [&](int r0, int r1) {
+            for (int j = r0; j < r1; j++)
+                for (int p = rp[j]; p < dpos[(size_t)j]; p++) {
+                    const int slot = __atomic_fetch_add(&fill[(size_t)ci[p]], 1, __ATOMIC_RELAXED);
+                    lts[(size_t)slot] = p;
+                    ltc[(size_t)slot] = j;
+                }
+        });
     }
+    parallel_rows(n, [&](int k0, int k1) {
+        std::vector<std::pair<int, int>> tmp;
+        for (int k = k0; k < k1; k++) {
+            const int a = ltp[(size_t)k], b = ltp[(size_t)k + 1];
+            if (b - a <= 32) {  // insertion sort, j descending
+                for (int x = a + 1; x < b; x++) {
+                    const int cj = ltc[(size_t)x], cp = lts[(size_t)x];
+                    int y = x - 1;
+                    for (; y >= a && ltc[(size_t)y] < cj; y--) {
+                        ltc[(size_t)y + 1] = ltc[(size_t)y];
+                        lts[(size_t)y + 1] = lts[(size_t)y];
+                    }
+                    ltc[(size_t)y + 1] = cj;
+                    lts[(size_t)y + 1] = cp;
+                }
+            } else {
+                tmp.resize((size_t)(b - a));
+                for (int x = a; x < b; x++) tmp[(size_t)(x - a)] = {ltc[(size_t)x], lts[(size_t)x]};
+                std::sort(tmp.begin(), tmp.end(), [](const std::pair<int, int> &u, const std::pair<int, int> &v) {
+                    return u.first > v.first;
+                });
+                for (int x = a; x < b; x++) {
+                    ltc[(size_t)x] = tmp[(size_t)(x - a)].first;
+                    lts[(size_t)x] = tmp[(size_t)(x - a)].second;
+                }
+            }
+        }
+    });
+    t_tr = now_ms() - t0;
     tl.join();
     tt.join();
+    const double t_j = now_ms() - t0;
     split_terms(rp, ci, hp);
+    if (env_int("RSP_ILU_TIMING", 0) >= 3)
+        fprintf(stderr, "rsp_ilu0_analysis n=%d     levels: L %.2f LT %.2f transpose %.2f joined %.2f split %.2f ms\n",
+                n, t_l, t_lt, t_tr, t_j, now_ms() - t0 - t_j);
 }
 
 rsp_status_t plan_symbolic(const int *rpp, const int *cip, IluHostPlan &hp) {
@@ -1245,8 +1294,9 @@ static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool
     hp.L.group = g_env ? (g_env == 2 ? 2 : 4) : group_of(cnt_l);
     hp.LT.group = g_env ? (g_env == 2 ? 2 : 4) : group_of(cnt_lt);
     // split term order (IluHostPlan::lpos): early terms first
-    auto ne_l = [&](int i) { return hp.ne_l[(size_t)i]; };
-    auto ne_lt = [&](int i) { return hp.ne_lt[(size_t)i]; };
+    // (empty: the reference's order, split_terms)
+    auto ne_l = [&](int i) { return hp.ne_l.empty() ? 0 : hp.ne_l[(size_t)i]; };
+    auto ne_lt = [&](int i) { return hp.ne_lt.empty() ? 0 : hp.ne_lt[(size_t)i]; };
     // the two DAGs' plans (flat terms in level order, thin-run chunks, y
     // sources) are independent: built concurrently
     Task tl([&] {
@@ -1255,7 +1305,7 @@ static void plan_solves_impl(const int *rp, const int *ci, IluHostPlan &hp, bool
             if (terms_on_host)
                 solve_plan_terms(n, hp.L.ptr, hp.L.group, [&](int i, auto emit) {
                     for (int o = rp[(size_t)i]; o < dpos[(size_t)i]; o++) {
-                        const int p = hp.lpos[(size_t)o];
+                        const int p = hp.lpos.empty() ? o : hp.lpos[(size_t)o];
                         emit(p, ci[(size_t)p]);
                     }
                 }, ne_l, hp.L.sp);

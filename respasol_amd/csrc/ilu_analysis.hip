@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256) void st_rows(rsp_k::SolveTermsArgs a) {
     const int i = t.i;
     int j0;
     const int cnt = st_row_terms(a, i, &j0);
-    const int ne = a.kind == 2 ? 0 : a.ne[i], g = a.group;
+    const int ne = a.kind == 2 || !a.ne ? 0 : a.ne[i], g = a.group;  // no ne / lpos: the reference's order
     const int lo = t.t1 - t.t0 == st_split_padded(ne, cnt, g) ? (ne + g - 1) / g * g : ne;
     const int tend = x + 1 < a.nx ? a.tasks[x + 1].t0 : a.total;
     for (int q = lane; q < tend - t.t0; q += 64) {
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(256) void st_rows(rsp_k::SolveTermsArgs a) {
         int tp = -1, c = rsp::kPadSrc;
         if (o >= 0) {
             const int j = j0 + o;
-            tp = a.kind == 0 ? a.lpos[j] : a.lts[j];
+            tp = a.kind == 0 ? (a.lpos ? a.lpos[j] : j) : a.lts[j];
             c = a.kind == 0 ? a.ci[tp] : a.ltc[j];
         }
         a.tpos[k] = tp;
@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256) void st_fill(rsp_k::SolveTermsArgs a) {
     for (int x = ch.x0 + (int)threadIdx.x; x < ch.x1; x += 256) {
         const rsp::RowTask t = a.tasks[x];
         int j0;
-        const int cnt = st_row_terms(a, t.i, &j0), ne = a.kind == 2 ? 0 : a.ne[t.i];
+        const int cnt = st_row_terms(a, t.i, &j0), ne = a.kind == 2 || !a.ne ? 0 : a.ne[t.i];
         const int eg = t.t1 - t.t0 == st_split_padded(ne, cnt, G) ? (ne + G - 1) / G : 0;  // early groups
         a.trow[x] = rsp::ThinRowPlan{(t.t0 - ch.k0) / G | ((t.t1 - t.t0) / G) << 16,
                                      ((x - base) & (rsp::kYWin - 1)) | eg << 16, t.i, t.d};

@@ -1386,7 +1386,18 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
         t_last = t;
     };
     rsp_an::hvec<int> dev_rows, long_rows;
-    for (int i = 0; i < n; i++) (rp[(size_t)i + 1] - rp[(size_t)i] <= kAnDevRow ? dev_rows : long_rows).push_back(i);
+    for (int i = 0; i < n; i++)
+        if (rp[(size_t)i + 1] - rp[(size_t)i] > kAnDevRow) long_rows.push_back(i);
+    dev_rows.resize((size_t)(n - (int)long_rows.size()));
+    if (long_rows.empty()) {  // every row (FEM / stencil patterns): 0 .. n-1 in parallel
+        rsp_an::parallel_for(n, 1 << 16, [&](long long a, long long b) {
+            for (long long i = a; i < b; i++) dev_rows[(size_t)i] = (int)i;
+        });
+    } else {
+        size_t w = 0;
+        for (int i = 0; i < n; i++)
+            if (rp[(size_t)i + 1] - rp[(size_t)i] <= kAnDevRow) dev_rows[w++] = i;
+    }
     // The host level pass needs only the pattern: download it first, check it
     // (columns in range, rows strictly increasing: the device check below
     // returns the same verdict), take the diagonal positions from it and run
@@ -1664,13 +1675,17 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
         tl.kind = 0;
         tl.rp = d_row_offsets;
         tl.ci = d_col_ind;
-        ar.up((int **)&tl.lpos, hp->lpos);  // the split term order (rsp_an::split_terms)
-        ar.up((int **)&tl.ne, hp->ne_l);
+        // the split term order (rsp_an::split_terms); none (nullptr) for the
+        // reference's order
+        if (!hp->lpos.empty()) {
+            ar.up((int **)&tl.lpos, hp->lpos);
+            ar.up((int **)&tl.ne, hp->ne_l);
+            ar.up((int **)&tt.ne, hp->ne_lt);
+        }
         tt.kind = 1;
         ar.up((int **)&tt.ltp, hp->ltp);
         ar.up((int **)&tt.lts, hp->lts);
         ar.up((int **)&tt.ltc, hp->ltc);
-        ar.up((int **)&tt.ne, hp->ne_lt);
     } else {
         dag_upload(ar, f->L, hp->L);
         dag_upload(ar, f->LT, hp->LT);
