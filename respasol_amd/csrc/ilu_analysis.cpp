@@ -643,8 +643,10 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
     const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
     const long long piece_items = std::max(1, env_int("RSP_ILU_PIECE_ITEMS", kRndPieceItems));
     const int nnz = rp[(size_t)n];
+    const double t0 = now_ms();
     hvec<long long> litems;
     const hvec<char> lthin = factor_thin_levels(rp, sym.upd_ptr, ptr, rows, thin_rows, &litems);
+    const double t_thin = now_ms() - t0;
     // pairs of position p of thin row i (packed, see IluSymbolic::pair_base)
     auto pair_off = [&](int i) {
         return sym.pair_base.empty() ? 0 : sym.pair_base[(size_t)i] - sym.upd_ptr[(size_t)rp[(size_t)i]];
@@ -678,6 +680,7 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
         pieces.push_back({s, lb, sg.le, FacPlan()});
     }
     hvec<unsigned long long> where((size_t)std::max(nnz, 1), 0ull);
+    const double t_where = now_ms() - t0;
     auto wload = [&](int q) { return __atomic_load_n(&where[(size_t)q], __ATOMIC_RELAXED); };
     pfor_dyn((int)pieces.size(), nnz, 1 << 15, [&](int pi) {
         Piece &pc = pieces[(size_t)pi];
@@ -720,14 +723,24 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
             ch.r1 = (int)o.rounds.size();
             o.chunks[(size_t)c] = ch;
         };
+        // this item's not-yet-staged operands (fresh), looked up by a second
+        // epoch-stamped hash: an item of a hub row has up to kRndItemPairs
+        // pairs, and a linear search of its fresh list was quadratic in them
+        constexpr int kF = 4 * rsp::kRndItemPairs;  // >= 2 x the 2 kRndItemPairs operands
+        hvec<int> fkey(kF), fval(kF), fep(kF, 0);
+        int fepoch = 0;
         auto ref = [&](int q, hvec<int> &fresh) {
             const unsigned long long w = wload(q), wk = w >> 12;
             if (wk == ckey) return (int)(w & 0xfff);
             if (c > 0 && wk == ckey - 1) return K + (int)(w & 0xfff);
             const int st = hfind(q);
             if (st >= 0) return 2 * K + st;
-            for (size_t f = 0; f < fresh.size(); f++)
-                if (fresh[f] == q) return 2 * K + (int)(nstg + f);
+            int h = (int)(((unsigned)q * 2654435761u) >> 20) & (kF - 1);
+            for (; fep[(size_t)h] == fepoch; h = (h + 1) & (kF - 1))
+                if (fkey[(size_t)h] == q) return 2 * K + (int)(nstg + fval[(size_t)h]);
+            fep[(size_t)h] = fepoch;
+            fkey[(size_t)h] = q;
+            fval[(size_t)h] = (int)fresh.size();
             fresh.push_back(q);
             return 2 * K + (int)(nstg + fresh.size() - 1);
         };
@@ -766,6 +779,7 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
                 const bool lower = p < dpos[(size_t)i];
                 for (int attempt = 0; attempt < 2; attempt++) {
                     fresh.clear();
+                    fepoch++;
                     ipairs.clear();
                     const int po = pair_off(i);
                     for (int u = sym.upd_ptr[(size_t)p]; u < sym.upd_ptr[(size_t)p + 1]; u++) {
@@ -809,6 +823,7 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
         }
         close_chunk();
     });
+    const double t_pieces = now_ms() - t0;
     // join: pieces in order, an empty chunk between two pieces of a segment
     fp.chunks.clear();
     fp.items.clear();
@@ -851,6 +866,9 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
     for (hvec<int> *v : {&fp.pairs, &fp.staged, &fp.rounds})
         if (v->empty()) v->push_back(0);
     if (fp.chunks.empty()) fp.chunks.push_back(rsp::RndChunk{});
+    if (env_int("RSP_ILU_TIMING", 0) >= 3)
+        fprintf(stderr, "rsp_ilu0_analysis n=%d     factor plan: thin levels %.2f where %.2f pieces (%zu) %.2f join %.2f ms\n",
+                n, t_thin, t_where, pieces.size(), t_pieces, now_ms() - t0);
 }
 
 // Symbolic ILU(0): the update list of every position (see IluArgs) and the
