@@ -633,7 +633,7 @@ hvec<int> factor_thin_rows(const int *rp, const IluHostPlan &hp) {
 // piece is writing concurrently (never its own chunk or the one before) only
 // ever gets "not here" — the relaxed atomics make those reads well defined.
 // The staged positions of the current chunk sit in a piece-private hash.
-static constexpr int kRndPieceItems = 1 << 16;  // A/B (scripts/piece_ab.sh): 2^17 / 2^16 / 2^15 gave factor 58.58 / 58.58 / 58.73 ms, circuits plan faster with smaller pieces
+static constexpr int kRndPieceItems = 1 << 16;  // the largest piece (round 4 A/B: 2^17 / 2^16 / 2^15 gave factor 58.58 / 58.58 / 58.73 ms); see build_factor_plan
 
 static void build_factor_plan(int n, const int *rp, const int *ci,
                               const hvec<int> &dpos, const hvec<int> &hasdiag,
@@ -641,12 +641,23 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
                               const hvec<int> &rows, int thin_rows, FacPlan &fp) {
     const int nlev = (int)ptr.size() - 1;
     const int K = rsp::kRndItems, S = rsp::kRndStaged, kZero = 2 * rsp::kRndItems + rsp::kRndStaged;
-    const long long piece_items = std::max(1, env_int("RSP_ILU_PIECE_ITEMS", kRndPieceItems));
     const int nnz = rp[(size_t)n];
     const double t0 = now_ms();
     hvec<long long> litems;
     const hvec<char> lthin = factor_thin_levels(rp, sym.upd_ptr, ptr, rows, thin_rows, &litems);
     const double t_thin = now_ms() - t0;
+    // piece size: about 1/32 of the thin positions, within [2^15, 2^16] — a
+    // function of the pattern only, so the plan is the same on every host
+    // (round 5: a fixed 2^16 left the circuits' 7-13 pieces, ~120 ns per
+    // position each, as the analysis' longest step; each extra piece adds an
+    // empty chunk to the factor, ~1.5 us: a 2^14 floor gave config-3 analysis
+    // -15 ms for +0.6 % on the circuits' factor, profiles/r05_piece_ab.txt)
+    long long thin_total = 0;
+    for (int l = 0; l < nlev; l++)
+        if (lthin[(size_t)l]) thin_total += litems[(size_t)l];
+    const long long piece_items = std::max(
+        1LL, (long long)env_int("RSP_ILU_PIECE_ITEMS",
+                                (int)std::min<long long>(kRndPieceItems, std::max<long long>(1 << 15, thin_total / 32))));
     // pairs of position p of thin row i (packed, see IluSymbolic::pair_base)
     auto pair_off = [&](int i) {
         return sym.pair_base.empty() ? 0 : sym.pair_base[(size_t)i] - sym.upd_ptr[(size_t)rp[(size_t)i]];
