@@ -135,6 +135,28 @@ struct rsp_ilu0_info {
     unsigned long long digest = 0;  // rsp_an::digest of the host plan
     std::unique_ptr<rsp_an::IluHostPlan> host;  // kept for the U plan
     rsp_an::hvec<int> host_rp, host_ci;
+    // Recovery of a call whose flow wait gave up (a co-running kernel kept
+    // some of the flow launch's workgroups from being scheduled past the
+    // give-up bound): rsp_ilu0_zero_pivot / rsp_trsv_zero_pivot re-run it
+    // without flow launches (every level its own launch: no co-residency
+    // needed), from the factor's input values — copied before every factor
+    // that has flow runs — or the solve's unchanged x. RSP_ILU_FLOW_RECOVER=0
+    // reports EXECUTION_FAILED instead (the round-4 behaviour).
+    void *d_fbackup = nullptr;
+    size_t fbackup_bytes = 0;
+    struct FacCall {
+        int valid = 0;
+        rsp_datatype_t type = RSP_R_64F;
+        void *vals = nullptr;
+    } last_fac;
+    struct SolveCall {
+        int valid = 0;
+        rsp_operation_t op = RSP_OPERATION_NON_TRANSPOSE;
+        double alpha = 1.0;
+        rsp_datatype_t type = RSP_R_64F;
+        const void *vals = nullptr, *x = nullptr;
+        void *y = nullptr;
+    } last_solve[3];
 };
 
 #define RSP_CHECK_HIP(call)                                                     \
@@ -1144,6 +1166,11 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     if (f->d_arena_pairs) (void)hipFree(f->d_arena_pairs);
     f->d_arena_sym = f->d_arena_pairs = nullptr;
     if (f->d_fslots) (void)hipFree(f->d_fslots);
+    if (f->d_fbackup) (void)hipFree(f->d_fbackup);
+    f->d_fbackup = nullptr;
+    f->fbackup_bytes = 0;
+    f->last_fac = rsp_ilu0_info::FacCall();
+    for (rsp_ilu0_info::SolveCall &c : f->last_solve) c = rsp_ilu0_info::SolveCall();
     f->d_arena = f->d_arena_u = nullptr;
     f->d_usval = nullptr;
     f->d_fslots = nullptr;
@@ -1884,6 +1911,17 @@ rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t f, int *levels_lower, int *levels_u
     return RSP_STATUS_SUCCESS;
 }
 
+// the recovery runs (rsp_ilu0_info::d_fbackup / last_solve), defined below
+static bool flow_recover();
+static rsp_status_t ilu_factor_run(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type, void *d_values,
+                                   bool flow_ok);
+static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op, const void *alpha,
+                                             rsp_ilu0_info_t f, rsp_datatype_t value_type, const void *d_values,
+                                             const void *d_x, void *d_y, bool flow_ok);
+static rsp_status_t rsp_trsv_upper_impl(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f,
+                                        rsp_datatype_t value_type, const void *d_values, const void *d_x, void *d_y,
+                                        bool flow_ok);
+
 rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *position) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     if (!f || !position) return RSP_STATUS_INVALID_VALUE;
@@ -1893,8 +1931,20 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
     int z[2] = {INT_MAX, 0};  // zero pivot, give-up generation of the factor calls
     RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
     RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
-    // the last factor's flow wait gave up: its values are wrong
-    if (f->factored && f->fac_gen > 0 && z[1] == f->fac_gen) return RSP_STATUS_EXECUTION_FAILED;
+    // the last factor's flow wait gave up: its values are wrong. Recovered
+    // (rsp_ilu0_info::d_fbackup): the input values restored, the factor run
+    // again without flow launches; else reported.
+    if (f->factored && f->fac_gen > 0 && z[1] == f->fac_gen) {
+        if (!f->last_fac.valid || !flow_recover()) return RSP_STATUS_EXECUTION_FAILED;
+        f->last_fac.valid = 0;
+        RSP_CHECK_HIP(hipMemcpyAsync(f->last_fac.vals, f->d_fbackup, (size_t)f->nnz_s * elem_size(f->last_fac.type),
+                                     hipMemcpyDeviceToDevice, h->stream));
+        const rsp_status_t st = ilu_factor_run(h, f, f->last_fac.type, f->last_fac.vals, false);
+        if (st != RSP_STATUS_SUCCESS) return st;
+        RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+        if (z[1] == f->fac_gen) return RSP_STATUS_EXECUTION_FAILED;
+    }
     if (f->factored && z[0] != INT_MAX && (pos < 0 || z[0] < pos)) pos = z[0];
     if (pos >= 0) {
         *position = pos;
@@ -1917,7 +1967,20 @@ rsp_status_t rsp_trsv_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int which, i
     RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
     RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
     const int g = f->solve_gen[which];
-    if (g > 0 && z[2 + which] == g) return RSP_STATUS_EXECUTION_FAILED;
+    if (g > 0 && z[2 + which] == g) {  // recovered: the solve run again without flow launches
+        const rsp_ilu0_info::SolveCall c = f->last_solve[which];
+        if (!c.valid || !flow_recover()) return RSP_STATUS_EXECUTION_FAILED;
+        const double a64 = c.alpha;
+        const float a32 = (float)c.alpha;
+        const void *al = c.type == RSP_R_64F ? (const void *)&a64 : (const void *)&a32;
+        const rsp_status_t st =
+            which == RSP_TRSV_U ? rsp_trsv_upper_impl(h, al, f, c.type, c.vals, c.x, c.y, false)
+                                : rsp_trsv_lower_unit_impl(h, c.op, al, f, c.type, c.vals, c.x, c.y, false);
+        if (st != RSP_STATUS_SUCCESS) return st;
+        RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
+        RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
+        if (z[2 + which] == f->solve_gen[which]) return RSP_STATUS_EXECUTION_FAILED;
+    }
     if (which == RSP_TRSV_U) {
         int pos = f->structural_zero;
         if (f->factored && z[0] != INT_MAX && (pos < 0 || z[0] < pos)) pos = z[0];
@@ -1972,11 +2035,12 @@ static rsp::LevelPlan level_plan(const rsp_ilu0_info::Dag &d, const rsp_an::hvec
     return p;
 }
 
-static rsp_status_t rsp_ilu0_factor_impl(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
-                             void *d_values) {
-    if (!h) return RSP_STATUS_NOT_INITIALIZED;
-    if (!f || !f->analysed || (f->nnz_s > 0 && !d_values)) return RSP_STATUS_INVALID_VALUE;
-    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+static bool flow_recover() { return env_int("RSP_ILU_FLOW_RECOVER", 1) != 0; }
+
+// One factor call (flow_ok = false: no flow launch, every fat level its own
+// launch — the recovery run of rsp_ilu0_zero_pivot).
+static rsp_status_t ilu_factor_run(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
+                                   void *d_values, bool flow_ok) {
     RSP_CHECK_HIP(hipMemsetD32Async(f->d_zero, INT_MAX, 1, h->stream));
     rsp::IluArgs a;
     a.n = f->n;
@@ -2015,7 +2079,7 @@ static rsp_status_t rsp_ilu0_factor_impl(rsp_handle_t h, rsp_ilu0_info_t f, rsp_
         f->fac_gen = 0;
     }
     a.gen = ++f->fac_gen;
-    a.flow = env_int("RSP_ILU_FLOW", 1) != 0;
+    a.flow = flow_ok && env_int("RSP_ILU_FLOW", 1) != 0;
     a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 4), 4), 16) / 4;
     a.flow_cus = h->num_cus;
     a.flow_sleep = std::min(std::max(env_int("RSP_ILU_FLOW_SLEEP", 1), 1), 64);
@@ -2054,6 +2118,33 @@ static rsp_status_t rsp_ilu0_factor_impl(rsp_handle_t h, rsp_ilu0_info_t f, rsp_
     }
     f->factored = 1;
     return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+}
+
+static rsp_status_t rsp_ilu0_factor_impl(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
+                             void *d_values) {
+    if (!h) return RSP_STATUS_NOT_INITIALIZED;
+    if (!f || !f->analysed || (f->nnz_s > 0 && !d_values)) return RSP_STATUS_INVALID_VALUE;
+    if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
+    // a factor with flow runs keeps its input values for a recovery run
+    // (rsp_ilu0_info::d_fbackup): one device copy of the values per call
+    f->last_fac.valid = 0;
+    const bool flows = !f->fruns.empty() && f->d_fslots && env_int("RSP_ILU_FLOW", 1) != 0 &&
+                       env_int("RSP_ILU_FAT_SLOT", 1) != 0;
+    if (flows && f->nnz_s > 0 && flow_recover()) {
+        const size_t bytes = (size_t)f->nnz_s * elem_size(value_type);
+        if (f->fbackup_bytes < bytes) {
+            if (f->d_fbackup) (void)hipFree(f->d_fbackup);
+            f->d_fbackup = nullptr;
+            f->fbackup_bytes = 0;
+            RSP_CHECK_HIP(hipMalloc(&f->d_fbackup, bytes));
+            f->fbackup_bytes = bytes;
+        }
+        RSP_CHECK_HIP(hipMemcpyAsync(f->d_fbackup, d_values, bytes, hipMemcpyDeviceToDevice, h->stream));
+        f->last_fac.valid = 1;
+        f->last_fac.type = value_type;
+        f->last_fac.vals = d_values;
+    }
+    return ilu_factor_run(h, f, value_type, d_values, true);
 }
 
 static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alpha, rsp_datatype_t t,
@@ -2103,14 +2194,32 @@ static hipError_t trsv_begin(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp::T
     return hipSuccess;
 }
 
+// A solve call's arguments, kept for its recovery run (rsp_ilu0_info::last_solve).
+static void remember_solve(rsp_ilu0_info *f, int which, rsp_operation_t op, const void *alpha, rsp_datatype_t t,
+                           const void *vals, const void *x, void *y) {
+    rsp_ilu0_info::SolveCall &c = f->last_solve[which];
+    c.valid = 1;
+    c.op = op;
+    c.alpha = t == RSP_R_64F ? *(const double *)alpha : (double)*(const float *)alpha;
+    c.type = t;
+    c.vals = vals;
+    c.x = x;
+    c.y = y;
+}
+
+// flow_ok = false: the recovery run of rsp_trsv_zero_pivot (no flow launch)
 static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                  rsp_ilu0_info_t f, rsp_datatype_t value_type,
-                                 const void *d_values, const void *d_x, void *d_y) {
+                                 const void *d_values, const void *d_x, void *d_y, bool flow_ok) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     if (!f || !f->analysed || !alpha) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
+    if (op != RSP_OPERATION_NON_TRANSPOSE && op != RSP_OPERATION_TRANSPOSE) return RSP_STATUS_INVALID_VALUE;
+    remember_solve(f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, op, alpha, value_type, d_values,
+                   d_x, d_y);
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
+    a.flow = a.flow && flow_ok;
     // diagnostics: RSP_ILU_TRACE=<file> appends per-chunk timestamps of the
     // prefetching thin kernel (host-blocking; never set in timed runs)
     const char *trace_file = getenv("RSP_ILU_TRACE");
@@ -2160,14 +2269,16 @@ static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op,
 
 static rsp_status_t rsp_trsv_upper_impl(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f,
                             rsp_datatype_t value_type, const void *d_values, const void *d_x,
-                            void *d_y) {
+                            void *d_y, bool flow_ok) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     if (!f || !f->analysed || !alpha) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     rsp_status_t st = ilu_plan_u(h, f);  // planned on first use
     if (st != RSP_STATUS_SUCCESS) return st;
+    remember_solve(f, RSP_TRSV_U, RSP_OPERATION_NON_TRANSPOSE, alpha, value_type, d_values, d_x, d_y);
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
+    a.flow = a.flow && flow_ok;
     a.plan = level_plan(f->U, f->U.segs, f->U.batch);
     a.sval = f->d_usval;
     RSP_CHECK_HIP(trsv_begin(h, f, RSP_TRSV_U, a));
@@ -2250,13 +2361,13 @@ rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t v
 rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void *alpha,
                                  rsp_ilu0_info_t f, rsp_datatype_t value_type,
                                  const void *d_values, const void *d_x, void *d_y) {
-    return guarded([&] { return rsp_trsv_lower_unit_impl(h, op, alpha, f, value_type, d_values, d_x, d_y); }, [] {});
+    return guarded([&] { return rsp_trsv_lower_unit_impl(h, op, alpha, f, value_type, d_values, d_x, d_y, true); }, [] {});
 }
 
 rsp_status_t rsp_trsv_upper(rsp_handle_t h, const void *alpha, rsp_ilu0_info_t f,
                             rsp_datatype_t value_type, const void *d_values, const void *d_x,
                             void *d_y) {
-    return guarded([&] { return rsp_trsv_upper_impl(h, alpha, f, value_type, d_values, d_x, d_y); }, [] {});
+    return guarded([&] { return rsp_trsv_upper_impl(h, alpha, f, value_type, d_values, d_x, d_y, true); }, [] {});
 }
 
 rsp_status_t rsp_spmv_plan_host(int m, const int *row_offsets, const int *col_ind, int64_t nnz,

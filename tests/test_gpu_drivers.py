@@ -305,12 +305,17 @@ def test_halo_direct_layout_single_gpu(P):
 def test_ilu0_driver_flow_give_up_exits_nonzero():
     """test_ilu0 treats a failed factor / solve as an error (exit 1), also on
     the reference call sequence: a flow wait forced to give up
-    (RSP_ILU_FLOW_TIMEOUT_US=0, every level fat) is caught by the zero-pivot
-    check after the factor; the same matrix with the normal bound runs clean."""
+    (RSP_ILU_FLOW_TIMEOUT_US=0, every level fat) with recovery off
+    (RSP_ILU_FLOW_RECOVER=0) is caught by the zero-pivot check after the
+    factor; with recovery on (default) the zero-pivot check re-runs the call
+    without flow launches and the driver succeeds; the normal bound runs clean."""
     env = dict(os.environ, RSP_ILU_THIN_FACTOR="0", RSP_ILU_THIN_SOLVE="0")
     exe = os.path.join(BIN, "test_ilu0")
     r = subprocess.run([exe, "surrogate:G2_circuit@0.1"], capture_output=True, text=True, timeout=300,
-                       env=dict(env, RSP_ILU_FLOW_TIMEOUT_US="0"))
+                       env=dict(env, RSP_ILU_FLOW_TIMEOUT_US="0", RSP_ILU_FLOW_RECOVER="0"))
     assert r.returncode == 1 and "RSP_STATUS_EXECUTION_FAILED" in r.stderr, (r.returncode, r.stderr)
+    r = subprocess.run([exe, "surrogate:G2_circuit@0.1"], capture_output=True, text=True, timeout=300,
+                       env=dict(env, RSP_ILU_FLOW_TIMEOUT_US="0"))
+    assert r.returncode == 0 and "Solve = " in r.stdout, r.stderr
     r = subprocess.run([exe, "surrogate:G2_circuit@0.1"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "Solve = " in r.stdout, r.stderr

@@ -440,12 +440,14 @@ def test_flow_segments(handle, monkeypatch, flow, wpc, mode, name, scale):
 
 def test_flow_give_up_is_reported(handle, monkeypatch):
     """A persistent (flow) launch whose dependency wait gives up is reported,
-    not silent: forced with a zero wait bound
+    not silent, when recovery is off
+    (RSP_ILU_FLOW_RECOVER=0): forced with a zero wait bound
     (RSP_ILU_FLOW_TIMEOUT_US=0) and every level fat, so every level is in a
     flow run. The factor's zero_pivot and the solves' status then raise
     EXECUTION_FAILED; the next call with the normal bound starts clean,
     reports SUCCESS and gives the oracle's bits."""
     from respasol_amd._lib import STATUS_EXECUTION_FAILED, RspError
+    monkeypatch.setenv("RSP_ILU_FLOW_RECOVER", "0")
     monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
     monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
     A = csr.surrogate("G2_circuit", 0.1)
@@ -476,5 +478,89 @@ def test_flow_give_up_is_reported(handle, monkeypatch):
     assert il.solve_zero_pivot(il.TRSV_LT) == -1
     _, _, _, rz, ry = oracle_ilu(A, torch.float64)
     rv, _, _ = ob.ilu0(A.rowptr, A.colidx, A.values)
+    assert np.array_equal(va.cpu().numpy(), rv)
+    assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_flow_give_up_is_recovered(handle, monkeypatch, dtype):
+    """The same forced give-ups with recovery on (the default): the zero-pivot
+    calls restore the factor's input values (copied before every factor with
+    flow runs) or keep the solve's x, re-run the call without flow launches,
+    report SUCCESS, and the results are the oracle's bits."""
+    monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
+    monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
+    monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", "0")
+    A = csr.surrogate("G2_circuit", 0.1)
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values, dtype)
+    il = Ilu0(handle, rp, ci, nnz=A.nnz)
+    il.analysis()
+    ones = torch.ones(A.n, dtype=dtype, device="cuda")
+    il.factor(va)
+    assert il.zero_pivot() == -1
+    z = il.solve_lower(va, ones)
+    assert il.solve_zero_pivot(il.TRSV_L) == -1
+    y = il.solve_lower(va, z, transpose=True)
+    assert il.solve_zero_pivot(il.TRSV_LT) == -1
+    rv, _, _, rz, ry = oracle_ilu(A, dtype)
+    assert np.array_equal(va.cpu().numpy(), rv)
+    assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)
+
+
+TESTKIT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "respasol_amd", "lib",
+                       "librsp_testkit.so")
+
+
+@pytest.mark.parametrize("hog_us,bound_us,recover", [(50000, 200000, 1), (100000, 5000, 1), (100000, 5000, 0)])
+def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us, recover):
+    """the factor and both solves (default schedule, flow runs
+    included) beside a kernel on another stream that holds all but 8 CUs —
+    one 1024-thread workgroup per CU with the CU's whole LDS, bounded by the
+    wall clock (librsp_testkit.so, test-only). (Half the CUs is not enough to
+    matter: a flow grid of one 4-wave workgroup per CU fits, several per CU,
+    on the free half, so nothing waits.) A 50 ms occupant inside the
+    give-up bound: the flow waves wait, then SUCCESS and the oracle's bits. A
+    100 ms occupant past a 5 ms bound: the waits give up; with recovery the
+    zero-pivot calls re-run the calls without flow launches (SUCCESS, the
+    oracle's bits), without it the factor reports EXECUTION_FAILED — which
+    shows the occupant really kept flow workgroups off the CUs."""
+    import ctypes
+    import time
+    from respasol_amd._lib import STATUS_EXECUTION_FAILED, RspError
+    tk = ctypes.CDLL(TESTKIT)
+    tk.rsp_testkit_occupy.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong]
+    monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", str(bound_us))
+    monkeypatch.setenv("RSP_ILU_FLOW_RECOVER", str(recover))
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    main, side = torch.cuda.Stream(), torch.cuda.Stream()
+    h = Handle(stream=main)
+    A = csr.surrogate("offshore", 0.2)
+    with torch.cuda.stream(main):
+        rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
+        il = Ilu0(h, rp, ci, nnz=A.nnz)
+        il.analysis()
+        ones = torch.ones(A.n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    assert tk.rsp_testkit_occupy(side.cuda_stream, ncu - 8, hog_us) == 0
+    time.sleep(0.002)  # the occupant is resident before the factor's launches
+    with torch.cuda.stream(main):
+        il.factor(va)
+        if not recover:
+            with pytest.raises(RspError) as e:
+                il.zero_pivot()
+            assert e.value.status == STATUS_EXECUTION_FAILED
+            torch.cuda.synchronize()
+            return
+        assert il.zero_pivot() == -1
+    torch.cuda.synchronize()
+    assert tk.rsp_testkit_occupy(side.cuda_stream, ncu - 8, hog_us) == 0
+    time.sleep(0.002)
+    with torch.cuda.stream(main):
+        z = il.solve_lower(va, ones)
+        assert il.solve_zero_pivot(il.TRSV_L) == -1
+        y = il.solve_lower(va, z, transpose=True)
+        assert il.solve_zero_pivot(il.TRSV_LT) == -1
+    torch.cuda.synchronize()
+    rv, _, _, rz, ry = oracle_ilu(A, torch.float64)
     assert np.array_equal(va.cpu().numpy(), rv)
     assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)
