@@ -166,16 +166,21 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t handle, int n, int nnz, const int *d
  * structurally missing (after analysis) or U(j,j) == 0 (after the numeric
  * factorisation); the smallest such j is reported. Otherwise SUCCESS, -1. */
 rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t handle, rsp_ilu0_info_t info, int *position);
-/* Also RSP_STATUS_EXECUTION_FAILED after a factor whose persistent (flow)
- * launch gave up a dependency wait (bounded by RSP_ILU_FLOW_TIMEOUT_US,
- * default 0.2 s; never expected): its values are wrong. Reported for the
- * LAST factor call only (each call starts clean). */
+/* A factor whose persistent (flow) launch gave up a dependency wait (bounded
+ * by RSP_ILU_FLOW_TIMEOUT_US, default 0.2 s: only when another kernel keeps
+ * the launch's workgroups off the CUs that long) is RECOVERED here: its
+ * input values (kept by the factor call) are restored, the factor runs again
+ * without flow launches — and so does every solve made after it — and the
+ * call reports as usual. RSP_STATUS_EXECUTION_FAILED only when recovery is
+ * off (RSP_ILU_FLOW_RECOVER=0) or fails. About the LAST factor call only. */
 
 /* cusparseXcsrsv2_zeroPivot (the csrsv2 infos of GPU/ilu0.cu:143-150) for
  * the solves below; which = RSP_TRSV_L (op N), RSP_TRSV_LT (op T) or
  * RSP_TRSV_U (rsp_trsv_upper). Host-blocking. Reports on the LAST solve of
- * that kind: RSP_STATUS_EXECUTION_FAILED if its flow launch gave up a wait
- * (its y is wrong); for RSP_TRSV_U, ZERO_PIVOT + *position as
+ * that kind. If its flow launch gave up a wait, the solve (its x is
+ * unchanged: x != y) and every solve made after it are run again without
+ * flow launches first; RSP_STATUS_EXECUTION_FAILED only with
+ * RSP_ILU_FLOW_RECOVER=0. For RSP_TRSV_U, ZERO_PIVOT + *position as
  * rsp_ilu0_zero_pivot (U divides by u_jj); else SUCCESS, -1. */
 #define RSP_TRSV_L 0
 #define RSP_TRSV_LT 1

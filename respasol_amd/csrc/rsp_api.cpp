@@ -142,14 +142,20 @@ struct rsp_ilu0_info {
     // needed), from the factor's input values — copied before every factor
     // that has flow runs — or the solve's unchanged x. RSP_ILU_FLOW_RECOVER=0
     // reports EXECUTION_FAILED instead (the round-4 behaviour).
+    // A recovered call's output feeds the calls made after it (the L^T solve
+    // reads the L solve's y; a solve reads the factor's values), so those are
+    // re-run too, in call order (seq).
     void *d_fbackup = nullptr;
     size_t fbackup_bytes = 0;
+    long long call_seq = 0;
     struct FacCall {
+        long long seq = 0;
         int valid = 0;
         rsp_datatype_t type = RSP_R_64F;
         void *vals = nullptr;
     } last_fac;
     struct SolveCall {
+        long long seq = 0;
         int valid = 0;
         rsp_operation_t op = RSP_OPERATION_NON_TRANSPOSE;
         double alpha = 1.0;
@@ -1922,6 +1928,37 @@ static rsp_status_t rsp_trsv_upper_impl(rsp_handle_t h, const void *alpha, rsp_i
                                         rsp_datatype_t value_type, const void *d_values, const void *d_x, void *d_y,
                                         bool flow_ok);
 
+// Re-run one recorded solve without flow launches (rsp_ilu0_info::last_solve).
+static rsp_status_t rerun_solve(rsp_handle_t h, rsp_ilu0_info *f, int which) {
+    const rsp_ilu0_info::SolveCall c = f->last_solve[which];
+    const double a64 = c.alpha;
+    const float a32 = (float)c.alpha;
+    const void *al = c.type == RSP_R_64F ? (const void *)&a64 : (const void *)&a32;
+    return which == RSP_TRSV_U ? rsp_trsv_upper_impl(h, al, f, c.type, c.vals, c.x, c.y, false)
+                               : rsp_trsv_lower_unit_impl(h, c.op, al, f, c.type, c.vals, c.x, c.y, false);
+}
+
+// The recorded solves made after call `seq`, in call order (their inputs
+// came from the call being recovered).
+struct LaterSolves {
+    int w[3];
+    int k = 0;
+};
+static LaterSolves later_solves(const rsp_ilu0_info *f, long long seq) {
+    LaterSolves l;
+    for (int w = 0; w < 3; w++)
+        if (f->last_solve[w].valid && f->last_solve[w].seq > seq) l.w[l.k++] = w;
+    std::sort(l.w, l.w + l.k, [&](int a, int b) { return f->last_solve[a].seq < f->last_solve[b].seq; });
+    return l;
+}
+static rsp_status_t rerun_solves(rsp_handle_t h, rsp_ilu0_info *f, const LaterSolves &l) {
+    for (int j = 0; j < l.k; j++) {
+        const rsp_status_t st = rerun_solve(h, f, l.w[j]);
+        if (st != RSP_STATUS_SUCCESS) return st;
+    }
+    return RSP_STATUS_SUCCESS;
+}
+
 rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *position) {
     if (!h) return RSP_STATUS_NOT_INITIALIZED;
     if (!f || !position) return RSP_STATUS_INVALID_VALUE;
@@ -1939,7 +1976,9 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
         f->last_fac.valid = 0;
         RSP_CHECK_HIP(hipMemcpyAsync(f->last_fac.vals, f->d_fbackup, (size_t)f->nnz_s * elem_size(f->last_fac.type),
                                      hipMemcpyDeviceToDevice, h->stream));
-        const rsp_status_t st = ilu_factor_run(h, f, f->last_fac.type, f->last_fac.vals, false);
+        const LaterSolves later = later_solves(f, f->last_fac.seq);
+        rsp_status_t st = ilu_factor_run(h, f, f->last_fac.type, f->last_fac.vals, false);
+        if (st == RSP_STATUS_SUCCESS) st = rerun_solves(h, f, later);
         if (st != RSP_STATUS_SUCCESS) return st;
         RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
         RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
@@ -1967,15 +2006,11 @@ rsp_status_t rsp_trsv_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int which, i
     RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
     RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
     const int g = f->solve_gen[which];
-    if (g > 0 && z[2 + which] == g) {  // recovered: the solve run again without flow launches
-        const rsp_ilu0_info::SolveCall c = f->last_solve[which];
-        if (!c.valid || !flow_recover()) return RSP_STATUS_EXECUTION_FAILED;
-        const double a64 = c.alpha;
-        const float a32 = (float)c.alpha;
-        const void *al = c.type == RSP_R_64F ? (const void *)&a64 : (const void *)&a32;
-        const rsp_status_t st =
-            which == RSP_TRSV_U ? rsp_trsv_upper_impl(h, al, f, c.type, c.vals, c.x, c.y, false)
-                                : rsp_trsv_lower_unit_impl(h, c.op, al, f, c.type, c.vals, c.x, c.y, false);
+    if (g > 0 && z[2 + which] == g) {  // recovered: the solve (and the solves after it) run again
+        if (!f->last_solve[which].valid || !flow_recover()) return RSP_STATUS_EXECUTION_FAILED;
+        const LaterSolves later = later_solves(f, f->last_solve[which].seq);
+        rsp_status_t st = rerun_solve(h, f, which);
+        if (st == RSP_STATUS_SUCCESS) st = rerun_solves(h, f, later);
         if (st != RSP_STATUS_SUCCESS) return st;
         RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
         RSP_CHECK_HIP(hipStreamSynchronize(h->stream));
@@ -2141,6 +2176,7 @@ static rsp_status_t rsp_ilu0_factor_impl(rsp_handle_t h, rsp_ilu0_info_t f, rsp_
         }
         RSP_CHECK_HIP(hipMemcpyAsync(f->d_fbackup, d_values, bytes, hipMemcpyDeviceToDevice, h->stream));
         f->last_fac.valid = 1;
+        f->last_fac.seq = ++f->call_seq;
         f->last_fac.type = value_type;
         f->last_fac.vals = d_values;
     }
@@ -2198,6 +2234,7 @@ static hipError_t trsv_begin(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp::T
 static void remember_solve(rsp_ilu0_info *f, int which, rsp_operation_t op, const void *alpha, rsp_datatype_t t,
                            const void *vals, const void *x, void *y) {
     rsp_ilu0_info::SolveCall &c = f->last_solve[which];
+    c.seq = ++f->call_seq;
     c.valid = 1;
     c.op = op;
     c.alpha = t == RSP_R_64F ? *(const double *)alpha : (double)*(const float *)alpha;

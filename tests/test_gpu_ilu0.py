@@ -486,8 +486,9 @@ def test_flow_give_up_is_reported(handle, monkeypatch):
 def test_flow_give_up_is_recovered(handle, monkeypatch, dtype):
     """The same forced give-ups with recovery on (the default): the zero-pivot
     calls restore the factor's input values (copied before every factor with
-    flow runs) or keep the solve's x, re-run the call without flow launches,
-    report SUCCESS, and the results are the oracle's bits."""
+    flow runs) or keep the solve's x, re-run the call — and every solve made
+    after it, whose input it produced — without flow launches, report
+    SUCCESS, and the results are the oracle's bits."""
     monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
     monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
     monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", "0")
@@ -498,9 +499,11 @@ def test_flow_give_up_is_recovered(handle, monkeypatch, dtype):
     ones = torch.ones(A.n, dtype=dtype, device="cuda")
     il.factor(va)
     assert il.zero_pivot() == -1
+    # the reference's order: both solves, then their status (GPU/ilu0.cu:284-310):
+    # recovering L re-runs the L^T solve that read L's y
     z = il.solve_lower(va, ones)
-    assert il.solve_zero_pivot(il.TRSV_L) == -1
     y = il.solve_lower(va, z, transpose=True)
+    assert il.solve_zero_pivot(il.TRSV_L) == -1
     assert il.solve_zero_pivot(il.TRSV_LT) == -1
     rv, _, _, rz, ry = oracle_ilu(A, dtype)
     assert np.array_equal(va.cpu().numpy(), rv)
@@ -555,10 +558,10 @@ def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us,
     torch.cuda.synchronize()
     assert tk.rsp_testkit_occupy(side.cuda_stream, ncu - 8, hog_us) == 0
     time.sleep(0.002)
-    with torch.cuda.stream(main):
+    with torch.cuda.stream(main):  # both solves, then their status (the L^T solve reads L's y)
         z = il.solve_lower(va, ones)
-        assert il.solve_zero_pivot(il.TRSV_L) == -1
         y = il.solve_lower(va, z, transpose=True)
+        assert il.solve_zero_pivot(il.TRSV_L) == -1
         assert il.solve_zero_pivot(il.TRSV_LT) == -1
     torch.cuda.synchronize()
     rv, _, _, rz, ry = oracle_ilu(A, torch.float64)
