@@ -285,21 +285,25 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
     const int nlev = (int)ptr.size() - 1;
     const long long nx = (long long)rows.size();
     constexpr long long kGrain = 1 << 14;
+    const bool tm = env_int("RSP_ILU_TIMING", 0) >= 4;  // diagnostics: sub-steps
+    double tq = now_ms();
+    auto step = [&](const char *what) {
+        if (!tm) return;
+        const double t = now_ms();
+        fprintf(stderr, "rsp_ilu0_analysis n=%d       solve rows %-10s %6.2f ms\n", n, what, t - tq);
+        tq = t;
+    };
     hvec<int> order(rows);
-    hvec<int> nt_row((size_t)n, 0), ne_row((size_t)n, 0);
-    pfor(n, kGrain, [&](long long a, long long b) {
-        for (long long i = a; i < b; i++) {
-            nt_row[(size_t)i] = row_count((int)i);
-            ne_row[(size_t)i] = row_early((int)i);
-        }
-    });
-    auto padded_row = [&](int i) { return split_padded(ne_row[(size_t)i], nt_row[(size_t)i], group); };
+    // (row_count / row_early are O(1) lookups: called where needed, not
+    // copied into per-row arrays first)
+    auto padded_row = [&](int i) { return split_padded(row_early(i), row_count(i), group); };
     hvec<int> lpad((size_t)std::max(nlev, 1), 0);
     pfor_dyn(nlev, nx, kGrain, [&](int l) {
         int t = 0;
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) t += padded_row(order[(size_t)x]);
         lpad[(size_t)l] = t;
     });
+    step("counts");
     // RSP_ILU_THIN_TERMS: tuning knob (a thin level's padded terms, <= kChunkTerms)
     const int thin_terms = std::min(env_int("RSP_ILU_THIN_TERMS", rsp::kThinSolveTerms), rsp::kChunkTerms);
     sp.segs.clear();
@@ -315,6 +319,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
     hvec<char> thin_lev((size_t)std::max(nlev, 1), 0);
     for (const rsp::LevelSeg &sg : sp.segs)
         for (int l = sg.lb; l < sg.le; l++) thin_lev[(size_t)l] = (char)sg.thin;
+    step("segs");
     // within each level (stable): short rows, then wave rows, then (fat
     // levels) hub rows
     const int fat_long = env_int("RSP_ILU_FAT_LONG", rsp::kFatLongDefault);
@@ -326,7 +331,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
         const int b = ptr[(size_t)l], e = ptr[(size_t)l + 1];
         int c[3] = {0, 0, 0};
         auto cls = [&](int i) {
-            const int t = nt_row[(size_t)i];
+            const int t = row_count(i);
             return t <= lim ? 0 : (thin_lev[(size_t)l] || t <= hub ? 1 : 2);
         };
         for (int x = b; x < e; x++) c[cls(order[(size_t)x])]++;
@@ -337,6 +342,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
         int w[3] = {b, b + c[0], b + c[0] + c[1]};
         for (int i : tmp) order[(size_t)w[cls(i)]++] = i;
     });
+    step("classes");
     // flat term ranges in level order: a thin row's terms padded to whole
     // groups; a padded fat level's short rows own kFatLongTerms terms each
     const bool pad_fat = fat_long == rsp::kFatLongTerms && env_int("RSP_ILU_FAT_PAD", 1) != 0;
@@ -346,12 +352,13 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
     pfor_dyn(nlev, nx, kGrain, [&](int l) {
         const bool padl = pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0;
         for (int x = ptr[(size_t)l]; x < ptr[(size_t)l + 1]; x++) {
-            const int i = order[(size_t)x], t = nt_row[(size_t)i];
+            const int i = order[(size_t)x], t = row_count(i);
             const int t1 = thin_lev[(size_t)l] ? padded_row(i) : t;
             len[(size_t)x] = padl && x - ptr[(size_t)l] < sp.nshort[(size_t)l] ? std::max(t1, rsp::kFatLongTerms) : t1;
             sp.tasks[(size_t)x].t1 = t1;  // length for now
         }
     });
+    step("lengths");
     long long total = 0;
     for (long long x = 0; x < nx; x++) {
         sp.tasks[(size_t)x].t0 = (int)total;
@@ -360,6 +367,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
     for (int l = 0; l < nlev; l++)
         if (pad_fat && !thin_lev[(size_t)l] && sp.nshort[(size_t)l] > 0) sp.sbase[(size_t)l] = sp.tasks[(size_t)ptr[(size_t)l]].t0;
     sp.nterm = total;
+    step("prefix");
     pfor(nx, kGrain, [&](long long a, long long b) {
         for (long long x = a; x < b; x++) {
             rsp::RowTask &t = sp.tasks[(size_t)x];
@@ -368,6 +376,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
             t.d = diag.empty() ? -1 : diag[(size_t)t.i];
         }
     });
+    step("tasks");
     // flow segments: fat segments of two or more levels run as one persistent
     // launch (trsv_flow) over work items in level order — a level's short rows
     // in groups of 64 (a lane each), then its wave and hub rows (a wave each).
@@ -403,6 +412,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
                 n, nlev, group, nthin, lthin, nfat, lfat, nflow, lflow, sp.fitems.size());
     }
     if (sp.fitems.empty()) sp.fitems.push_back({0, 0, -1, -1});
+    step("flow");
     hvec<int> lterms((size_t)std::max(nlev, 1), 0);
     for (int l = 0; l < nlev; l++)
         if (ptr[(size_t)l + 1] > ptr[(size_t)l])
@@ -443,6 +453,7 @@ static void solve_plan_rows(int n, const hvec<int> &ptr, const hvec<int> &rows,
         sp.chunks.push_back({0, 0, 0, 0, 0, 0, 0, 0});
         sp.cbase.push_back(0);
     }
+    step("chunks");
 }
 
 // row_terms(i, emit) calls emit(tpos, col) for the terms of row i in order
