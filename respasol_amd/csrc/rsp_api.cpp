@@ -1443,9 +1443,14 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     }
     sub("D2H pattern");
     {
-        std::atomic<int> bad{0};
+        // (and the diagonal flags and the structural zero: the device rows
+        // kernel below computes the same arrays for the device, so nothing of
+        // it is read back — round 5: two synchronisations fewer per analysis)
+        std::atomic<int> bad{0}, szero{INT_MAX};
         hp.dpos.resize((size_t)n);
+        hp.hasdiag.resize((size_t)n);
         rsp_an::parallel_for(n, 1 << 14, [&](long long r0, long long r1) {
+            int sz = INT_MAX;
             for (long long i = r0; i < r1; i++) {
                 const int a = rp[(size_t)i], b = rp[(size_t)i + 1];
                 int d = b, prev = -1;
@@ -1456,9 +1461,15 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
                     prev = c;
                 }
                 hp.dpos[(size_t)i] = d;
+                const int hd = d < b && ci[(size_t)d] == (int)i ? 1 : 0;
+                hp.hasdiag[(size_t)i] = hd;
+                if (!hd && sz == INT_MAX) sz = (int)i;
+            }
+            for (int cur = szero.load(); sz < cur && !szero.compare_exchange_weak(cur, sz);) {
             }
         });
         if (bad.load()) return RSP_STATUS_INVALID_VALUE;  // a column out of range or a row not increasing
+        hp.structural_zero = szero.load() == INT_MAX ? -1 : szero.load();
     }
     sub("host check + dpos");
     rsp_an::Task levels([&] { rsp_an::plan_levels(rp.data(), ci.data(), hp); });
@@ -1481,23 +1492,13 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     ar.up(&d_rows, dev_rows);
     sub("arena");
     RSP_CHECK_HIP(ar.commit(&f->d_arena_sym, s));
-    const int flags0[2] = {0, INT_MAX};
-    int flags[2] = {0, INT_MAX};
-    RSP_CHECK_HIP(hipMemcpyAsync(d_flags, flags0, sizeof(flags0), hipMemcpyHostToDevice, s));
+    // the device's diagonal positions and flags (its validation flags are not
+    // read: the host check above gave the same verdict)
     RSP_CHECK_HIP(rsp_k::ilu_an_rows(n, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_flags, s));
-    RSP_CHECK_HIP(hipMemcpyAsync(flags, d_flags, sizeof(flags), hipMemcpyDeviceToHost, s));
-    RSP_CHECK_HIP(hipStreamSynchronize(s));
-    if (flags[0]) return RSP_STATUS_INVALID_VALUE;  // a column out of range or a row not increasing
-    sub("rows kernel + flags");
-    hp.structural_zero = flags[1] == INT_MAX ? -1 : flags[1];
     const int n_c[3] = {(int)dev_rows.size(), 0, 0};
     const int *rows_c[3] = {d_rows, nullptr, nullptr};
     RSP_CHECK_HIP(rsp_k::ilu_an_count(rows_c, n_c, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_cnt, d_scratch, s));
-    hp.hasdiag.resize((size_t)n);
-    if (n > 0)
-        RSP_CHECK_HIP(hipMemcpyAsync(hp.hasdiag.data(), f->d_hasdiag, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    RSP_CHECK_HIP(hipStreamSynchronize(s));
-    sub("count kernel + D2H hasdiag");
+    sub("rows + count kernels");
     // the long rows' counts on the host
     rsp_an::hvec<int> hcnt(long_rows.empty() ? 0 : (size_t)nnz_s);
     rsp_an::symbolic_rows(long_rows, n, rp.data(), ci.data(), hp.dpos.data(), hp.hasdiag.data(), hcnt.data(),
