@@ -151,12 +151,14 @@ struct rsp_ilu0_info {
     struct FacCall {
         long long seq = 0;
         int valid = 0;
+        int ftz = 0;  // the handle's FTZ mode at the call
         rsp_datatype_t type = RSP_R_64F;
         void *vals = nullptr;
     } last_fac;
     struct SolveCall {
         long long seq = 0;
         int valid = 0;
+        int ftz = 0;
         rsp_operation_t op = RSP_OPERATION_NON_TRANSPOSE;
         double alpha = 1.0;
         rsp_datatype_t type = RSP_R_64F;
@@ -1935,8 +1937,13 @@ static rsp_status_t rerun_solve(rsp_handle_t h, rsp_ilu0_info *f, int which) {
     const double a64 = c.alpha;
     const float a32 = (float)c.alpha;
     const void *al = c.type == RSP_R_64F ? (const void *)&a64 : (const void *)&a32;
-    return which == RSP_TRSV_U ? rsp_trsv_upper_impl(h, al, f, c.type, c.vals, c.x, c.y, false)
-                               : rsp_trsv_lower_unit_impl(h, c.op, al, f, c.type, c.vals, c.x, c.y, false);
+    const int ftz = h->ftz;
+    h->ftz = c.ftz;  // the mode of the call being re-run
+    const rsp_status_t st = which == RSP_TRSV_U
+                                ? rsp_trsv_upper_impl(h, al, f, c.type, c.vals, c.x, c.y, false)
+                                : rsp_trsv_lower_unit_impl(h, c.op, al, f, c.type, c.vals, c.x, c.y, false);
+    h->ftz = ftz;
+    return st;
 }
 
 // The recorded solves made after call `seq`, in call order (their inputs
@@ -1978,7 +1985,10 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
         RSP_CHECK_HIP(hipMemcpyAsync(f->last_fac.vals, f->d_fbackup, (size_t)f->nnz_s * elem_size(f->last_fac.type),
                                      hipMemcpyDeviceToDevice, h->stream));
         const LaterSolves later = later_solves(f, f->last_fac.seq);
+        const int ftz = h->ftz;
+        h->ftz = f->last_fac.ftz;  // the mode of the call being re-run
         rsp_status_t st = ilu_factor_run(h, f, f->last_fac.type, f->last_fac.vals, false);
+        h->ftz = ftz;
         if (st == RSP_STATUS_SUCCESS) st = rerun_solves(h, f, later);
         if (st != RSP_STATUS_SUCCESS) return st;
         RSP_CHECK_HIP(hipMemcpyAsync(z, f->d_zero, sizeof(z), hipMemcpyDeviceToHost, h->stream));
@@ -2178,6 +2188,7 @@ static rsp_status_t rsp_ilu0_factor_impl(rsp_handle_t h, rsp_ilu0_info_t f, rsp_
         RSP_CHECK_HIP(hipMemcpyAsync(f->d_fbackup, d_values, bytes, hipMemcpyDeviceToDevice, h->stream));
         f->last_fac.valid = 1;
         f->last_fac.seq = ++f->call_seq;
+        f->last_fac.ftz = h->ftz;
         f->last_fac.type = value_type;
         f->last_fac.vals = d_values;
     }
@@ -2232,11 +2243,12 @@ static hipError_t trsv_begin(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp::T
 }
 
 // A solve call's arguments, kept for its recovery run (rsp_ilu0_info::last_solve).
-static void remember_solve(rsp_ilu0_info *f, int which, rsp_operation_t op, const void *alpha, rsp_datatype_t t,
-                           const void *vals, const void *x, void *y) {
+static void remember_solve(rsp_handle_t h, rsp_ilu0_info *f, int which, rsp_operation_t op, const void *alpha,
+                           rsp_datatype_t t, const void *vals, const void *x, void *y) {
     rsp_ilu0_info::SolveCall &c = f->last_solve[which];
     c.seq = ++f->call_seq;
     c.valid = 1;
+    c.ftz = h->ftz;
     c.op = op;
     c.alpha = t == RSP_R_64F ? *(const double *)alpha : (double)*(const float *)alpha;
     c.type = t;
@@ -2254,8 +2266,8 @@ static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op,
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     if (op != RSP_OPERATION_NON_TRANSPOSE && op != RSP_OPERATION_TRANSPOSE) return RSP_STATUS_INVALID_VALUE;
-    remember_solve(f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, op, alpha, value_type, d_values,
-                   d_x, d_y);
+    remember_solve(h, f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, op, alpha, value_type,
+                   d_values, d_x, d_y);
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
     a.flow = a.flow && flow_ok;
     // diagnostics: RSP_ILU_TRACE=<file> appends per-chunk timestamps of the
@@ -2314,7 +2326,7 @@ static rsp_status_t rsp_trsv_upper_impl(rsp_handle_t h, const void *alpha, rsp_i
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     rsp_status_t st = ilu_plan_u(h, f);  // planned on first use
     if (st != RSP_STATUS_SUCCESS) return st;
-    remember_solve(f, RSP_TRSV_U, RSP_OPERATION_NON_TRANSPOSE, alpha, value_type, d_values, d_x, d_y);
+    remember_solve(h, f, RSP_TRSV_U, RSP_OPERATION_NON_TRANSPOSE, alpha, value_type, d_values, d_x, d_y);
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
     a.flow = a.flow && flow_ok;
     a.plan = level_plan(f->U, f->U.segs, f->U.batch);

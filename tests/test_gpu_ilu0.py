@@ -482,8 +482,8 @@ def test_flow_give_up_is_reported(handle, monkeypatch):
     assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)
 
 
-@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_flow_give_up_is_recovered(handle, monkeypatch, dtype):
+@pytest.mark.parametrize("dtype,ftz", [(torch.float64, False), (torch.float32, False), (torch.float32, True)])
+def test_flow_give_up_is_recovered(handle, monkeypatch, dtype, ftz):
     """The same forced give-ups with recovery on (the default): the zero-pivot
     calls restore the factor's input values (copied before every factor with
     flow runs) or keep the solve's x, re-run the call — and every solve made
@@ -497,15 +497,19 @@ def test_flow_give_up_is_recovered(handle, monkeypatch, dtype):
     il = Ilu0(handle, rp, ci, nnz=A.nnz)
     il.analysis()
     ones = torch.ones(A.n, dtype=dtype, device="cuda")
+    handle.set_ftz(ftz)
     il.factor(va)
+    handle.set_ftz(False)  # the recovery re-runs in the mode of the call, not the current one
     assert il.zero_pivot() == -1
+    handle.set_ftz(ftz)
     # the reference's order: both solves, then their status (GPU/ilu0.cu:284-310):
     # recovering L re-runs the L^T solve that read L's y
     z = il.solve_lower(va, ones)
     y = il.solve_lower(va, z, transpose=True)
+    handle.set_ftz(False)
     assert il.solve_zero_pivot(il.TRSV_L) == -1
     assert il.solve_zero_pivot(il.TRSV_LT) == -1
-    rv, _, _, rz, ry = oracle_ilu(A, dtype)
+    rv, _, _, rz, ry = oracle_ilu(A, dtype, ftz=ftz)
     assert np.array_equal(va.cpu().numpy(), rv)
     assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)
 
