@@ -209,6 +209,9 @@ __device__ __forceinline__ void lds_barrier() {
 // ms; dc1 4.86 -> 5.62). A narrow level is ~425 cycles (160 ns, dc1,
 // RSP_ILU_TRACE_CLK) and any extra LDS traffic or wake-up delay lands on it.
 // (Mode 1 was removed in round 4 with the other inline-asm ordering.)
+// 4 (round 5) = s_sleep between reads, ended early by the publishing wave's
+// s_wakeup: dc1 fp32 solve 4.16 -> 4.71 ms, the factor slower too
+// (profiles/r05_poll_wakeup_ab.txt).
 // The counter is published by lds_publish (release) and read here with an
 // acquire fence after the last poll: the HIP memory model orders a wave's y
 // stores before the counter and the waiting wave's y loads after it.
