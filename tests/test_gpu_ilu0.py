@@ -549,7 +549,7 @@ def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us,
         ones = torch.ones(A.n, dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
     assert tk.rsp_testkit_occupy(side.cuda_stream, ncu - 8, hog_us) == 0
-    time.sleep(0.002)  # the occupant is resident before the factor's launches
+    time.sleep(0.01)  # the occupant is resident before the factor's launches
     with torch.cuda.stream(main):
         il.factor(va)
         if not recover:
@@ -561,7 +561,7 @@ def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us,
         assert il.zero_pivot() == -1
     torch.cuda.synchronize()
     assert tk.rsp_testkit_occupy(side.cuda_stream, ncu - 8, hog_us) == 0
-    time.sleep(0.002)
+    time.sleep(0.01)
     with torch.cuda.stream(main):  # both solves, then their status (the L^T solve reads L's y)
         z = il.solve_lower(va, ones)
         y = il.solve_lower(va, z, transpose=True)
