@@ -232,15 +232,51 @@ static void pfor_dyn(int n, long long work, long long grain, F f) {
     Pool::get().run(n, nt, [&](int j) { f(j); });
 }
 
-// rows grouped by level (stable: ascending row within a level)
+// rows grouped by level (stable: ascending row within a level). A counting
+// sort; on large level sets with few levels per row block, in parallel: each
+// of T contiguous row blocks counts its levels, block t's rows of level v go
+// after those of blocks < t (the same order as the sequential pass).
 static void group_levels(const hvec<int> &lev, int nlev, hvec<int> &ptr,
                          hvec<int> &rows) {
+    const int n = (int)lev.size();
+    const int T = host_threads();
     ptr.assign((size_t)nlev + 1, 0);
-    for (int v : lev) ptr[(size_t)v + 1]++;
-    for (int l = 0; l < nlev; l++) ptr[(size_t)l + 1] += ptr[(size_t)l];
-    hvec<int> fill(ptr.begin(), ptr.end() - 1);
     rows.resize(lev.size());
-    for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
+    if (n < (1 << 16) || T < 2 || (long long)nlev * T > n) {
+        for (int v : lev) ptr[(size_t)v + 1]++;
+        for (int l = 0; l < nlev; l++) ptr[(size_t)l + 1] += ptr[(size_t)l];
+        hvec<int> fill(ptr.begin(), ptr.end() - 1);
+        for (size_t i = 0; i < lev.size(); i++) rows[(size_t)fill[(size_t)lev[i]]++] = (int)i;
+        return;
+    }
+    std::vector<int> cnt((size_t)T * nlev, 0);  // cnt[t * nlev + v]
+    auto block = [&](int t, int &a, int &b) {
+        a = (int)((long long)n * t / T);
+        b = (int)((long long)n * (t + 1) / T);
+    };
+    pfor_dyn(T, n, 1, [&](int t) {
+        int a, b;
+        block(t, a, b);
+        int *c = cnt.data() + (size_t)t * nlev;
+        for (int i = a; i < b; i++) c[lev[(size_t)i]]++;
+    });
+    // per level: its start, then each block's offset within it (level-major)
+    int run = 0;
+    for (int v = 0; v < nlev; v++) {
+        ptr[(size_t)v] = run;
+        for (int t = 0; t < T; t++) {
+            const int k = cnt[(size_t)t * nlev + v];
+            cnt[(size_t)t * nlev + v] = run;
+            run += k;
+        }
+    }
+    ptr[(size_t)nlev] = run;
+    pfor_dyn(T, n, 1, [&](int t) {
+        int a, b;
+        block(t, a, b);
+        int *c = cnt.data() + (size_t)t * nlev;
+        for (int i = a; i < b; i++) rows[(size_t)c[lev[(size_t)i]]++] = i;
+    });
 }
 
 // fma-chain batch for a mean chain length of total / count
