@@ -1692,6 +1692,15 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
         }
         f->digest = e == hipSuccess ? 1 : 0;  // computed once the solve terms exist (below)
     }
+    // (diagnostics, RSP_ILU_TIMING >= 3: the upload's steps)
+    auto t_up = std::chrono::steady_clock::now();
+    auto up_step = [&](const char *what) {
+        if (!tm3) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "rsp_ilu0_analysis n=%d     upload: %-16s %8.2f ms\n", n, what,
+                std::chrono::duration<double, std::milli>(t - t_up).count());
+        t_up = t;
+    };
     // everything in one device allocation
     Arena ar;
     ar.up(&f->d_rchunks, hp->fplan.chunks);
@@ -1738,12 +1747,15 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
         ar.up(&d_desc, hp->slot_desc);
         ar.up(&d_offs, hp->slot_offs);
     }
+    up_step("arena build");
     hipError_t e = ar.commit(&f->d_arena, h->stream);
+    up_step("commit (H2D)");
     if (e == hipSuccess && dev_terms) {
         tl.dpos = f->d_dpos;
         e = dag_build_terms(f->L, tl, h->stream);
         if (e == hipSuccess) e = dag_build_terms(f->LT, tt, h->stream);
     }
+    up_step("solve terms");
     if (e == hipSuccess && env_int("RSP_ILU_DIGEST", 0)) {  // tests only
         if (dev_terms) {
             e = dag_download_terms(f->L, tl, hp->L, h->stream);
@@ -1777,6 +1789,7 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
             es = rsp_k::ilu0_build_slots(a, d_desc, d_offs, (int)hp->slot_desc.size(), f->d_fslots, h->stream);
             if (es == hipSuccess) es = hipStreamSynchronize(h->stream);
         }
+        up_step("factor slots");
         if (es != hipSuccess) {
             (void)hipGetLastError();
             if (f->d_fslots) (void)hipFree(f->d_fslots);
