@@ -754,6 +754,46 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, un
     }
 }
 
+// The whole factor of a pattern without update pairs (IluArgs::fac_one: a
+// stored lower triangle): l_ik = a_ik / u_kk for every lower position, where
+// u_kk = a_kk is never updated, and the zero-pivot check of each diagonal; a
+// thread per row. Per position the division factor_row and row_lds_factor
+// make (no fma: the update lists are empty), the divisor read as they read
+// it (0 for a row without diagonal): the same bits. Diagonals are only read,
+// so the rows are independent. One launch instead of the L DAG's levels
+// (G2_circuit: 5 799) or of the one-level plan's per-row workgroups. A row
+// with more than kScaleRow lower entries (a circuit's hub row: thousands, a
+// serial chain of dependent gathers for one thread) is listed in LDS and
+// done by the whole workgroup after its short rows.
+template <typename T>
+__global__ __launch_bounds__(256) void ilu0_scale_lower(IluArgs a) {
+    constexpr int kScaleRow = 32;
+    __shared__ int hub[256];
+    __shared__ int nhub;
+    if (threadIdx.x == 0) nhub = 0;
+    __syncthreads();
+    T *vals = (T *)a.vals;
+    auto scale = [&](int p) {
+        const int k = a.colidx[p];
+        const T ukk = a.hasdiag[k] ? vals[a.dpos[k]] : T(0);
+        vals[p] = vals[p] / ukk;
+    };
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < a.n) {
+        const int rs = a.rowptr[i], di = a.dpos[i];
+        if (di - rs <= kScaleRow)
+            for (int p = rs; p < di; ++p) scale(p);
+        else
+            hub[atomicAdd(&nhub, 1)] = i;
+        if (a.hasdiag[i] && vals[di] == T(0)) atomicMin(a.zero_pivot, i);
+    }
+    __syncthreads();
+    for (int h = 0; h < nhub; ++h) {
+        const int r = hub[h], di = a.dpos[r];
+        for (int p = a.rowptr[r] + (int)threadIdx.x; p < di; p += 256) scale(p);
+    }
+}
+
 // Thin run of the factor in ROUNDS (plan: build_factor_plan; rsp::RndChunk,
 // rsp::RndItem), one 1024-thread workgroup. A round's items (positions) are
 // independent: each is v = a_ij - sum_k l_ik u_kj over its update pairs (k
@@ -2167,6 +2207,10 @@ static unsigned long long flow_claims(const rsp::FlowCtl &fc, int items, int gri
 
 template <typename T, int B>
 static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
+    if (a.fac_one) {
+        if (a.n > 0) hipLaunchKernelGGL((ilu0_scale_lower<T>), dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     const LevelPlan &P = a.plan;
     int fr = 0;  // next flow run (sorted by level)
     int flow_launched = 0;

@@ -793,9 +793,16 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
         constexpr int kF = 4 * rsp::kRndItemPairs;  // >= 2 x the 2 kRndItemPairs operands
         hvec<int> fkey(kF), fval(kF), fep(kF, 0);
         int fepoch = 0;
+        // first slot of the item's round in its chunk: a position placed at
+        // or after it is computed in the same round, so it is no operand
+        // slot. Only a one-level factor (IluHostPlan::fac_one) reads such a
+        // position — a u_kk of a row without lower entries, final from the
+        // start — and stages its input instead; in an L-level plan every
+        // operand lies in an earlier round, so this never triggers there.
+        int rstart = 0;
         auto ref = [&](int q, hvec<int> &fresh) {
             const unsigned long long w = wload(q), wk = w >> 12;
-            if (wk == ckey) return (int)(w & 0xfff);
+            if (wk == ckey && (int)(w & 0xfff) < rstart) return (int)(w & 0xfff);
             if (c > 0 && wk == ckey - 1) return K + (int)(w & 0xfff);
             const int st = hfind(q);
             if (st >= 0) return 2 * K + st;
@@ -845,6 +852,8 @@ static void build_factor_plan(int n, const int *rp, const int *ci,
                     fresh.clear();
                     fepoch++;
                     ipairs.clear();
+                    rstart = key != last_round_key ? (int)o.items.size() - ch.i0
+                                                   : (o.rounds.back() & ~rsp::kRndLevelStart);
                     const int po = pair_off(i);
                     for (int u = sym.upd_ptr[(size_t)p]; u < sym.upd_ptr[(size_t)p + 1]; u++) {
                         const int lc = ref(sym.upd_l[(size_t)(u + po)], fresh), uc = ref(sym.upd_u[(size_t)(u + po)], fresh);
@@ -1416,10 +1425,32 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
     const int thin_factor = thin_factor_rows();
     IluSymbolic &sym = hp.sym;
     hp.fac_batch = chain_batch((long long)sym.upd_ptr[(size_t)nnz_s], nnz_s);
+    // No update pairs at all (a stored lower triangle): the factor is
+    // l_ik = a_ik / a_kk for every lower position and nothing else, and the
+    // a_kk are never written with other bits, so every row goes in ONE level
+    // (IluHostPlan::F) instead of the L DAG's — for G2_circuit 5 799 levels.
+    // The positions' arithmetic is unchanged (same division, same operands):
+    // same bits. In that level a row may read a u_kk that the row k's own
+    // work item rewrites concurrently with identical bits (fat kernels) or
+    // that a thin run has not placed yet (its rounds are in order: lower
+    // items in round 0, a row's diagonal in round 1, so a round-0 item finds
+    // the divisor "not here" and stages the input). No flow run (one level).
+    // RSP_ILU_FAC_ONE=0 keeps L's levels (A/B).
+    hp.fac_one = n > 0 && sym.upd_ptr[(size_t)nnz_s] == 0 && env_int("RSP_ILU_FAC_ONE", 1) != 0;
+    if (hp.fac_one) {
+        hp.F.ptr = hvec<int>{0, n};
+        hp.F.rows.resize((size_t)n);
+        pfor(n, 1 << 16, [&](long long a, long long b) {
+            for (long long x = a; x < b; x++) hp.F.rows[(size_t)x] = (int)x;
+        });
+    } else {
+        hp.F = DagHost();
+    }
+    const hvec<int> &lp = hp.fac_one ? hp.F.ptr : hp.L.ptr;
+    const hvec<int> &rows_l = hp.fac_one ? hp.F.rows : hp.L.rows;
     timed_plan(n, "factor", [&] {
-        build_factor_plan(n, rp, ci, dpos, hasdiag, sym, hp.L.ptr, hp.L.rows, thin_factor, hp.fplan);
+        build_factor_plan(n, rp, ci, dpos, hasdiag, sym, lp, rows_l, thin_factor, hp.fplan);
     });
-    const hvec<int> &rows_l = hp.L.rows;
     const long long nx = (long long)rows_l.size();
     hp.frow.assign(std::max<size_t>(rows_l.size(), 1), rsp::FacRow{});
     pfor(nx, 1 << 14, [&](long long a, long long b) {
@@ -1436,7 +1467,6 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
     // budget, keeps the FacRow path. Per level (parallel): the largest
     // LDS-path row and pair count, the rows' own structure size, whether
     // every row fits the LDS path (flow runs); then the offsets in order.
-    const hvec<int> &lp = hp.L.ptr;
     const int nlev = (int)lp.size() - 1;
     hp.fslev.assign((size_t)std::max(nlev, 0), rsp::FacSlotLevel{0, 0, 0, 0, 0});
     struct LevStat {
@@ -1646,6 +1676,9 @@ uint64_t digest(const IluHostPlan &hp) {
         f.vec(d->sp.sbase);
         f.vec(d->sp.fitems);
     }
+    f.bytes(&hp.fac_one, sizeof(hp.fac_one));
+    f.vec(hp.F.ptr);
+    f.vec(hp.F.rows);
     f.vec(hp.fplan.segs);
     f.vec(hp.fplan.chunks);
     f.vec(hp.fplan.items);

@@ -104,6 +104,13 @@ struct IluHostPlan {
     hvec<int> dpos, hasdiag, udiv;
     IluSymbolic sym;
     DagHost L, LT, U;
+    // The factor's level sets: L's, or ONE level holding every row (F, with
+    // fac_one set) for a pattern without update pairs — a stored lower
+    // triangle (the symmetric matrices' storage), where no position of any
+    // row's upper part is ever updated, so every u_kk a division reads is
+    // final from the start and the L DAG's order constrains nothing.
+    DagHost F;
+    bool fac_one = false;
     // transposed strict lower part (row k: (position of l_jk, j), j descending)
     hvec<int> ltp, lts, ltc;
     // the solves' term order. Default: the reference's (L column ascending,
@@ -119,7 +126,7 @@ struct IluHostPlan {
     FacPlan fplan;
     int fac_batch = 8;
     hvec<rsp::FacRow> frow;
-    // fat factor levels in the slot layout: per L level (stride 0: FacRow
+    // fat factor levels in the slot layout: per factor level (stride 0: FacRow
     // path), the rows to write (desc) and their offsets, total ints
     hvec<rsp::FacSlotLevel> fslev;
     hvec<int4> slot_desc;

@@ -113,8 +113,10 @@ struct rsp_ilu0_info {
         rsp_an::hvec<rsp::LevelSeg> segs;       // thread-per-row solve plan
         int batch = 8;                         // solve fma-chain batch
         int group = 4;                         // thin-run term groups (2 or 4)
-    } L, LT, U;
-    rsp_an::hvec<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over L
+    } L, LT, U, F;  // F: the factor's one level when fac_one (ptr, d_rows, d_ptr; rsp_an::IluHostPlan::F)
+    bool fac_one = false;
+    const Dag &fdag() const { return fac_one ? F : L; }  // the factor's level sets
+    rsp_an::hvec<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over fdag()
     void *d_sval = nullptr, *d_sx = nullptr, *d_sdg = nullptr;  // solve streams (trsv_stream)
     rsp::RndChunk *d_rchunks = nullptr;        // round-based factor chunks (thin runs)
     rsp::RndItem *d_ritems = nullptr;
@@ -124,7 +126,7 @@ struct rsp_ilu0_info {
     rsp::FacFlowItem *d_ffitems = nullptr;
     void *d_forig = nullptr;                   // flow rows' upper input values (ilu0_flow_prep), fp64-sized
     int fac_gen = 0;
-    rsp_an::hvec<rsp::FacSlotLevel> fslev;      // per L level (stride 0: FacRow path)
+    rsp_an::hvec<rsp::FacSlotLevel> fslev;      // per factor level (stride 0: FacRow path)
     int *d_rpairs = nullptr, *d_rstaged = nullptr, *d_rrounds = nullptr;
     int fac_batch;
     void *d_arena = nullptr;    // one allocation holding the analysis' arrays (Arena)
@@ -1193,7 +1195,8 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     f->d_rchunks = nullptr;
     f->d_ritems = nullptr;
     f->d_rpairs = f->d_rstaged = f->d_rrounds = nullptr;
-    for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U}) *d = rsp_ilu0_info::Dag();
+    for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U, &f->F}) *d = rsp_ilu0_info::Dag();
+    f->fac_one = false;
 }
 
 rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
@@ -1711,6 +1714,14 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     ar.up(&f->d_frow, hp->frow);
     ar.up(&f->d_ffitems, hp->ffitems);
     f->fruns = hp->fruns;
+    f->fac_one = hp->fac_one;  // the factor's one level (rsp_an::IluHostPlan::F), else L's
+    if (hp->fac_one) {
+        f->F.ptr = hp->F.ptr;
+        f->F.group = hp->L.group;
+        f->F.batch = hp->L.batch;
+        ar.up(&f->F.d_rows, hp->F.rows);
+        ar.up(&f->F.d_ptr, hp->F.ptr);
+    }
     // flow runs: the saved upper input values of their rows (ilu0_flow_prep)
     if (!hp->fruns.empty()) ar.space(&f->d_forig, (size_t)std::max(hp->nnz_s, 1) * sizeof(double));
     rsp_k::SolveTermsArgs tl{}, tt{};
@@ -1785,7 +1796,7 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
             a.lord = f->d_lord;
             a.lend = f->d_lend;
             a.udiv = f->d_udiv;
-            a.plan.rows = f->L.d_rows;
+            a.plan.rows = f->fdag().d_rows;
             es = rsp_k::ilu0_build_slots(a, d_desc, d_offs, (int)hp->slot_desc.size(), f->d_fslots, h->stream);
             if (es == hipSuccess) es = hipStreamSynchronize(h->stream);
         }
@@ -1808,6 +1819,7 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     hp->fplan = rsp_an::FacPlan();
     hp->L = rsp_an::DagHost();
     hp->LT = rsp_an::DagHost();
+    hp->F = rsp_an::DagHost();
     hp->ltp.clear();
     hp->lts.clear();
     hp->ltc.clear();
@@ -2127,7 +2139,8 @@ static rsp_status_t ilu_factor_run(rsp_handle_t h, rsp_ilu0_info_t f, rsp_dataty
     a.rpairs = f->d_rpairs;
     a.rstaged = f->d_rstaged;
     a.rrounds = f->d_rrounds;
-    a.plan = level_plan(f->L, f->fac_segs, f->fac_batch);
+    a.plan = level_plan(f->fdag(), f->fac_segs, f->fac_batch);
+    a.fac_one = f->fac_one && env_int("RSP_ILU_FAC_SCALE", 1) != 0;
     a.fitems = f->d_ffitems;
     a.fruns = f->fruns.empty() ? nullptr : f->fruns.data();
     a.nfruns = a.fat_slots ? (int)f->fruns.size() : 0;

@@ -108,6 +108,24 @@ def test_numerical_zero_pivot(handle, monkeypatch, fat):
     assert zp == 1
 
 
+@pytest.mark.parametrize("scale_kernel", [1, 0])
+@pytest.mark.parametrize("dtype,ftz,u11", [(torch.float64, False, 0.0), (torch.float32, False, 0.0),
+                                           (torch.float32, True, 1e-40), (torch.float32, False, 1e-40)])
+def test_lower_triangle_factor_zero_pivot(handle, monkeypatch, scale_kernel, dtype, ftz, u11):
+    """A stored lower triangle (no update pairs: the one-launch factor,
+    ilu0_scale_lower, or the one-level plan with RSP_ILU_FAC_SCALE=0) whose
+    u_11 is 0 (or a denormal, flushed under FTZ): the zero pivot is reported
+    and l_21 = a_21 / u_11 has the oracle's bits (inf, or the denormal
+    quotient without FTZ)."""
+    monkeypatch.setenv("RSP_ILU_FAC_SCALE", str(scale_kernel))
+    A = csr.CsrMatrix(0, 3, 3, 6, np.array([0, 1, 3, 6], np.int32), np.array([0, 0, 1, 0, 1, 2], np.int32),
+                      np.array([2.0, 1.0, u11, 1.0, 1.0, 1.0]))
+    v, zp, _, _, _ = gpu_ilu(handle, A, dtype, ftz=ftz)
+    rv, _, rzp = ob.ilu0(A.rowptr, A.colidx, A.values.astype(NP[dtype]), ftz=ftz)
+    assert zp == rzp == (1 if (u11 == 0.0 or ftz) else -1)
+    assert np.array_equal(v.view(np.uint8), rv.view(np.uint8))
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("name,scale", [
     ("2cubes_sphere", 0.1), ("ASIC_320ks", 0.05), ("Baumann", 0.1), ("crashbasis", 0.1),
@@ -450,6 +468,9 @@ def test_flow_give_up_is_reported(handle, monkeypatch):
     monkeypatch.setenv("RSP_ILU_FLOW_RECOVER", "0")
     monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
     monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
+    # (G2_circuit is a stored lower triangle: its factor is one level, no
+    # flow run, unless it runs over L's levels)
+    monkeypatch.setenv("RSP_ILU_FAC_ONE", "0")
     A = csr.surrogate("G2_circuit", 0.1)
     rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
     va0 = va.clone()
@@ -492,6 +513,7 @@ def test_flow_give_up_is_recovered(handle, monkeypatch, dtype, ftz):
     monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
     monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
     monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", "0")
+    monkeypatch.setenv("RSP_ILU_FAC_ONE", "0")  # the factor's flow runs (see above)
     A = csr.surrogate("G2_circuit", 0.1)
     rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values, dtype)
     il = Ilu0(handle, rp, ci, nnz=A.nnz)
@@ -538,6 +560,9 @@ def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us,
     tk.rsp_testkit_occupy.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong]
     monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", str(bound_us))
     monkeypatch.setenv("RSP_ILU_FLOW_RECOVER", str(recover))
+    # offshore is a stored lower triangle: its factor runs over L's levels
+    # here (RSP_ILU_FAC_ONE=0) so that it has flow runs to block
+    monkeypatch.setenv("RSP_ILU_FAC_ONE", "0")
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
     main, side = torch.cuda.Stream(), torch.cuda.Stream()
     h = Handle(stream=main)

@@ -17,7 +17,9 @@ NP = {torch.float64: np.float64, torch.float32: np.float32}
 SEEDS = range(8)
 
 
-def random_matrix(seed):
+def random_matrix(seed, lower=False):
+    """lower: only the stored lower triangle (the symmetric matrices'
+    storage): no update pairs, so the factor runs as one level."""
     rng = np.random.default_rng(2000 + seed)
     n = int(rng.choice([5, 400, 6000, 30000]))
     kind = seed % 4
@@ -39,6 +41,8 @@ def random_matrix(seed):
     col = np.concatenate([col, np.arange(n)])
     key = np.unique(row.astype(np.int64) * n + col)
     row, col = key // n, key % n
+    if lower:
+        row, col = row[col <= row], col[col <= row]
     rp = np.zeros(n + 1, np.int32)
     np.add.at(rp, row + 1, 1)
     rp = np.cumsum(rp).astype(np.int32)
@@ -49,16 +53,24 @@ def random_matrix(seed):
     return csr.CsrMatrix(0, n, n, int(col.size), rp, col.astype(np.int32), vals)
 
 
+@pytest.mark.parametrize("lower", [0, 1, 2])
 @pytest.mark.parametrize("fat", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_random_patterns_bitwise(monkeypatch, dtype, fat):
+def test_random_patterns_bitwise(monkeypatch, dtype, fat, lower):
+    """lower 1 / 2: stored lower triangles (no update pairs), factored in
+    one launch (ilu0_scale_lower, 1) or as ONE level of the factor plan
+    (RSP_ILU_FAC_SCALE=0, 2: a row's divisor u_kk may be in the same level —
+    thin runs stage its input, fat levels read it while its row rewrites the
+    same bits)."""
     assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    if lower == 2:
+        monkeypatch.setenv("RSP_ILU_FAC_SCALE", "0")
     if fat:
         monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
         monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
     h = Handle()
     for seed in SEEDS:
-        A = random_matrix(seed)
+        A = random_matrix(seed, lower > 0)
         v, sz, zp = ob.ilu0(A.rowptr, A.colidx, A.values.astype(NP[dtype]))
         assert sz == -1 and zp == -1
         x = np.random.default_rng(seed).uniform(-1, 1, A.n).astype(NP[dtype])

@@ -275,9 +275,27 @@ def test_ilu_analysis_plan_thread_independent(monkeypatch, name, scale):
         assert st == 0
         dg.add(d)
     assert len(dg) == 1
+    # (parabolic_fem is a stored lower triangle: its factor is one fat level
+    # by default, no thin pieces; with its L levels it has them)
+    monkeypatch.setenv("RSP_ILU_FAC_ONE", "0")
+    dg = {_analysis_host(A)[3]}
     monkeypatch.setenv("RSP_ILU_PIECE_ITEMS", "500")
     small = {_analysis_host(A)[3] for t in ("1", "8") if not monkeypatch.setenv("OMP_NUM_THREADS", t)}
     assert len(small) == 1 and small != dg
+
+
+@pytest.mark.parametrize("name,one", [("parabolic_fem", True), ("G2_circuit", True), ("dc1", False),
+                                      ("tmt_unsym", False)])
+def test_ilu_factor_one_level_without_update_pairs(monkeypatch, name, one):
+    """A stored lower triangle (the symmetric matrices) has no update pairs:
+    its factor plan is one level of every row, a different plan from the one
+    over L's levels (RSP_ILU_FAC_ONE=0); a pattern with update pairs keeps
+    L's levels either way (the same digest)."""
+    A = csr.surrogate(name, 0.05)
+    d1 = _analysis_host(A)[3]
+    monkeypatch.setenv("RSP_ILU_FAC_ONE", "0")
+    d0 = _analysis_host(A)[3]
+    assert (d1 != d0) == one
 
 
 def test_ilu_analysis_host_rejects_malformed():
