@@ -1446,6 +1446,18 @@ void plan_factor(const int *rp, const int *ci, long long slot_cap, IluHostPlan &
     } else {
         hp.F = DagHost();
     }
+    hp.fac_scale = hp.fac_one && env_int("RSP_ILU_FAC_SCALE", 1) != 0;
+    if (hp.fac_scale) {  // ilu0_scale_lower needs no plan
+        hp.fplan = FacPlan();
+        hp.frow.assign(1, rsp::FacRow{});
+        hp.fslev.clear();
+        hp.slot_desc.clear();
+        hp.slot_offs.clear();
+        hp.slot_total = 0;
+        hp.fruns.clear();
+        hp.ffitems.assign(1, rsp::FacFlowItem{0, 0, -1});
+        return;
+    }
     const hvec<int> &lp = hp.fac_one ? hp.F.ptr : hp.L.ptr;
     const hvec<int> &rows_l = hp.fac_one ? hp.F.rows : hp.L.rows;
     timed_plan(n, "factor", [&] {
@@ -1677,6 +1689,7 @@ uint64_t digest(const IluHostPlan &hp) {
         f.vec(d->sp.fitems);
     }
     f.bytes(&hp.fac_one, sizeof(hp.fac_one));
+    f.bytes(&hp.fac_scale, sizeof(hp.fac_scale));
     f.vec(hp.F.ptr);
     f.vec(hp.F.rows);
     f.vec(hp.fplan.segs);

@@ -111,6 +111,10 @@ struct IluHostPlan {
     // final from the start and the L DAG's order constrains nothing.
     DagHost F;
     bool fac_one = false;
+    // fac_one and the factor is ilu0_scale_lower (one launch, no plan: the
+    // factor plan, FacRow records and slots stay empty); RSP_ILU_FAC_SCALE=0
+    // at analysis time plans the one level instead (A/B, tests)
+    bool fac_scale = false;
     // transposed strict lower part (row k: (position of l_jk, j), j descending)
     hvec<int> ltp, lts, ltc;
     // the solves' term order. Default: the reference's (L column ascending,

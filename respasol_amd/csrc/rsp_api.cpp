@@ -114,7 +114,7 @@ struct rsp_ilu0_info {
         int batch = 8;                         // solve fma-chain batch
         int group = 4;                         // thin-run term groups (2 or 4)
     } L, LT, U, F;  // F: the factor's one level when fac_one (ptr, d_rows, d_ptr; rsp_an::IluHostPlan::F)
-    bool fac_one = false;
+    bool fac_one = false, fac_scale = false;  // fac_scale: the factor is ilu0_scale_lower (IluHostPlan::fac_scale)
     const Dag &fdag() const { return fac_one ? F : L; }  // the factor's level sets
     rsp_an::hvec<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over fdag()
     void *d_sval = nullptr, *d_sx = nullptr, *d_sdg = nullptr;  // solve streams (trsv_stream)
@@ -1196,7 +1196,7 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     f->d_ritems = nullptr;
     f->d_rpairs = f->d_rstaged = f->d_rrounds = nullptr;
     for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U, &f->F}) *d = rsp_ilu0_info::Dag();
-    f->fac_one = false;
+    f->fac_one = f->fac_scale = false;
 }
 
 rsp_status_t rsp_create_ilu0_info(rsp_ilu0_info_t *info) {
@@ -1715,6 +1715,7 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     ar.up(&f->d_ffitems, hp->ffitems);
     f->fruns = hp->fruns;
     f->fac_one = hp->fac_one;  // the factor's one level (rsp_an::IluHostPlan::F), else L's
+    f->fac_scale = hp->fac_scale;
     if (hp->fac_one) {
         f->F.ptr = hp->F.ptr;
         f->F.group = hp->L.group;
@@ -2140,7 +2141,7 @@ static rsp_status_t ilu_factor_run(rsp_handle_t h, rsp_ilu0_info_t f, rsp_dataty
     a.rstaged = f->d_rstaged;
     a.rrounds = f->d_rrounds;
     a.plan = level_plan(f->fdag(), f->fac_segs, f->fac_batch);
-    a.fac_one = f->fac_one && env_int("RSP_ILU_FAC_SCALE", 1) != 0;
+    a.fac_one = f->fac_scale;
     a.fitems = f->d_ffitems;
     a.fruns = f->fruns.empty() ? nullptr : f->fruns.data();
     a.nfruns = a.fat_slots ? (int)f->fruns.size() : 0;

@@ -373,9 +373,9 @@ struct IluArgs {
     int flow, flow_grid, flow_sleep;
     int flow_cus;               // CUs of the device (caps a flow grid)
     FlowCtl fc;                 // flow launches: give-up status word, claim counter
-    // a pattern without update pairs (rsp_an::IluHostPlan::fac_one): the
-    // whole factor is ilu0_scale_lower, one launch (RSP_ILU_FAC_SCALE=0: the
-    // one-level plan instead)
+    // a pattern without update pairs (rsp_an::IluHostPlan::fac_scale): the
+    // whole factor is ilu0_scale_lower, one launch (RSP_ILU_FAC_SCALE=0 at
+    // analysis: the one-level plan instead)
     int fac_one;
 };
 
