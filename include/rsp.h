@@ -166,21 +166,29 @@ rsp_status_t rsp_ilu0_analysis(rsp_handle_t handle, int n, int nnz, const int *d
  * structurally missing (after analysis) or U(j,j) == 0 (after the numeric
  * factorisation); the smallest such j is reported. Otherwise SUCCESS, -1. */
 rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t handle, rsp_ilu0_info_t info, int *position);
-/* A factor whose persistent (flow) launch gave up a dependency wait (bounded
- * by RSP_ILU_FLOW_TIMEOUT_US, default 0.2 s: only when another kernel keeps
- * the launch's workgroups off the CUs that long) is RECOVERED here: its
- * input values (kept by the factor call) are restored, the factor runs again
- * without flow launches — and so does every solve made after it — and the
- * call reports as usual. RSP_STATUS_EXECUTION_FAILED only when recovery is
- * off (RSP_ILU_FLOW_RECOVER=0) or fails. About the LAST factor call only. */
+/* Flow launches (one launch over a run of fat levels) take their work items by
+ * start tickets (the default since round 6): a workgroup waits only on items
+ * of workgroups that started before it, so progress never depends on other
+ * kernels leaving CUs free and no wait gives up in normal operation. The
+ * bounded wait (RSP_ILU_FLOW_TIMEOUT_US, default 0.2 s) stays as a backstop,
+ * and it is what the older static item walk (RSP_ILU_FLOW_MODE=0) needs: a
+ * factor whose flow wait gave up is RECOVERED here — its input values (kept
+ * by the factor call) are restored, the factor runs again without flow
+ * launches, and so does every solve made after it — and the call reports as
+ * usual. The buffers of the recorded calls (values, x) must then be unchanged
+ * since those calls; a later recorded solve that wrote its y over one of them
+ * (e.g. L: r -> z, then L^T: z -> r) makes the recovery impossible and the
+ * call returns RSP_STATUS_EXECUTION_FAILED, as it does when recovery is off
+ * (RSP_ILU_FLOW_RECOVER=0). About the LAST factor call only. */
 
 /* cusparseXcsrsv2_zeroPivot (the csrsv2 infos of GPU/ilu0.cu:143-150) for
  * the solves below; which = RSP_TRSV_L (op N), RSP_TRSV_LT (op T) or
  * RSP_TRSV_U (rsp_trsv_upper). Host-blocking. Reports on the LAST solve of
  * that kind. If its flow launch gave up a wait, the solve (its x is
  * unchanged: x != y) and every solve made after it are run again without
- * flow launches first; RSP_STATUS_EXECUTION_FAILED only with
- * RSP_ILU_FLOW_RECOVER=0. For RSP_TRSV_U, ZERO_PIVOT + *position as
+ * flow launches first (their x and values must be unchanged, as above);
+ * RSP_STATUS_EXECUTION_FAILED with RSP_ILU_FLOW_RECOVER=0 or when a later
+ * recorded solve overwrote one of those inputs. For RSP_TRSV_U, ZERO_PIVOT + *position as
  * rsp_ilu0_zero_pivot (U divides by u_jj); else SUCCESS, -1. */
 #define RSP_TRSV_L 0
 #define RSP_TRSV_LT 1
@@ -272,6 +280,14 @@ rsp_status_t rsp_spmv_batch_info(rsp_spmv_batch_t batch, int64_t *tiles, int64_t
 
 /* Number of dependency levels found by the analysis (L DAG, L^T DAG). */
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t info, int *levels_lower, int *levels_upper);
+/* Extension (round 6): the blocks of the block-inverse solve the analysis
+ * planned for the L and L^T solves (0: that solve is level-scheduled). Deep
+ * DAGs (<= 32 rows per level on average; RSP_ILU_BLOCKS=1 / 0 at analysis
+ * time forces it on / off) are solved block by block, each row's unknown
+ * written as a combination of its block's right-hand sides and of earlier
+ * blocks' unknowns: same unknowns, rounding of that order (restated in the
+ * oracle), within SURVEY 8c's tolerance of the reference's order. */
+rsp_status_t rsp_ilu0_solve_blocks(rsp_ilu0_info_t info, int *blocks_lower, int *blocks_upper);
 
 /* Tests and profiling (no cuSPARSE counterpart, no device needed): the host
  * phases of rsp_ilu0_analysis on HOST arrays (base 0) — validation, levels,

@@ -307,6 +307,329 @@ static void lower_by_cols(int n, const int *rp, const int *ci, int **cp_, int **
 ORACLE_TRSV_SPLIT(double, d, fma)
 ORACLE_TRSV_SPLIT(float, s, fmaf)
 
+/* ---------------------------------------------- block-inverse solve order
+ * (round 6, the deep-DAG solve of the MI355X plans; rsp_oracle.h). Every
+ * step restated from the definition, independently of the product's planner
+ * (respasol_amd/csrc/ilu_blocks.cpp):
+ *  1. dependencies of row i in their order: kind 0 (L): (column j, position)
+ *     of row i's strict lower part, j ascending; kind 1 (L^T): the rows j > i
+ *     with l_ji != 0, j descending (the TRANSPOSE column sweep's order);
+ *  2. levels (longest dependency path) and the level order: by level, rows
+ *     ascending inside a level; "position" = index in that order;
+ *  3. CHUNKS, one pass over the positions: a chunk starts at 0, at a
+ *     position ch after its chunk's start, and at a position whose row has
+ *     more than lcap dependencies at or after its chunk's start (that row
+ *     starts a new chunk); no block crosses a chunk. Blocks, greedily over
+ *     the positions: row p joins the current block (first position s) if the
+ *     block has < bs rows, p does not start a chunk, and p's pattern with the
+ *     block (below) has <= ymax y terms of which <= near are NEAR (position
+ *     >= max(chunk start, s - nw));
+ *     otherwise the block is closed and p starts a new block with its own
+ *     dependencies as pattern; if that pattern breaks the same caps, p is a
+ *     LONG block of its own (the next row starts a new block);
+ *  4. pattern of p in block b (first position s): x sources = {p} and the x
+ *     sources of its in-block dependencies; y sources = the y sources of its
+ *     in-block dependencies and the positions of its dependencies before s;
+ *     ordered x ascending, then y ascending;
+ *  5. coefficients E (one per pattern entry, the block's partitioned
+ *     inverse): start at 1 for x source p, 0 elsewhere; then, dependency by
+ *     dependency in the order of 1. with value l: an in-block dependency q
+ *     adds E_p[u] = fma(-l, E_q[u], E_p[u]) for every source u of q's
+ *     pattern; one before the block adds E_p[q] = fma(-l, 1, E_p[q]);
+ *  6. the solve, positions in order: a normal row is s = 0, then
+ *     s = fma(E_k, v_k, s) over its pattern in order, v = alpha x_node for an
+ *     x source (alpha x rounded first) and y of the source's position for a y
+ *     source; a long row sums its pattern's entries k into 64 partials
+ *     (k mod 64, each in order, from 0) combined by a xor butterfly
+ *     (stride 32, 16, ..., 1: p_l = p_l + p_(l xor stride)), partial 0. */
+#define BLK_DEFAULTS {64, 32, 12, 1 << 30, 16384, 768}
+typedef struct {
+    int *dp, *dj, *dv;  /* row i's dependencies [dp[i], dp[i+1]): source row, value position */
+} BlkDeps;
+static void blk_deps(int kind, int n, const int *rp, const int *ci, BlkDeps *d) {
+    d->dp = (int *)calloc((size_t)n + 1, sizeof(int));
+    if (kind == 0) {
+        for (int i = 0; i < n; i++) {
+            int c = 0;
+            for (int p = rp[i]; p < rp[i + 1] && ci[p] < i; p++) c++;
+            d->dp[i + 1] = d->dp[i] + c;
+        }
+        int m = d->dp[n] > 0 ? d->dp[n] : 1;
+        d->dj = (int *)malloc((size_t)m * sizeof(int));
+        d->dv = (int *)malloc((size_t)m * sizeof(int));
+        for (int i = 0; i < n; i++) {
+            int o = d->dp[i];
+            for (int p = rp[i]; p < rp[i + 1] && ci[p] < i; p++, o++) {
+                d->dj[o] = ci[p];
+                d->dv[o] = p;
+            }
+        }
+    } else {
+        int *cp, *tp, *tr;
+        lower_by_cols(n, rp, ci, &cp, &tp, &tr);
+        memcpy(d->dp, cp, ((size_t)n + 1) * sizeof(int));
+        d->dj = tr;
+        d->dv = tp;
+        free(cp);
+    }
+}
+/* position -> row: level order, rows ascending inside a level */
+static int *blk_order(int kind, int n, const BlkDeps *d) {
+    int *lv = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    int nl = 0;
+    for (int k = 0; k < n; k++) {
+        int i = kind == 0 ? k : n - 1 - k, l = 0;
+        for (int o = d->dp[i]; o < d->dp[i + 1]; o++)
+            if (lv[d->dj[o]] + 1 > l) l = lv[d->dj[o]] + 1;
+        lv[i] = l;
+        if (l + 1 > nl) nl = l + 1;
+    }
+    int *cnt = (int *)calloc((size_t)nl + 1, sizeof(int));
+    for (int i = 0; i < n; i++) cnt[lv[i] + 1]++;
+    for (int l = 0; l < nl; l++) cnt[l + 1] += cnt[l];
+    int *ord = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int i = 0; i < n; i++) ord[cnt[lv[i]]++] = i;
+    free(cnt);
+    free(lv);
+    return ord;
+}
+typedef struct {
+    int *v;
+    long long n, cap;
+} BlkVec;
+static void bv_push(BlkVec *b, int x) {
+    if (b->n == b->cap) {
+        b->cap = b->cap ? 2 * b->cap : 1024;
+        b->v = (int *)realloc(b->v, (size_t)b->cap * sizeof(int));
+    }
+    b->v[b->n++] = x;
+}
+static int cmp_int(const void *a, const void *b) {
+    int x = *(const int *)a, y = *(const int *)b;
+    return x < y ? -1 : x > y;
+}
+/* the plan: blocks, patterns (per position: sources at pool[po[p] ..], nx x
+ * sources first), long blocks */
+typedef struct {
+    int nb;
+    int *blk, *bstart, *islong; /* per position; per block (bstart[nb] = n) */
+    long long *po;              /* per position: pattern offset, po[n] = total */
+    int *nx;                    /* per position: x sources */
+    int *pool;
+} BlkPlan;
+static void blk_plan(int n, const int *ord, const BlkDeps *d, const int *prm, BlkPlan *P) {
+    const int bs = prm[0], ymax = prm[1], nmax = prm[2], nw = prm[3], ch = prm[4], lcap = prm[5];
+    int *pos = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int p = 0; p < n; p++) pos[ord[p]] = p;
+    /* chunk starts: cst[p] = the first position of p's chunk */
+    int *cst = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int p = 0, c0 = 0; p < n; p++) {
+        if (p - c0 == ch) c0 = p;
+        else if (p > c0) {
+            const int r = ord[p];
+            int m = 0;
+            for (int o = d->dp[r]; o < d->dp[r + 1]; o++) m += pos[d->dj[o]] >= c0;
+            if (m > lcap) c0 = p;
+        }
+        cst[p] = c0;
+    }
+    int *stamp = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    for (int p = 0; p < n; p++) stamp[p] = -1;
+    P->blk = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    P->bstart = (int *)malloc(((size_t)n + 2) * sizeof(int));
+    P->islong = (int *)calloc((size_t)n + 2, sizeof(int));
+    P->po = (long long *)malloc(((size_t)n + 1) * sizeof(long long));
+    P->nx = (int *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int));
+    BlkVec pool = {0, 0, 0}, xs = {0, 0, 0}, ys = {0, 0, 0};
+    int tag = 0, b = 0, bsize = 0, bst = 0, near = 0;
+    /* the candidate pattern of position p in a block starting at s (s == p:
+     * no block rows before p) */
+#define BLK_CAND(S)                                                                         \
+    do {                                                                                    \
+        const int s_ = (S), lo_ = cst[p] > s_ - nw ? cst[p] : s_ - nw;                      \
+        xs.n = ys.n = 0;                                                                    \
+        near = 0;                                                                           \
+        tag++;                                                                              \
+        bv_push(&xs, p);                                                                    \
+        stamp[p] = tag;                                                                     \
+        for (int o = d->dp[r]; o < d->dp[r + 1]; o++) {                                     \
+            const int q = pos[d->dj[o]];                                                    \
+            if (q >= s_) {                                                                  \
+                for (long long k = P->po[q]; k < P->po[q + 1]; k++) {                       \
+                    const int u = pool.v[k];                                                \
+                    if (stamp[u] == tag) continue;                                          \
+                    stamp[u] = tag;                                                         \
+                    bv_push(k - P->po[q] < P->nx[q] ? &xs : &ys, u);                        \
+                }                                                                           \
+            } else if (stamp[q] != tag) {                                                   \
+                stamp[q] = tag;                                                             \
+                bv_push(&ys, q);                                                            \
+            }                                                                               \
+        }                                                                                   \
+        for (long long k = 0; k < ys.n; k++) near += ys.v[k] >= lo_;                        \
+    } while (0)
+    for (int p = 0; p < n; p++) {
+        const int r = ord[p];
+        int ok = 0;
+        P->po[p] = pool.n; /* (the end of p - 1's pattern) */
+        if (bsize > 0) {
+            if (cst[p] != p) {
+                BLK_CAND(bst);
+                ok = bsize < bs && ys.n <= ymax && near <= nmax;
+            }
+            if (!ok) {
+                P->bstart[b] = bst;
+                b++;
+                bsize = 0;
+                bst = p;
+            }
+        }
+        if (!ok) {
+            BLK_CAND(p);
+        }
+        qsort(xs.v, (size_t)xs.n, sizeof(int), cmp_int);
+        qsort(ys.v, (size_t)ys.n, sizeof(int), cmp_int);
+        P->po[p] = pool.n;
+        P->nx[p] = (int)xs.n;
+        for (long long k = 0; k < xs.n; k++) bv_push(&pool, xs.v[k]);
+        for (long long k = 0; k < ys.n; k++) bv_push(&pool, ys.v[k]);
+        P->blk[p] = b;
+        if (bsize == 0) bst = p;
+        bsize++;
+        if (!ok && (ys.n > ymax || near > nmax)) { /* a long row: a block of its own */
+            P->islong[b] = 1;
+            P->bstart[b] = bst;
+            b++;
+            bsize = 0;
+            bst = p + 1;
+        }
+    }
+#undef BLK_CAND
+    if (bsize > 0) {
+        P->bstart[b] = bst;
+        b++;
+    }
+    P->po[n] = pool.n;
+    P->bstart[b] = n;
+    P->nb = b;
+    P->pool = pool.v;
+    free(xs.v);
+    free(ys.v);
+    free(stamp);
+    free(pos);
+    free(cst);
+}
+static void blk_free(BlkPlan *P, BlkDeps *d, int *ord) {
+    free(P->blk);
+    free(P->bstart);
+    free(P->islong);
+    free(P->po);
+    free(P->nx);
+    free(P->pool);
+    free(d->dp);
+    free(d->dj);
+    free(d->dv);
+    free(ord);
+}
+#define ORACLE_BLOCKS(T, SUF, FMA)                                                             \
+    static int blocks_##SUF(int kind, int n, const int *rp, const int *ci, const T *v, T alpha, \
+                            const T *x, T *y, const int *params) {                            \
+        static const int dflt[6] = BLK_DEFAULTS;                                               \
+        const int *prm = params ? params : dflt;                                               \
+        if (n < 0 || kind < 0 || kind > 1 || prm[0] < 1 || prm[0] > 64 || prm[4] < 1) return -1; \
+        if (n == 0) return 0;                                                                  \
+        BlkDeps d;                                                                             \
+        blk_deps(kind, n, rp, ci, &d);                                                         \
+        int *ord = blk_order(kind, n, &d);                                                     \
+        BlkPlan P;                                                                             \
+        blk_plan(n, ord, &d, prm, &P);                                                         \
+        int *pos = (int *)malloc((size_t)n * sizeof(int));                                     \
+        for (int p = 0; p < n; p++) pos[ord[p]] = p;                                           \
+        T *E = (T *)malloc((size_t)(P.po[n] > 0 ? P.po[n] : 1) * sizeof(T));                   \
+        T *acc = (T *)calloc((size_t)n, sizeof(T));                                            \
+        for (int p = 0; p < n; p++) { /* 5. coefficients */                                    \
+            const int r = ord[p], s0 = P.bstart[P.blk[p]];                                     \
+            for (long long k = P.po[p]; k < P.po[p + 1]; k++) acc[P.pool[k]] = (T)0;          \
+            acc[p] = (T)1;                                                                     \
+            for (int o = d.dp[r]; o < d.dp[r + 1]; o++) {                                      \
+                const T l = v[d.dv[o]];                                                        \
+                const int q = pos[d.dj[o]];                                                    \
+                if (q >= s0)                                                                   \
+                    for (long long k = P.po[q]; k < P.po[q + 1]; k++)                          \
+                        acc[P.pool[k]] = FMA(-l, E[k], acc[P.pool[k]]);                        \
+                else                                                                           \
+                    acc[q] = FMA(-l, (T)1, acc[q]);                                            \
+            }                                                                                  \
+            for (long long k = P.po[p]; k < P.po[p + 1]; k++) E[k] = acc[P.pool[k]];          \
+        }                                                                                      \
+        T *yp = acc; /* 6. the solve (acc reused: positions' y) */                             \
+        for (int p = 0; p < n; p++) {                                                          \
+            const long long k0 = P.po[p], k1 = P.po[p + 1];                                    \
+            T s = 0;                                                                           \
+            if (!P.islong[P.blk[p]]) {                                                         \
+                for (long long k = k0; k < k1; k++) {                                          \
+                    const int u = P.pool[k];                                                   \
+                    const T val = k - k0 < P.nx[p] ? (T)(alpha * x[ord[u]]) : yp[u];           \
+                    s = FMA(E[k], val, s);                                                     \
+                }                                                                              \
+            } else {                                                                           \
+                T part[64], tmp[64];                                                           \
+                for (int l = 0; l < 64; l++) part[l] = 0;                                      \
+                for (long long k = k0; k < k1; k++) {                                          \
+                    const int u = P.pool[k];                                                   \
+                    const T val = k - k0 < P.nx[p] ? (T)(alpha * x[ord[u]]) : yp[u];           \
+                    part[(k - k0) & 63] = FMA(E[k], val, part[(k - k0) & 63]);                 \
+                }                                                                              \
+                for (int off = 32; off >= 1; off >>= 1) {                                      \
+                    for (int l = 0; l < 64; l++) tmp[l] = part[l] + part[l ^ off];             \
+                    memcpy(part, tmp, sizeof(part));                                           \
+                }                                                                              \
+                s = part[0];                                                                   \
+            }                                                                                  \
+            yp[p] = s;                                                                         \
+        }                                                                                      \
+        for (int p = 0; p < n; p++) y[ord[p]] = yp[p];                                         \
+        const int nb = P.nb;                                                                   \
+        free(E);                                                                               \
+        free(acc);                                                                             \
+        free(pos);                                                                             \
+        blk_free(&P, &d, ord);                                                                 \
+        return nb;                                                                             \
+    }
+ORACLE_BLOCKS(double, d, fma)
+ORACLE_BLOCKS(float, s, fmaf)
+
+int oracle_dag_levels(int kind, int n, const int *rp, const int *ci) {
+    if (n <= 0 || kind < 0 || kind > 1) return 0;
+    BlkDeps d;
+    blk_deps(kind, n, rp, ci, &d);
+    int *lv = (int *)malloc((size_t)n * sizeof(int)), nl = 0;
+    for (int k = 0; k < n; k++) {
+        int i = kind == 0 ? k : n - 1 - k, l = 0;
+        for (int o = d.dp[i]; o < d.dp[i + 1]; o++)
+            if (lv[d.dj[o]] + 1 > l) l = lv[d.dj[o]] + 1;
+        lv[i] = l;
+        if (l + 1 > nl) nl = l + 1;
+    }
+    free(lv);
+    free(d.dp);
+    free(d.dj);
+    free(d.dv);
+    return nl;
+}
+
+int oracle_trsv_blocks_f64(int kind, int n, const int *rp, const int *ci, const double *v, double alpha,
+                           const double *x, double *y, const int *params) {
+    return blocks_d(kind, n, rp, ci, v, alpha, x, y, params);
+}
+int oracle_trsv_blocks_f32(int kind, int n, const int *rp, const int *ci, const float *v, float alpha,
+                           const float *x, float *y, const int *params, int ftz) {
+    unsigned old = ftz_enter(ftz);
+    const int r = blocks_s(kind, n, rp, ci, v, alpha, x, y, params);
+    ftz_leave(old);
+    return r;
+}
+
 void oracle_trsv_lower_n_split_f64(int n, const int *rp, const int *ci, const double *v, double alpha,
                                    const double *x, double *y) {
     lower_n_split_d(n, rp, ci, v, alpha, x, y);

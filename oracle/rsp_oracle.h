@@ -84,6 +84,27 @@ void oracle_trsv_lower_t_split_f64(int n, const int *rowptr, const int *colidx, 
                                    double alpha, const double *x, double *y);
 void oracle_trsv_lower_t_split_f32(int n, const int *rowptr, const int *colidx, const float *vals,
                                    float alpha, const float *x, float *y, int ftz);
+/* The two unit-lower solves (kind 0: L y = alpha x; kind 1: L^T y = alpha x)
+ * in the BLOCK-INVERSE order of the MI355X deep-DAG solve (round 6; the
+ * product's planner is ilu_blocks.cpp, restated here independently):
+ * rows in level order, cut greedily into blocks of <= bs rows; inside a
+ * block every row's unknown is written as a combination of the block's
+ * right-hand sides (alpha x) and of y values of earlier blocks (the
+ * block's explicit partitioned inverse), so a block is one dependent step.
+ * Same unknowns, different rounding from the reference order: within
+ * SURVEY 8c's solve tolerance (tests/test_oracle.py), and the GPU equals
+ * THIS restatement bit for bit. params = {bs, ymax, near, nw, ch, lcap}
+ * (rows per block, y terms of a row, near terms of a row, near window in
+ * positions, chunk length, a row with more dependencies in its chunk starts
+ * a new one; see rsp_oracle.c); null = the product's defaults. Returns the number of blocks (< 0: bad
+ * arguments). */
+/* Levels (longest dependency path + 1) of the L (kind 0) or L^T (kind 1) DAG. */
+int oracle_dag_levels(int kind, int n, const int *rowptr, const int *colidx);
+int oracle_trsv_blocks_f64(int kind, int n, const int *rowptr, const int *colidx, const double *vals,
+                           double alpha, const double *x, double *y, const int *params);
+int oracle_trsv_blocks_f32(int kind, int n, const int *rowptr, const int *colidx, const float *vals,
+                           float alpha, const float *x, float *y, const int *params, int ftz);
+
 /* U y = alpha x (upper incl. diagonal) — the desc_U extension. */
 void oracle_trsv_upper_f64(int n, const int *rowptr, const int *colidx, const double *vals,
                            double alpha, const double *x, double *y);

@@ -415,8 +415,30 @@ __device__ __forceinline__ int flow_item(unsigned long long c, unsigned long lon
     return __builtin_amdgcn_readfirstlane((int)min(d, (long long)(it1 - it0))) + it0;
 }
 
-// One wave's walk over the items [it0, it1) of a flow launch (rsp::FlowCtl).
-// Static (default): w, w + W, ... Claimed (kFlowClaims): in start order, TWO items ahead — the claim for item
+// One wave's walk over the items [it0, it1) of a flow launch (rsp::FlowCtl):
+//   for (fq.first(); fq.more(); fq.next()) { const int it = fq.item(); if (it < it1) ... }
+// Start tickets (kFlowTickets, the default): the workgroup takes TICKETS in
+// the order it runs — thread 0 alone, agent-scope fetch_adds on the flow
+// counter, so its tickets increase with its rounds — and in round r each
+// wave runs item 4 t_r + (its wave) of that round's ticket. Thread 0 claims
+// kTicketAhead rounds ahead and publishes each ticket in an LDS ring
+// (kTicketRing slots, with the round it belongs to); a wave entering round r
+// waits (in LDS) for round r's ticket, so the waves of a workgroup run
+// independently up to the lookahead — no workgroup barrier per round.
+// Thread 0 never runs more than kTicketRing - kTicketAhead rounds ahead of
+// the slowest wave (its ring slot would be reused).
+// Progress: an item waits only on items of lower tickets. Let u be the
+// lowest unfinished item, in round r of workgroup X; X's earlier rounds hold
+// lower tickets, so they are finished and u's wave is in round r or entering
+// it, whose ticket wave 0 published kTicketAhead - 1 rounds earlier (wave 0's
+// own round-r item is below u or is u). Every ticket is held by a workgroup
+// that has started: progress needs no co-residency, only that a started
+// workgroup keeps running.
+// The counter is restored at the end of the launch (the last workgroup to
+// exit, counted on fc.exits, stores `base` back), so a ticket launch leaves
+// the host mirror unchanged.
+// Static (RSP_ILU_FLOW_MODE=0): w, w + W, ... (the whole grid must be resident).
+// Claimed (kFlowClaims): in start order, TWO items ahead — the claim for item
 // j + 2 is issued during item j, behind its first loads (claim_ahead), and
 // read when item j + 1 ends, so the atomic's latency hides under a whole
 // item. A wave makes 2 + (items it processes) claims, so a launch advances
@@ -424,29 +446,124 @@ __device__ __forceinline__ int flow_item(unsigned long long c, unsigned long lon
 // unfinished item is always some running wave's CURRENT item (a wave's
 // claimed items are above its current one), so progress needs no
 // co-residency.
+constexpr int kTicketRing = 16, kTicketAhead = 4;
+struct FlowTicketLds {
+    int tk[kTicketRing];   // ticket of the round in pub[] (ring slot r % kTicketRing)
+    int pub[kTicketRing];  // the round whose ticket the slot holds
+    int cur[4];            // the round each wave is in
+};
 struct FlowClaims {
     const rsp::FlowCtl &fc;
     unsigned long long base, c1 = 0, c2 = 0;
-    int it0, it1, cur, stride;
-    bool dyn;
-    __device__ FlowClaims(const rsp::FlowCtl &f, unsigned long long b, int i0, int i1, int w, int W)
-        : fc(f), base(b), it0(i0), it1(i1), cur(i0 + w), stride(W), dyn((f.mode & rsp::kFlowClaims) != 0) {}
-    __device__ int first() {
-        if (!dyn) return cur;
-        const unsigned long long c0 = flow_claim(fc);
-        c1 = flow_claim(fc);
-        return flow_item(c0, base, it0, it1);
+    int it0, it1, cur, stride, wv;
+    int mode;  // 0 static, 1 claims, 2 tickets
+    FlowTicketLds *L;
+    int A = 0, r = 0;
+    // thread 0 (tickets): the claim in flight (value cv for round cr > 0, or
+    // cr == 0: none), the next round to claim, whether claims go on
+    int cv = 0, cr = 0, nclaimed = 0;
+    bool claiming = false;
+    __device__ FlowClaims(const rsp::FlowCtl &f, unsigned long long b, int i0, int i1, int w, int W,
+                          FlowTicketLds *l)
+        : fc(f), base(b), it0(i0), it1(i1), cur(i0 + w), stride(W), wv(w & 3),
+          mode((f.mode & rsp::kFlowTickets) ? 2 : (f.mode & rsp::kFlowClaims) ? 1 : 0), L(l) {}
+    __device__ int ticket() const {
+        return (int)(__hip_atomic_fetch_add(fc.claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base);
     }
+    __device__ int rounds() const { return (it1 - it0 + 3) >> 2; }
+    __device__ static int lds_ld(const int *p) {
+        return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    }
+    // LDS-only acquire / release (the "local" address-space fences): a
+    // workgroup-scope acquire or release on a plain atomic would also wait
+    // for the wave's outstanding GLOBAL accesses (s_waitcnt vmcnt(0)), here
+    // the item's y / value stores still in flight
+    __device__ static int lds_acq(const int *p) {
+        const int v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        return v;
+    }
+    __device__ void first() {
+        if (mode == 0) return;
+        if (mode == 1) {
+            const unsigned long long c0 = flow_claim(fc);
+            c1 = flow_claim(fc);
+            cur = flow_item(c0, base, it0, it1);
+            return;
+        }
+        if (threadIdx.x == 0) {  // rounds 0 .. kTicketAhead - 1 (the atomics overlap)
+            int t[kTicketAhead];
+#pragma unroll
+            for (int k = 0; k < kTicketAhead; ++k) t[k] = ticket();
+#pragma unroll
+            for (int k = 0; k < kTicketAhead; ++k) L->tk[k] = t[k];
+            claiming = t[kTicketAhead - 1] < rounds();
+            nclaimed = kTicketAhead;
+        }
+        if (threadIdx.x < kTicketRing) L->pub[threadIdx.x] = threadIdx.x < kTicketAhead ? (int)threadIdx.x : -1;
+        if (threadIdx.x < 4) L->cur[threadIdx.x] = 0;
+        __syncthreads();  // (once, at the start)
+        A = lds_ld(&L->tk[0]);
+    }
+    __device__ bool more() const { return mode == 2 ? A < rounds() : cur < it1; }
+    __device__ int item() const { return mode == 2 ? it0 + 4 * A + wv : cur; }
     __device__ void claim_ahead() {
         __builtin_amdgcn_sched_barrier(0);
-        if (dyn) c2 = flow_claim(fc);
+        if (mode == 1) c2 = flow_claim(fc);
         __builtin_amdgcn_sched_barrier(0);
     }
-    __device__ int next() {
-        if (!dyn) return cur += stride;
-        const int it = flow_item(c1, base, it0, it1);
-        c1 = c2;
-        return it;
+    // thread 0: publish the claim in flight (issued at least a round ago, so
+    // its value is back), then claim round `nclaimed` if it is at most
+    // kTicketAhead past this wave's round and its ring slot is free (every
+    // other wave is past the round that slot held)
+    __device__ void service() {
+        if (cr > 0) {
+            __hip_atomic_store(&L->tk[cr % kTicketRing], cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            __hip_atomic_store(&L->pub[cr % kTicketRing], cr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            claiming = cv < rounds();
+            cr = 0;
+        }
+        if (claiming && nclaimed <= r + kTicketAhead) {
+            const int lo = min(lds_ld(&L->cur[1]), min(lds_ld(&L->cur[2]), lds_ld(&L->cur[3])));
+            if (lo > nclaimed - kTicketRing) {
+                cv = ticket();
+                cr = nclaimed++;
+            }
+        }
+    }
+    __device__ void next() {
+        if (mode == 0) {
+            cur += stride;
+            return;
+        }
+        if (mode == 1) {
+            cur = flow_item(c1, base, it0, it1);
+            c1 = c2;
+            return;
+        }
+        const bool lead = wv == 0 && (threadIdx.x & 63) == 0;
+        if (lead) service();
+        ++r;
+        const int *pub = &L->pub[r % kTicketRing];
+        while (lds_acq(pub) != r) {  // (wave 0 publishes the round itself if it is not yet)
+            if (lead) service();
+            __builtin_amdgcn_s_sleep(1);
+        }
+        A = lds_ld(&L->tk[r % kTicketRing]);
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_store(&L->cur[wv], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // tickets: the last workgroup to finish restores the counter (every
+    // thread calls it after its loop; thread 0 acts)
+    __device__ void finish() {
+        if (mode != 2 || threadIdx.x != 0) return;
+        const int e = __hip_atomic_fetch_add(fc.exits, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == (int)gridDim.x - 1) {
+            __hip_atomic_store(fc.claim, base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(fc.exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 };
 
@@ -670,8 +787,11 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, un
     unsigned short *pl = pl_[wv];
     T *vals = (T *)a.vals;
     const T *orig = (const T *)a.forig;
-    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4);
-    for (int it = fq.first(); it < it1; it = fq.next()) {
+    __shared__ FlowTicketLds tl;
+    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4, &tl);
+    for (fq.first(); fq.more(); fq.next()) {
+        const int it = fq.item();
+        if (it >= it1) continue;  // (tickets: a last round's spare waves)
         const rsp::FacFlowItem f = a.fitems[it];
         const int *slot = a.fslots + f.off;
         const int rm = f.rmqm & 0xffff, qm = f.rmqm >> 16, pa = rsp::fac_pairs_at(rm);
@@ -752,6 +872,7 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, un
             for (int x = lane; x < nr; x += 64) flow_store(vals + rs + x, flow_publishable(rv[x]));
         }
     }
+    fq.finish();
 }
 
 // The whole factor of a pattern without update pairs (IluArgs::fac_one: a
@@ -1314,9 +1435,12 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, u
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     };
-    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4);
+    __shared__ FlowTicketLds tl;
+    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4, &tl);
     // claims are issued behind each item's first loads (task, term values and sources)
-    for (int it = fq.first(); it < it1; it = fq.next()) {
+    for (fq.first(); fq.more(); fq.next()) {
+        const int it = fq.item();
+        if (it >= it1) continue;  // (tickets: a last round's spare waves)
         const rsp::FlowItem f = a.plan.fitems[it];
         if (f.n > 0) {  // short rows, a lane each (lanes past them repeat the last row)
             const int r = min(lane, f.n - 1), x = f.x0 + r;
@@ -1387,6 +1511,7 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, u
             if (lane == 0) flow_store(y + t.i, s);
         }
     }
+    fq.finish();
 }
 
 // Thin run (levels cut into LDS-staged chunks [c0, c1)), one 1024-thread
@@ -2186,7 +2311,8 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
 // margin (it can overstate by one, MI355X_MICROARCH.md residency notes),
 // caps the requested grid.
 template <auto KERNEL>
-static int flow_grid(int want, int cus, int items) {
+static int flow_grid(const rsp::FlowCtl &fc, int want, int cus, int items) {
+    (void)fc;  // (start tickets need no residency; the same grid keeps the polling load of the static walk)
     static int occ = 0;  // per kernel
     if (occ == 0) {
         int nb = 0;
@@ -2200,6 +2326,7 @@ static int flow_grid(int want, int cus, int items) {
 // and the host mirror advanced by the claims it will make (rsp::FlowCtl).
 static unsigned long long flow_claims(const rsp::FlowCtl &fc, int items, int grid) {
     const unsigned long long base = *fc.claim_host;
+    if (fc.mode & rsp::kFlowTickets) return base;  // the launch restores the counter (FlowClaims::finish)
     if (!(fc.mode & rsp::kFlowClaims)) return base;  // static items: no claims
     *fc.claim_host = base + (unsigned long long)items + 2ull * 4ull * (unsigned long long)grid;
     return base;
@@ -2228,7 +2355,7 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
             while (fr < a.nfruns && a.fruns[fr].lb < l) ++fr;
             if (a.flow && fr < a.nfruns && a.fruns[fr].lb == l) {  // flow run: one persistent launch
                 const rsp::FacFlowRun r = a.fruns[fr];
-                const int grid = flow_grid<ilu0_flow<T>>(a.flow_grid, a.flow_cus, r.c1 - r.c0);
+                const int grid = flow_grid<ilu0_flow<T>>(a.fc, a.flow_grid, a.flow_cus, r.c1 - r.c0);
                 const unsigned long long base = flow_claims(a.fc, r.c1 - r.c0, grid);
                 hipLaunchKernelGGL((ilu0_flow<T>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, base);
                 ++flow_launched;
@@ -2291,7 +2418,7 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             continue;
         }
         if (a.flow && sg.c1 > sg.c0) {  // flow segment: one persistent launch
-            const int grid = flow_grid<trsv_flow<T, KIND>>(a.flow_grid, a.flow_cus, sg.c1 - sg.c0);
+            const int grid = flow_grid<trsv_flow<T, KIND>>(a.fc, a.flow_grid, a.flow_cus, sg.c1 - sg.c0);
             const unsigned long long base = flow_claims(a.fc, sg.c1 - sg.c0, grid);
             hipLaunchKernelGGL((trsv_flow<T, KIND>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1, base);
             continue;

@@ -1023,6 +1023,10 @@ static bool ilu_symbolic(int n, const hvec<int> &rp, const hvec<int> &ci,
     return true;
 }
 
+static void symbolic_row(int i, std::vector<int> &map, std::vector<int> &cur, std::vector<int> &order,
+                         const int *rp, const int *ci, const int *dpos, const int *hasdiag, int *cnt,
+                         const int *ptr, int *upd_l, int *upd_u, int *stage, int *lord, int *lend, int *udiv);
+
 // The symbolic factor of a few given rows on the host (the device analysis
 // leaves its long rows here: a hub row's lower positions form a long serial
 // chain that one GPU lane walks at global-memory latency, where the host
@@ -1034,11 +1038,26 @@ void symbolic_rows(const hvec<int> &rows, int n, const int *rp, const int *ci, c
                    int *lend, int *udiv) {
     if (rows.empty()) return;
     // rows in parallel (each writes only its own positions and update-list
-    // slots), each with its own column map (round 5: the hub rows were one
-    // sequential pass, ~1-1.7 ms per circuit, twice)
-    pfor_dyn((int)rows.size(), (long long)rows.size() << 14, 1 << 14, [&](int ri) {
-        const int i = rows[(size_t)ri];
+    // slots; round 5: the hub rows were one sequential pass, ~1-1.7 ms per
+    // circuit, twice), in blocks of rows: a block has ONE column map of n
+    // entries, reset after each row at the row's own columns only, so the
+    // pass stays O(nnz of the rows' DAG) plus O(n) per block (a map per row
+    // cost O(n) per long row: quadratic on patterns with many long rows)
+    const int nr = (int)rows.size();
+    const int nblk = std::max(1, std::min(nr, 2 * host_threads()));
+    pfor_dyn(nblk, (long long)nr << 14, 1 << 14, [&](int b) {
         std::vector<int> map((size_t)n, -1), cur, order;
+        for (int ri = (int)((long long)nr * b / nblk); ri < (int)((long long)nr * (b + 1) / nblk); ri++)
+            symbolic_row(rows[(size_t)ri], map, cur, order, rp, ci, dpos, hasdiag, cnt, ptr, upd_l, upd_u, stage,
+                         lord, lend, udiv);
+    });
+}
+
+// One row of symbolic_rows; `map` is all -1 on entry and on return.
+static void symbolic_row(int i, std::vector<int> &map, std::vector<int> &cur, std::vector<int> &order,
+                         const int *rp, const int *ci, const int *dpos, const int *hasdiag, int *cnt,
+                         const int *ptr, int *upd_l, int *upd_u, int *stage, int *lord, int *lend, int *udiv) {
+    {
         const int rs = rp[i], re = rp[i + 1], di = dpos[i];
         for (int p = rs; p < re; p++) map[(size_t)ci[p]] = p;
         if (cnt) {
@@ -1063,6 +1082,7 @@ void symbolic_rows(const hvec<int> &rows, int n, const int *rp, const int *ci, c
                 }
             }
         }
+        for (int p = rs; p < re; p++) map[(size_t)ci[p]] = -1;
         if (cnt) return;
         order.resize((size_t)(di - rs));
         for (int p = rs; p < di; p++) order[(size_t)(p - rs)] = p;
@@ -1077,7 +1097,7 @@ void symbolic_rows(const hvec<int> &rows, int n, const int *rp, const int *ci, c
             const int k = ci[p];
             udiv[p] = (p < di && hasdiag[k]) ? dpos[k] : -1;
         }
-    });
+    }
 }
 
 // The U DAG (extension: the true L.U apply, rsp_trsv_upper): row i waits
@@ -1626,6 +1646,9 @@ rsp_status_t plan_host(int n, const int *rp, const int *ci, long long slot_cap, 
         hp.sym.upd_u.swap(pu);
     }
     plan_rest(rp, ci, slot_cap, want_u, hp);
+    // block-inverse plans of the deep DAGs (as rsp_ilu0_analysis)
+    if (blocks_wanted(n, (int)hp.L.ptr.size() - 1)) hp.has_lb = plan_blocks(0, rp, ci, hp, hp.Lb);
+    if (blocks_wanted(n, (int)hp.LT.ptr.size() - 1)) hp.has_ltb = plan_blocks(1, rp, ci, hp, hp.LTb);
     lord.swap(hp.sym.lord);
     lend.swap(hp.sym.lend);
     udiv.swap(hp.udiv);
@@ -1687,6 +1710,21 @@ uint64_t digest(const IluHostPlan &hp) {
         f.vec(d->sp.nwave);
         f.vec(d->sp.sbase);
         f.vec(d->sp.fitems);
+    }
+    for (const BlkPlanHost *b : {&hp.Lb, &hp.LTb}) {
+        f.bytes(&b->nb, sizeof(b->nb));
+        f.bytes(&b->lds_elems, sizeof(b->lds_elems));
+        f.bytes(&b->lds_words, sizeof(b->lds_words));
+        f.vec(b->order);
+        f.vec(b->desc);
+        f.vec(b->rows);
+        f.vec(b->ref);
+        f.vec(b->vpos);
+        f.vec(b->eord);
+        f.vec(b->lptr);
+        f.vec(b->rptr);
+        f.vec(b->rit);
+        f.vec(b->segs);
     }
     f.bytes(&hp.fac_one, sizeof(hp.fac_one));
     f.bytes(&hp.fac_scale, sizeof(hp.fac_scale));

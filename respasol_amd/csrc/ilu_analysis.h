@@ -98,12 +98,29 @@ struct DagHost {
     bool planned = false;
 };
 
+// The block-inverse solve plan of a deep DAG (ilu_blocks.cpp; rsp::BlkDesc).
+struct BlkPlanHost {
+    int n = 0, nb = 0, nlong = 0, entries = 0;
+    int lds_elems = 0;  // coefficient build: LDS values (T) of the largest normal block
+    int lds_words = 0;  // ... and 32-bit words of its slot data (eord, rptr, recipe items, levels)
+    long long novf = 0; // long blocks' record overflow entries
+    hvec<int> order;    // position -> row
+    hvec<rsp::BlkDesc> desc;
+    hvec<rsp::BlkRow> rows;
+    hvec<int> ref, vpos, lptr, rptr;
+    hvec<unsigned> eord, rit;
+    hvec<rsp::BlkSeg> segs;
+};
+
 // Everything the analysis computes on the host.
 struct IluHostPlan {
     int n = 0, nnz_s = 0, structural_zero = -1;
     hvec<int> dpos, hasdiag, udiv;
     IluSymbolic sym;
     DagHost L, LT, U;
+    // block-inverse solve plans of L / L^T where the DAG is deep (blocks_wanted)
+    BlkPlanHost Lb, LTb;
+    bool has_lb = false, has_ltb = false;
     // The factor's level sets: L's, or ONE level holding every row (F, with
     // fac_one set) for a pattern without update pairs — a stored lower
     // triangle (the symmetric matrices' storage), where no position of any
@@ -187,6 +204,13 @@ void symbolic_rows(const hvec<int> &rows, int n, const int *rp, const int *ci, c
 // or unsorted pattern, ALLOC_FAILED if the update lists overflow int.
 rsp_status_t plan_host(int n, const int *rp, const int *ci, long long slot_cap_ints, bool want_u,
                        IluHostPlan &hp, Phases &ph);
+// Block-inverse solves (ilu_blocks.cpp): whether a DAG of n rows and nlev
+// levels gets one (RSP_ILU_BLOCKS: -1 auto = deep DAGs, <= 32 rows per level
+// on average; 0 never; 1 always), and its plan (kind 0: L, 1: L^T; needs the
+// DAG's levels, dpos and for L^T ltp / lts / ltc). false: no plan (the
+// level-scheduled solve runs).
+bool blocks_wanted(int n, int nlev);
+bool plan_blocks(int kind, const int *rp, const int *ci, const IluHostPlan &hp, BlkPlanHost &bp);
 // Build the U DAG's levels and solve plan (lazily, on first use).
 void plan_u(const int *rp, const int *ci, IluHostPlan &hp);
 // 64-bit digest (FNV-1a) of every array of the plan (tests: identical plans).

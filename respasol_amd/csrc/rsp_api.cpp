@@ -89,7 +89,8 @@ struct rsp_ilu0_info {
     int *d_upd_ptr, *d_upd_l, *d_upd_u, *d_lord, *d_lend, *d_udiv;
     // d_zero: [0] numerical zero pivot (atomicMin), [1] generation of the
     // last factor call whose flow wait gave up, [2..4] the same for the L,
-    // L^T and U solves (rsp::FlowCtl), [6..7] the flow claim counter
+    // L^T and U solves (rsp::FlowCtl), [5] the finished workgroups of a
+    // ticket launch, [6..7] the flow claim counter
     int *d_zero;
     unsigned long long claim_host = 0;  // flow claims issued (rsp::FlowCtl)
     int solve_gen[3] = {0, 0, 0};       // per solve kind: generation of the last call
@@ -114,6 +115,19 @@ struct rsp_ilu0_info {
         int batch = 8;                         // solve fma-chain batch
         int group = 4;                         // thin-run term groups (2 or 4)
     } L, LT, U, F;  // F: the factor's one level when fac_one (ptr, d_rows, d_ptr; rsp_an::IluHostPlan::F)
+    // block-inverse solve plans of deep L / L^T DAGs (rsp_an::plan_blocks,
+    // trsv_blocks.hip); on = false: the level-scheduled solve runs
+    struct BlkDag {
+        bool on = false;
+        int nb = 0, lds_elems = 0, lds_words = 0, entries = 0, nlong = 0;
+        rsp_an::hvec<rsp::BlkSeg> segs;  // host
+        int *d_order = nullptr, *d_ref = nullptr, *d_vpos = nullptr, *d_lptr = nullptr, *d_rptr = nullptr;
+        rsp::BlkDesc *d_desc = nullptr;
+        rsp::BlkRow *d_rows = nullptr;
+        unsigned *d_eord = nullptr, *d_rit = nullptr;
+        void *d_ev = nullptr, *d_yp = nullptr;  // scratch, fp64-sized
+        void *d_rc = nullptr;  // block records (fp64-sized: 64 x 144 B per block)
+    } Lb, LTb;
     bool fac_one = false, fac_scale = false;  // fac_scale: the factor is ilu0_scale_lower (IluHostPlan::fac_scale)
     const Dag &fdag() const { return fac_one ? F : L; }  // the factor's level sets
     rsp_an::hvec<rsp::LevelSeg> fac_segs;       // wave-per-row factor plan over fdag()
@@ -1196,6 +1210,8 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     f->d_ritems = nullptr;
     f->d_rpairs = f->d_rstaged = f->d_rrounds = nullptr;
     for (rsp_ilu0_info::Dag *d : {&f->L, &f->LT, &f->U, &f->F}) *d = rsp_ilu0_info::Dag();
+    f->Lb = rsp_ilu0_info::BlkDag();
+    f->LTb = rsp_ilu0_info::BlkDag();
     f->fac_one = f->fac_scale = false;
 }
 
@@ -1300,6 +1316,29 @@ static void dag_upload(Arena &ar, rsp_ilu0_info::Dag &d, const rsp_an::DagHost &
     ar.up(&d.d_sid, h.sp.sid);
     ar.up(&d.d_stg, h.sp.stg);
     ar.up(&d.d_fitems, h.sp.fitems);
+}
+
+// Upload a block-inverse solve plan (into the arena) with its scratch.
+static void blk_upload(Arena &ar, rsp_ilu0_info::BlkDag &d, const rsp_an::BlkPlanHost &h) {
+    d.on = true;
+    d.nb = h.nb;
+    d.lds_elems = h.lds_elems;
+    d.lds_words = h.lds_words;
+    d.entries = h.entries;
+    d.nlong = h.nlong;
+    d.segs = h.segs;
+    ar.up(&d.d_order, h.order);
+    ar.up(&d.d_desc, h.desc);
+    ar.up(&d.d_rows, h.rows);
+    ar.up(&d.d_ref, h.ref);
+    ar.up(&d.d_vpos, h.vpos);
+    ar.up(&d.d_eord, h.eord);
+    ar.up(&d.d_lptr, h.lptr);
+    ar.up(&d.d_rptr, h.rptr);
+    ar.up(&d.d_rit, h.rit);
+    ar.space(&d.d_ev, ((size_t)h.entries + 1) * sizeof(double));
+    ar.space(&d.d_yp, ((size_t)h.n + 1) * sizeof(double));  // (+ a spare cell, trsv_blk_seg)
+    ar.space(&d.d_rc, (size_t)h.nb * 64 * 144);
 }
 
 // Upload one DAG's per-row solve plan (L or L^T) into the arena and reserve
@@ -1661,10 +1700,20 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     std::unique_ptr<rsp_an::Task> solves;
     rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph, [&] {
         solves.reset(new rsp_an::Task([&] {
+            // block-inverse plans of the deep DAGs, beside the row plans
+            auto blk = [&](int kind) {
+                const rsp_an::DagHost &dg = kind == 0 ? hp->L : hp->LT;
+                if (!rsp_an::blocks_wanted(n, (int)dg.ptr.size() - 1)) return;
+                bool &has = kind == 0 ? hp->has_lb : hp->has_ltb;
+                has = rsp_an::plan_blocks(kind, rp.data(), ci.data(), *hp, kind == 0 ? hp->Lb : hp->LTb);
+            };
+            rsp_an::Task bl([&] { blk(0); }), bt([&] { blk(1); });
             if (dev_terms)
                 rsp_an::plan_solves_rows(rp.data(), ci.data(), *hp);
             else
                 rsp_an::plan_solves(rp.data(), ci.data(), *hp);
+            bl.join();
+            bt.join();
         }));
     });
     if (st == RSP_STATUS_SUCCESS) rsp_an::plan_factor(rp.data(), ci.data(), slot_cap_ints(), *hp);
@@ -1747,6 +1796,8 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
         dag_upload(ar, f->L, hp->L);
         dag_upload(ar, f->LT, hp->LT);
     }
+    if (hp->has_lb) blk_upload(ar, f->Lb, hp->Lb);
+    if (hp->has_ltb) blk_upload(ar, f->LTb, hp->LTb);
     // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
     const size_t nt = (size_t)std::max({f->L.nterms, f->LT.nterms, 1});
     ar.space(&f->d_sval, nt * sizeof(double));
@@ -1821,6 +1872,8 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     hp->L = rsp_an::DagHost();
     hp->LT = rsp_an::DagHost();
     hp->F = rsp_an::DagHost();
+    hp->Lb = rsp_an::BlkPlanHost();
+    hp->LTb = rsp_an::BlkPlanHost();
     hp->ltp.clear();
     hp->lts.clear();
     hp->ltc.clear();
@@ -1939,6 +1992,13 @@ rsp_status_t rsp_ilu0_plan_digest(rsp_ilu0_info_t f, uint64_t *digest) {
     return RSP_STATUS_SUCCESS;
 }
 
+rsp_status_t rsp_ilu0_solve_blocks(rsp_ilu0_info_t f, int *blocks_lower, int *blocks_upper) {
+    if (!f || !blocks_lower || !blocks_upper || !f->analysed) return RSP_STATUS_INVALID_VALUE;
+    *blocks_lower = f->Lb.on ? f->Lb.nb : 0;
+    *blocks_upper = f->LTb.on ? f->LTb.nb : 0;
+    return RSP_STATUS_SUCCESS;
+}
+
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t f, int *levels_lower, int *levels_upper) {
     if (!f || !f->analysed) return RSP_STATUS_INVALID_VALUE;
     if (levels_lower) *levels_lower = (int)f->L.ptr.size() - 1;
@@ -1985,6 +2045,39 @@ static LaterSolves later_solves(const rsp_ilu0_info *f, long long seq) {
     std::sort(l.w, l.w + l.k, [&](int a, int b) { return f->last_solve[a].seq < f->last_solve[b].seq; });
     return l;
 }
+// Whether a re-run of `first` (a solve kind, or -1 for the factor) and then
+// of the solves `l` reads the inputs the original calls read: no recorded
+// call after a re-run call may have written (its y) over that call's x or
+// values. The ping-pong pattern (L solve r -> z, then L^T z -> r) overwrites
+// the L solve's x, so its re-run would read the L^T result: not recoverable.
+static bool overlaps(const void *a, size_t na, const void *b, size_t nb) {
+    const char *p = (const char *)a, *q = (const char *)b;
+    return p && q && p < q + nb && q < p + na;
+}
+static bool rerun_inputs_intact(const rsp_ilu0_info *f, int first, const LaterSolves &l) {
+    int seq[4], k = 0;
+    if (first >= 0) seq[k++] = first;
+    for (int j = 0; j < l.k; j++) seq[k++] = l.w[j];
+    for (int a = 0; a < k; a++) {
+        const rsp_ilu0_info::SolveCall &c = f->last_solve[seq[a]];
+        const size_t ny = (size_t)f->n * elem_size(c.type), nv = (size_t)f->nnz_s * elem_size(c.type);
+        for (int b = a + 1; b < k; b++) {
+            const rsp_ilu0_info::SolveCall &d = f->last_solve[seq[b]];
+            if (overlaps(d.y, (size_t)f->n * elem_size(d.type), c.x, ny) ||
+                overlaps(d.y, (size_t)f->n * elem_size(d.type), c.vals, nv))
+                return false;
+        }
+    }
+    if (first < 0 && f->last_fac.valid)  // the factor's values are restored from the copy, but a
+        for (int a = 0; a < k; a++) {    // later solve must not have written into them
+            const rsp_ilu0_info::SolveCall &d = f->last_solve[seq[a]];
+            if (overlaps(d.y, (size_t)f->n * elem_size(d.type), f->last_fac.vals,
+                         (size_t)f->nnz_s * elem_size(f->last_fac.type)))
+                return false;
+        }
+    return true;
+}
+
 static rsp_status_t rerun_solves(rsp_handle_t h, rsp_ilu0_info *f, const LaterSolves &l) {
     for (int j = 0; j < l.k; j++) {
         const rsp_status_t st = rerun_solve(h, f, l.w[j]);
@@ -2007,10 +2100,11 @@ rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int *positio
     // again without flow launches; else reported.
     if (f->factored && f->fac_gen > 0 && z[1] == f->fac_gen) {
         if (!f->last_fac.valid || !flow_recover()) return RSP_STATUS_EXECUTION_FAILED;
+        const LaterSolves later = later_solves(f, f->last_fac.seq);
+        if (!rerun_inputs_intact(f, -1, later)) return RSP_STATUS_EXECUTION_FAILED;
         f->last_fac.valid = 0;
         RSP_CHECK_HIP(hipMemcpyAsync(f->last_fac.vals, f->d_fbackup, (size_t)f->nnz_s * elem_size(f->last_fac.type),
                                      hipMemcpyDeviceToDevice, h->stream));
-        const LaterSolves later = later_solves(f, f->last_fac.seq);
         const int ftz = h->ftz;
         h->ftz = f->last_fac.ftz;  // the mode of the call being re-run
         rsp_status_t st = ilu_factor_run(h, f, f->last_fac.type, f->last_fac.vals, false);
@@ -2046,6 +2140,7 @@ rsp_status_t rsp_trsv_zero_pivot(rsp_handle_t h, rsp_ilu0_info_t f, int which, i
     if (g > 0 && z[2 + which] == g) {  // recovered: the solve (and the solves after it) run again
         if (!f->last_solve[which].valid || !flow_recover()) return RSP_STATUS_EXECUTION_FAILED;
         const LaterSolves later = later_solves(f, f->last_solve[which].seq);
+        if (!rerun_inputs_intact(f, which, later)) return RSP_STATUS_EXECUTION_FAILED;
         rsp_status_t st = rerun_solve(h, f, which);
         if (st == RSP_STATUS_SUCCESS) st = rerun_solves(h, f, later);
         if (st != RSP_STATUS_SUCCESS) return st;
@@ -2073,8 +2168,9 @@ static rsp::FlowCtl flow_ctl(rsp_ilu0_info *f, int word, int gen) {
     const long long us = std::max(env_int("RSP_ILU_FLOW_TIMEOUT_US", 200000), 0);
     c.ticks = (unsigned long long)us * 100ull;  // 100 MHz wall clock
     c.claim = reinterpret_cast<unsigned long long *>(f->d_zero + 6);
+    c.exits = f->d_zero + 5;
     c.claim_host = &f->claim_host;
-    c.mode = env_int("RSP_ILU_FLOW_MODE", 0);
+    c.mode = env_int("RSP_ILU_FLOW_MODE", rsp::kFlowTickets);
     return c;
 }
 
@@ -2313,6 +2409,37 @@ static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op,
     const bool f64 = value_type == RSP_R_64F, ftz = h->ftz != 0;
     if (op != RSP_OPERATION_NON_TRANSPOSE && op != RSP_OPERATION_TRANSPOSE) return RSP_STATUS_INVALID_VALUE;
     RSP_CHECK_HIP(trsv_begin(h, f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, a));
+    // a deep DAG: the block-inverse solve (trsv_blocks.hip; RSP_ILU_BLOCKS=0
+    // at solve time runs the level-scheduled solve of the same analysis)
+    const rsp_ilu0_info::BlkDag &bd = op == RSP_OPERATION_NON_TRANSPOSE ? f->Lb : f->LTb;
+    if (bd.on && env_int("RSP_ILU_BLOCKS", -1) != 0) {
+        rsp::BlkArgs b{};
+        b.n = f->n;
+        b.nb = bd.nb;
+        b.order = bd.d_order;
+        b.desc = bd.d_desc;
+        b.rows = bd.d_rows;
+        b.ref = bd.d_ref;
+        b.vpos = bd.d_vpos;
+        b.eord = bd.d_eord;
+        b.lptr = bd.d_lptr;
+        b.rptr = bd.d_rptr;
+        b.rit = bd.d_rit;
+        b.segs = bd.segs.data();
+        b.nseg = (int)bd.segs.size();
+        b.lds_elems = bd.lds_elems;
+        b.lds_words = bd.lds_words;
+        b.rc = bd.d_rc;
+        b.vals = d_values;
+        b.x = d_x;
+        b.y = d_y;
+        b.alpha = a.alpha;
+        b.ev = bd.d_ev;
+        b.yp = bd.d_yp;
+        e = f64 ? rsp_k::trsv_blocks_f64(b, h->stream)
+                : (ftz ? rsp_k_ftz::trsv_blocks_f32(b, h->stream) : rsp_k::trsv_blocks_f32(b, h->stream));
+        return e == hipSuccess ? RSP_STATUS_SUCCESS : RSP_STATUS_EXECUTION_FAILED;
+    }
     if (op == RSP_OPERATION_NON_TRANSPOSE) {
         e = f64 ? rsp_k::trsv_lower_n_f64(a, h->stream)
                 : (ftz ? rsp_k_ftz::trsv_lower_n_f32(a, h->stream) : rsp_k::trsv_lower_n_f32(a, h->stream));

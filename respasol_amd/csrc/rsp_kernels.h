@@ -295,10 +295,21 @@ struct FacFlowRun {
     int lb, le, c0, c1;
 };
 
-// Flow launches (ilu0_flow, trsv_flow): one persistent launch over a run of
-// work items in level order; an item waits only for items of lower index.
+// Flow launches (ilu0_flow, trsv_flow): one launch over a run of work items
+// in level order; an item waits only for items of lower index.
 // Item assignment (FlowCtl::mode):
-//  * static (default): wave w of the grid takes items w, w + W, ... Progress
+//  * start tickets (kFlowTickets, the default, RSP_ILU_FLOW_MODE=2): the
+//    workgroups take tickets in the order they run (ONE agent-scope
+//    fetch_add per workgroup per round of four items, claimed a round ahead;
+//    ilu0.hip FlowClaims) and a ticket's waves run its four items. An item
+//    waits only on items of lower tickets, all held by workgroups that have
+//    started: the lowest unfinished item always belongs to a running
+//    workgroup, and a workgroup that cannot be scheduled yet holds no ticket
+//    anybody waits on. Progress needs no co-residency at all (a co-running
+//    kernel that holds all but a few CUs only slows the launch down). A
+//    launch of G workgroups over T = ceil(items / 4) tickets advances the
+//    counter by exactly T + 2 G (flow_claims on the host);
+//  * static (RSP_ILU_FLOW_MODE=0): wave w of the grid takes items w, w + W, ... Progress
 //    needs every workgroup of the grid resident together: the grid is sized
 //    from the occupancy query (one 4-wave workgroup per CU by default), and
 //    a wait that outlasts `ticks` gives up and is REPORTED (below), so a
@@ -322,10 +333,12 @@ struct FlowCtl {
     int gen;                          // this call's generation (>= 1)
     unsigned long long ticks;         // give-up bound (RSP_ILU_FLOW_TIMEOUT_US)
     unsigned long long *claim;        // device claim counter
+    int *exits;                       // device: workgroups of a ticket launch that have finished (0 between launches)
     unsigned long long *claim_host;   // host: claims issued by the launches enqueued so far
-    int mode;                         // RSP_ILU_FLOW_MODE: 0 static items, kFlowClaims claimed items
+    int mode;                         // RSP_ILU_FLOW_MODE: 0 static items, kFlowClaims claimed items, kFlowTickets start tickets
 };
 constexpr int kFlowClaims = 1;
+constexpr int kFlowTickets = 2;
 
 
 struct IluArgs {
@@ -379,6 +392,59 @@ struct IluArgs {
     int fac_one;
 };
 
+// Block-inverse solve of a deep DAG (round 6; plan: ilu_blocks.cpp, kernels:
+// trsv_blocks.hip). The rows in level order ("positions") are cut into
+// chunks of kBlkWin positions and, inside a chunk, into blocks of <=
+// kBlkRows rows; every row's unknown is a combination (its PATTERN: x
+// sources, the block's right-hand sides, then y sources, earlier blocks'
+// unknowns, each ascending by position) with coefficients E — the block's
+// partitioned inverse, built by the solve from the factor's values
+// (trsv_blk_coef). A row's y terms of EARLIER chunks are summed by a parallel
+// prologue per chunk (with its x terms); its y terms of its OWN chunk
+// (<= kBlkNear for a normal row) are one short fma chain on the chunk's LDS
+// window, so a normal block is one dependent step of one wave (lane = row).
+// A LONG block is one row whose pattern breaks the caps (a circuit's hub
+// row): its terms are summed by a whole wave.
+constexpr int kBlkRows = 64, kBlkYMax = 32, kBlkNear = 12, kBlkNearWin = 1 << 30, kBlkWin = 16384;
+constexpr int kBlkLongCap = 64 * kBlkNear;  // a long row's in-chunk terms (one record); more start a chunk
+constexpr int kBlkPre = 6;  // records in flight in the chunk walk (trsv_blk_seg)
+struct alignas(16) BlkDesc {
+    int p0, np, kind, kn;     // first position, rows, 0 normal / 1 long, in-chunk terms (rounds: long)
+    int eoff, ne, doff, nd;   // its pattern entries (and coefficient slots), its dependencies
+    int loff, nlev, ovf, pad; // coefficient build: level ranges at lptr[loff ..], intra-block levels;
+                              // ovf: a long block's record overflow offset
+};
+struct alignas(16) BlkRow {
+    int off, nx, ny, nfar;    // pattern entries [off, off + nx + ny): x, far y, near y
+};
+struct BlkSeg {
+    int b0, b1, p0, p1;       // blocks [b0, b1) = positions [p0, p1)
+};
+struct BlkArgs {
+    int n, nb;
+    const int *order;         // position -> row
+    const BlkDesc *desc;
+    const BlkRow *rows;       // per position
+    const int *ref;           // per entry: x source -> its row (x index); y source -> its position
+    const int *vpos;          // per dependency (block order): position of its value
+    const unsigned *eord;     // per coefficient slot (intra-block level order): entry | init 1 << 31
+    const int *lptr;          // per block, nlev + 1 slot offsets
+    const int *rptr;          // per slot: its recipe items [rptr[k], rptr[k + 1])
+    const unsigned *rit;      // recipe item: dependency << 16 | source (0: the constant 1, else entry + 1); long blocks: dependency
+    const BlkSeg *segs;       // host
+    int nseg;
+    int lds_elems;            // coefficient build: LDS values (T) of the largest normal block
+    int lds_words;            // ... and LDS words (32-bit) of its slot data
+    const void *vals, *x;
+    void *y;
+    double alpha;
+    void *ev, *yp;            // scratch: coefficients (per entry), y by position
+    // block records (trsv_blk_pro -> trsv_blk_seg): per block 64 lane records
+    // (trsv_blocks.hip BlkLane: the lane's sum so far, its in-chunk
+    // coefficients and window slots, its position; 144 / 96 B for fp64 / fp32)
+    void *rc;
+};
+
 struct TrsvArgs {
     int n;
     const int *rowptr;
@@ -418,6 +484,7 @@ struct TrsvArgs {
     hipError_t trsv_lower_n_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
     hipError_t trsv_lower_t_f32(const rsp::TrsvArgs &a, hipStream_t s);                         \
     hipError_t trsv_upper_f32(const rsp::TrsvArgs &a, hipStream_t s);                           \
+    hipError_t trsv_blocks_f32(const rsp::BlkArgs &a, hipStream_t s);                           \
     void warm_spmv();                                                                           \
     void warm_ilu();                                                                            \
     }
@@ -441,6 +508,7 @@ hipError_t ilu0_factor_f64(const rsp::IluArgs &a, hipStream_t s);
 hipError_t trsv_lower_n_f64(const rsp::TrsvArgs &a, hipStream_t s);
 hipError_t trsv_lower_t_f64(const rsp::TrsvArgs &a, hipStream_t s);
 hipError_t trsv_upper_f64(const rsp::TrsvArgs &a, hipStream_t s);
+hipError_t trsv_blocks_f64(const rsp::BlkArgs &a, hipStream_t s);
 // Writes the slots of the fat factor levels (rsp::FacSlotLevel layout) from
 // the symbolic arrays already on the device: one workgroup per slot row,
 // desc[t] = {level-order slot x, rm, qm, 0}, offs[t] = its slot's offset.

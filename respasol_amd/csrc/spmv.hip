@@ -305,18 +305,20 @@ __device__ __forceinline__ void reduce_rows(const T *lds, const unsigned short *
                 if (lane == 0) hl[atomicAdd(hn, 1)] = rr;
             } else {
                 // branch-free: every step issues its NA loads together
-                // (clamped into the row) and adds a product or +0 (exact: a
-                // partial that starts at +0 is never -0). A predicated load
-                // per product made the compiler wait on each one, so a
-                // 256-entry row in a tile of short rows held its workgroup
-                // ~8 us (scripts/percall_probe.py).
+                // (clamped into the row) and a slot past the row keeps its
+                // partial by a select (one v_cndmask), not by adding +0: under
+                // FTZ a partial can be -0 (a negative denormal sum flushed),
+                // and -0 + +0 is +0 where the canonical order has no add. A
+                // predicated load per product made the compiler wait on each
+                // one, so a 256-entry row in a tile of short rows held its
+                // workgroup ~8 us (scripts/percall_probe.py).
                 for (int base = a0 + lane; base < a1; base += 8) {
                     T v[NA];
 #pragma unroll
                     for (int t = 0; t < NA; ++t) v[t] = lds[min(base + t * L, last)];
 #pragma unroll
                     for (int t = 0; t < NA; ++t)  // partial (lane + t*L) of the row
-                        acc[t] += base + t * L < a1 ? v[t] : T(0);
+                        acc[t] = base + t * L < a1 ? acc[t] + v[t] : acc[t];
                 }
             }
         }
@@ -355,7 +357,7 @@ __device__ __forceinline__ void reduce_heavy_rows(const T *lds, const unsigned s
 #pragma unroll
                 for (int t = 0; t < 4; ++t) v[t] = lds[min(base + 8 * t, last)];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) acc += base + 8 * t < a1 ? v[t] : T(0);
+                for (int t = 0; t < 4; ++t) acc = base + 8 * t < a1 ? acc + v[t] : acc;  // (select: see reduce_rows)
             }
         }
 #pragma unroll
@@ -422,6 +424,14 @@ __device__ __forceinline__ T reduce_long(const T *lds, int a, int e, T *wsum) {
 // they were ~1.7 us each). The last arriver's lanes load the partials in
 // parallel (lane c: partial c), one memory round trip instead of one per
 // chunk, and the in-order sum runs on shuffles.
+// The relaxed form above relies on gfx9-family ordering (LLVM AMDGPU memory
+// model, GFX942/GFX950 rows: stores are counted by vmcnt, and agent-scope
+// (sc1) stores write through and sc1 loads bypass the non-coherent caches).
+// gfx10+ counts stores in a separate vscnt, so this file builds for gfx950
+// only (the library's one target).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "longrow_arrive's relaxed hand-off is only valid on gfx942 / gfx950"
+#endif
 template <typename T>
 __device__ __forceinline__ void longrow_arrive(const SpmvBlock blk, const int *__restrict__ rowptr,
                                                T *partials, T *__restrict__ y, T t, T alpha, T beta,

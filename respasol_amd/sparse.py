@@ -277,6 +277,12 @@ class Ilu0:
         check(rsp.rsp_ilu0_levels(self._info, C.byref(lo), C.byref(up)), "rsp_ilu0_levels")
         return lo.value, up.value
 
+    def solve_blocks(self) -> tuple[int, int]:
+        """Blocks of the block-inverse L / L^T solves (0: level-scheduled)."""
+        lo, up = C.c_int(), C.c_int()
+        check(rsp.rsp_ilu0_solve_blocks(self._info, C.byref(lo), C.byref(up)), "rsp_ilu0_solve_blocks")
+        return lo.value, up.value
+
     def factor(self, values: torch.Tensor) -> None:
         check(rsp.rsp_ilu0_factor(self.handle.ptr, self._info, _DT[values.dtype], _ptr(values)),
               "rsp_ilu0_factor")

@@ -41,6 +41,12 @@ def _load():
         f = getattr(lib, f"oracle_trsv_{n}_f32")
         f.argtypes = [C.c_int, ip, ip, vp, C.c_float, vp, vp, C.c_int]
         f.restype = None
+    lib.oracle_dag_levels.argtypes = [C.c_int, C.c_int, ip, ip]
+    lib.oracle_dag_levels.restype = C.c_int
+    lib.oracle_trsv_blocks_f64.argtypes = [C.c_int, C.c_int, ip, ip, vp, C.c_double, vp, vp, vp]
+    lib.oracle_trsv_blocks_f64.restype = C.c_int
+    lib.oracle_trsv_blocks_f32.argtypes = [C.c_int, C.c_int, ip, ip, vp, C.c_float, vp, vp, vp, C.c_int]
+    lib.oracle_trsv_blocks_f32.restype = C.c_int
     lib.oracle_dlarnv.argtypes = [C.c_int, ip, C.c_int, vp]
     lib.oracle_dlarnv.restype = C.c_int
     return lib
@@ -94,15 +100,39 @@ def ilu0(rowptr, colidx, vals, ftz=False):
     return v, s, zp.value
 
 
+def dag_levels(kind, rowptr, colidx):
+    """Levels of the L (kind 0) or L^T (kind 1) DAG."""
+    rp = np.ascontiguousarray(rowptr, np.int32)
+    ci = np.ascontiguousarray(colidx, np.int32)
+    return lib.oracle_dag_levels(kind, rp.shape[0] - 1, rp.ctypes.data_as(C.POINTER(C.c_int)),
+                                 ci.ctypes.data_as(C.POINTER(C.c_int)))
+
+
+def blocks_wanted(kind, rowptr, colidx):
+    """The product's rule for a block-inverse solve of that DAG
+    (rsp_an::blocks_wanted, ilu_blocks.cpp): RSP_ILU_BLOCKS -1 (default) for
+    DAGs of <= 32 rows per level on average, 1 always, 0 never."""
+    mode = int(os.environ.get("RSP_ILU_BLOCKS", "-1") or "-1")
+    n = len(rowptr) - 1
+    if mode == 0 or n <= 0:
+        return False
+    return mode > 0 or n <= 32 * dag_levels(kind, rowptr, colidx)
+
+
 def trsv(kind, rowptr, colidx, vals, x, alpha=1.0, ftz=False):
     """kind in {'lower_n', 'lower_t', 'upper', 'lower_n_ref', 'lower_t_ref',
-    'lower_n_split', 'lower_t_split'}. '*_ref' is the reference's own order
-    (L: column ascending; L^T: the column sweep), '*_split' the split order
-    (a row's terms from the level just below it applied last, rsp_oracle.c
-    ORACLE_TRSV_SPLIT); 'lower_n' / 'lower_t' follow the product's plan
-    order: the reference's, or the split one where RSP_ILU_SPLIT=1 is set
-    (the analysis knob)."""
+    'lower_n_split', 'lower_t_split', 'lower_n_blocks', 'lower_t_blocks'}.
+    '*_ref' is the reference's own order (L: column ascending; L^T: the
+    column sweep), '*_split' the split order (a row's terms from the level
+    just below it applied last, rsp_oracle.c ORACLE_TRSV_SPLIT), '*_blocks'
+    the block-inverse order of the deep-DAG solve (ORACLE_BLOCKS, round 6);
+    'lower_n' / 'lower_t' follow the product's plan order: the block order
+    where the product plans blocks for that DAG (blocks_wanted), else the
+    reference's, or the split one where RSP_ILU_SPLIT=1 is set (the analysis
+    knobs)."""
     split = os.environ.get("RSP_ILU_SPLIT", "0") not in ("", "0")
+    if kind in ("lower_n", "lower_t") and blocks_wanted(0 if kind == "lower_n" else 1, rowptr, colidx):
+        kind += "_blocks"
     kind = {"lower_n": "lower_n_split" if split else "lower_n",
             "lower_t": "lower_t_split" if split else "lower_t",
             "lower_n_ref": "lower_n", "lower_t_ref": "lower_t"}.get(kind, kind)
@@ -112,6 +142,19 @@ def trsv(kind, rowptr, colidx, vals, x, alpha=1.0, ftz=False):
     xx = np.ascontiguousarray(x, v.dtype)
     n = rp.shape[0] - 1
     y = np.empty(n, v.dtype)
+    if kind.endswith("_blocks"):
+        bk = 0 if kind == "lower_n_blocks" else 1
+        if v.dtype == np.float64:
+            r = lib.oracle_trsv_blocks_f64(bk, n, rp.ctypes.data_as(C.POINTER(C.c_int)),
+                                           ci.ctypes.data_as(C.POINTER(C.c_int)), v.ctypes.data, alpha,
+                                           xx.ctypes.data, y.ctypes.data, None)
+        else:
+            r = lib.oracle_trsv_blocks_f32(bk, n, rp.ctypes.data_as(C.POINTER(C.c_int)),
+                                           ci.ctypes.data_as(C.POINTER(C.c_int)), v.ctypes.data, alpha,
+                                           xx.ctypes.data, y.ctypes.data, None, 1 if ftz else 0)
+        if r < 0:
+            raise ValueError("oracle_trsv_blocks: bad arguments")
+        return y
     if v.dtype == np.float64:
         getattr(lib, f"oracle_trsv_{kind}_f64")(n, rp.ctypes.data_as(C.POINTER(C.c_int)),
                                                 ci.ctypes.data_as(C.POINTER(C.c_int)), v.ctypes.data,

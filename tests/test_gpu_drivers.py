@@ -310,7 +310,9 @@ def test_ilu0_driver_flow_give_up_exits_nonzero():
     factor; with recovery on (default) the zero-pivot check re-runs the call
     without flow launches and the driver succeeds; the normal bound runs clean."""
     # (RSP_ILU_FAC_ONE=0: G2_circuit's factor over L's levels, with flow runs)
-    env = dict(os.environ, RSP_ILU_THIN_FACTOR="0", RSP_ILU_THIN_SOLVE="0", RSP_ILU_FAC_ONE="0")
+    # (RSP_ILU_BLOCKS=0: the solves level-scheduled too, with flow launches)
+    env = dict(os.environ, RSP_ILU_THIN_FACTOR="0", RSP_ILU_THIN_SOLVE="0", RSP_ILU_FAC_ONE="0",
+               RSP_ILU_BLOCKS="0")
     exe = os.path.join(BIN, "test_ilu0")
     r = subprocess.run([exe, "surrogate:G2_circuit@0.1"], capture_output=True, text=True, timeout=300,
                        env=dict(env, RSP_ILU_FLOW_TIMEOUT_US="0", RSP_ILU_FLOW_RECOVER="0"))

@@ -21,6 +21,15 @@ NP = {torch.float64: np.float64, torch.float32: np.float32}
 TOL = {torch.float64: (1e-13, 1e-12), torch.float32: (1e-5, 1e-4)}
 
 
+@pytest.fixture(autouse=True)
+def level_scheduled_solves(monkeypatch):
+    """This file holds the level-scheduled kernels (thin runs, flow launches,
+    fat levels) to the reference-order oracle: every analysis here plans
+    level-scheduled solves (RSP_ILU_BLOCKS=0). The block-inverse solves of
+    deep DAGs, the default there since round 6, are tests/test_gpu_blocks.py."""
+    monkeypatch.setenv("RSP_ILU_BLOCKS", "0")
+
+
 @pytest.fixture(scope="module")
 def handle():
     assert torch.cuda.is_available(), "GPU tests need the MI355X"
@@ -438,15 +447,17 @@ def test_narrow_runs_two_levels_per_turn(handle, monkeypatch, waves, group, pair
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
-@pytest.mark.parametrize("flow,wpc,mode", [(0, 8, 0), (1, 4, 0), (1, 8, 0), (1, 16, 0), (1, 4, 1), (1, 16, 1)])
+@pytest.mark.parametrize("flow,wpc,mode", [(0, 8, 0), (1, 4, 0), (1, 8, 0), (1, 16, 0), (1, 4, 1), (1, 16, 1),
+                                           (1, 4, 2)])
 @pytest.mark.parametrize("name,scale", [("xenon2", 0.3), ("offshore", 0.2), ("cfd2", 0.3), ("ss1", 0.2)])
 def test_flow_segments(handle, monkeypatch, flow, wpc, mode, name, scale):
     """Fat solve segments and fat factor levels as one persistent launch each
     (trsv_flow: items start when the y they read exist, read from y itself;
     ilu0_flow: rows start when the u values they read exist, read from the
     values themselves) or a launch per level, 1-4 workgroups per CU, items
-    walked statically (mode 0) or claimed from the flow counter (mode 1):
-    bitwise equal to the oracle for the factor, L, L^T and U."""
+    walked statically (mode 0), claimed from the flow counter (mode 1) or by
+    workgroup start tickets (mode 2, the default): bitwise equal to the
+    oracle for the factor, L, L^T and U."""
     monkeypatch.setenv("RSP_ILU_FLOW", str(flow))
     monkeypatch.setenv("RSP_ILU_FLOW_WPC", str(wpc))
     monkeypatch.setenv("RSP_ILU_FLOW_MODE", str(mode))
@@ -540,16 +551,19 @@ TESTKIT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
                        "librsp_testkit.so")
 
 
-@pytest.mark.parametrize("hog_us,bound_us,recover", [(50000, 200000, 1), (100000, 5000, 1), (100000, 5000, 0)])
-def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us, recover):
-    """the factor and both solves (default schedule, flow runs
-    included) beside a kernel on another stream that holds all but 8 CUs —
-    one 1024-thread workgroup per CU with the CU's whole LDS, bounded by the
-    wall clock (librsp_testkit.so, test-only). (Half the CUs is not enough to
-    matter: a flow grid of one 4-wave workgroup per CU fits, several per CU,
-    on the free half, so nothing waits.) A 50 ms occupant inside the
-    give-up bound: the flow waves wait, then SUCCESS and the oracle's bits. A
-    100 ms occupant past a 5 ms bound: the waits give up; with recovery the
+@pytest.mark.parametrize("hog_us,bound_us,recover,mode", [(50000, 200000, 1, 2), (100000, 5000, 0, 2),
+                                                        (100000, 5000, 1, 0), (100000, 5000, 0, 0)])
+def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us, recover, mode):
+    """the factor and both solves (default
+    schedule, flow runs included) beside a kernel on another stream that holds
+    all but 8 CUs — one 1024-thread workgroup per CU with the CU's whole LDS,
+    bounded by the wall clock (librsp_testkit.so, test-only).
+    Start tickets (mode 2, the default): a flow workgroup waits only on
+    workgroups that started before it, so the launch runs on the 8 free CUs:
+    SUCCESS and the oracle's bits with recovery OFF, even with a 5 ms wait
+    bound under a 100 ms occupant — nothing waits for the occupant.
+    The static walk (mode 0) needs its whole grid resident: under the 100 ms
+    occupant its waits give up past a 5 ms bound; with recovery the
     zero-pivot calls re-run the calls without flow launches (SUCCESS, the
     oracle's bits), without it the factor reports EXECUTION_FAILED — which
     shows the occupant really kept flow workgroups off the CUs."""
@@ -560,6 +574,7 @@ def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us,
     tk.rsp_testkit_occupy.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong]
     monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", str(bound_us))
     monkeypatch.setenv("RSP_ILU_FLOW_RECOVER", str(recover))
+    monkeypatch.setenv("RSP_ILU_FLOW_MODE", str(mode))
     # offshore is a stored lower triangle: its factor runs over L's levels
     # here (RSP_ILU_FAC_ONE=0) so that it has flow runs to block
     monkeypatch.setenv("RSP_ILU_FAC_ONE", "0")
@@ -577,7 +592,7 @@ def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us,
     time.sleep(0.01)  # the occupant is resident before the factor's launches
     with torch.cuda.stream(main):
         il.factor(va)
-        if not recover:
+        if mode == 0 and not recover:
             with pytest.raises(RspError) as e:
                 il.zero_pivot()
             assert e.value.status == STATUS_EXECUTION_FAILED
@@ -595,4 +610,39 @@ def test_flow_launches_beside_an_occupying_kernel(monkeypatch, hog_us, bound_us,
     torch.cuda.synchronize()
     rv, _, _, rz, ry = oracle_ilu(A, torch.float64)
     assert np.array_equal(va.cpu().numpy(), rv)
+    assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)
+
+
+def test_flow_recovery_refuses_overwritten_inputs(handle, monkeypatch):
+    """a recovery re-runs the recorded solves from their recorded
+    buffers, so it must not run when a later recorded solve wrote over one of
+    them. The ping-pong pattern — L: r -> z, then L^T: z -> r — overwrites
+    the L solve's x; with forced give-ups (static walk, zero bound) the L
+    solve's status is EXECUTION_FAILED instead of a silently wrong re-run.
+    With separate buffers the same sequence recovers (the oracle's bits)."""
+    from respasol_amd._lib import STATUS_EXECUTION_FAILED, RspError
+    monkeypatch.setenv("RSP_ILU_THIN_FACTOR", "0")
+    monkeypatch.setenv("RSP_ILU_THIN_SOLVE", "0")
+    monkeypatch.setenv("RSP_ILU_FAC_ONE", "0")
+    monkeypatch.setenv("RSP_ILU_FLOW_MODE", "0")
+    A = csr.surrogate("G2_circuit", 0.1)
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
+    il = Ilu0(handle, rp, ci, nnz=A.nnz)
+    il.analysis()
+    il.factor(va)
+    assert il.zero_pivot() == -1
+    monkeypatch.setenv("RSP_ILU_FLOW_TIMEOUT_US", "0")
+    r = torch.ones(A.n, dtype=torch.float64, device="cuda")
+    z = torch.empty_like(r)
+    il.solve_lower(va, r, y=z)
+    il.solve_lower(va, z, y=r, transpose=True)  # writes over the L solve's x
+    with pytest.raises(RspError) as e:
+        il.solve_zero_pivot(il.TRSV_L)
+    assert e.value.status == STATUS_EXECUTION_FAILED
+    r = torch.ones(A.n, dtype=torch.float64, device="cuda")
+    z = il.solve_lower(va, r)
+    y = il.solve_lower(va, z, transpose=True)
+    assert il.solve_zero_pivot(il.TRSV_L) == -1
+    assert il.solve_zero_pivot(il.TRSV_LT) == -1
+    _, _, _, rz, ry = oracle_ilu(A, torch.float64)
     assert np.array_equal(z.cpu().numpy(), rz) and np.array_equal(y.cpu().numpy(), ry)

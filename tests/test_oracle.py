@@ -154,7 +154,7 @@ def test_fp32_solve_fuses_with_one_rounding():
     rp = np.array([0, 1, 3], np.int32)
     ci = np.array([0, 0, 1], np.int32)
     v = np.array([1.0, -a, 1.0], np.float32)  # L = [[1, 0], [-a, 1]]
-    z = ob.trsv("lower_n", rp, ci, v, np.array([b, c], np.float32))
+    z = ob.trsv("lower_n_ref", rp, ci, v, np.array([b, c], np.float32))
     assert z[0] == b
     assert z[1] == np.float32(1 + 2.0 ** -23)
     assert np.float32(np.float64(c) + np.float64(a) * np.float64(b)) == np.float32(1 + 2.0 ** -22)
@@ -186,3 +186,49 @@ def test_split_order_solves_within_tolerance(name, scale):
             b = ob.trsv(k + "_ref", A.rowptr, A.colidx, vv, xx).astype(np.float64)
             assert np.linalg.norm(a - b) <= tol * np.linalg.norm(b)
             assert np.mean(a == b) > 0.5
+
+
+@pytest.mark.parametrize("name,scale", [("dc1", 0.2), ("G2_circuit", 0.2), ("matrix-new_3", 0.2), ("xenon2", 0.03),
+                                        ("ASIC_320ks", 0.05), ("ecology2", 0.02)])
+def test_block_order_solves_within_tolerance(name, scale):
+    """The block-inverse order of the deep-DAG solves (round 6,
+    oracle_trsv_blocks_*: each block's unknowns as combinations of its
+    right-hand sides and of earlier blocks' unknowns) against the reference's
+    own order: same unknowns, rounding only — normwise within SURVEY 8c's
+    1e-12 (fp64) and 1e-4 (fp32), for L and L^T, alpha = 1 and a scaled
+    alpha."""
+    A = csr.surrogate(name, scale)
+    v, _, _ = ob.ilu0(A.rowptr, A.colidx, A.values)
+    x = csr.dlarnv(2, [0, 0, 0, 1], A.n)[0]
+    for dt, tol in ((np.float64, 1e-12), (np.float32, 1e-4)):
+        vv, xx = v.astype(dt), x.astype(dt)
+        for k in ("lower_n", "lower_t"):
+            for alpha in (1.0, -2.5):
+                a = ob.trsv(k + "_blocks", A.rowptr, A.colidx, vv, xx, alpha=alpha).astype(np.float64)
+                b = ob.trsv(k + "_ref", A.rowptr, A.colidx, vv, xx, alpha=alpha).astype(np.float64)
+                assert np.isfinite(a).all()
+                assert np.linalg.norm(a - b) <= tol * np.linalg.norm(b)
+
+
+def test_block_order_kat_bcspwr01():
+    """The bcspwr01 L L^T solve with x = 1 is integer-exact (SURVEY 8c KAT):
+    the block order reproduces it exactly (every coefficient and partial sum
+    is a small integer)."""
+    import json
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    kat = json.load(open(os.path.join(gold, "kat.json")))["bcspwr01"]
+    A = csr.load_matrix_market(os.path.join(gold, "mtx", "bcspwr01.mtx"))
+    v, _, _ = ob.ilu0(A.rowptr, A.colidx, A.values)
+    z = ob.trsv("lower_n_blocks", A.rowptr, A.colidx, v, np.ones(A.n))
+    y = ob.trsv("lower_t_blocks", A.rowptr, A.colidx, v, z)
+    assert y[:4].tolist() == kat["ilu_LLt_solve_x1_first4"]
+    assert np.abs(y).max() == kat["ilu_LLt_solve_x1_maxabs"]
+
+
+def test_block_rule_matches_the_product():
+    """oracle_bind.blocks_wanted restates the product's rule
+    (rsp_an::blocks_wanted): deep DAGs (<= 32 rows per level) only."""
+    deep = csr.surrogate("dc1", 0.2)
+    wide = csr.surrogate("xenon2", 0.03)
+    assert ob.blocks_wanted(0, deep.rowptr, deep.colidx) and ob.blocks_wanted(1, deep.rowptr, deep.colidx)
+    assert not ob.blocks_wanted(0, wide.rowptr, wide.colidx)
