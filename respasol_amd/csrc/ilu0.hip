@@ -446,7 +446,10 @@ __device__ __forceinline__ int flow_item(unsigned long long c, unsigned long lon
 // unfinished item is always some running wave's CURRENT item (a wave's
 // claimed items are above its current one), so progress needs no
 // co-residency.
-constexpr int kTicketRing = 16, kTicketAhead = 4;
+#ifndef RSP_TICKET_AHEAD
+#define RSP_TICKET_AHEAD 4
+#endif
+constexpr int kTicketRing = 4 * RSP_TICKET_AHEAD, kTicketAhead = RSP_TICKET_AHEAD;
 struct FlowTicketLds {
     int tk[kTicketRing];   // ticket of the round in pub[] (ring slot r % kTicketRing)
     int pub[kTicketRing];  // the round whose ticket the slot holds
@@ -459,17 +462,21 @@ struct FlowClaims {
     int mode;  // 0 static, 1 claims, 2 tickets
     FlowTicketLds *L;
     int A = 0, r = 0;
-    // thread 0 (tickets): the claim in flight (value cv for round cr > 0, or
-    // cr == 0: none), the next round to claim, whether claims go on
-    int cv = 0, cr = 0, nclaimed = 0;
+    // thread 0 (tickets): the claim in flight (raw counter value cv for round
+    // cr > 0, or cr == 0: none; base is subtracted when it is published, not
+    // at the claim, so nothing waits for the atomic until then), the next
+    // round to claim, whether claims go on
+    unsigned long long cv = 0;
+    int cr = 0, nclaimed = 0;
     bool claiming = false;
     __device__ FlowClaims(const rsp::FlowCtl &f, unsigned long long b, int i0, int i1, int w, int W,
                           FlowTicketLds *l)
         : fc(f), base(b), it0(i0), it1(i1), cur(i0 + w), stride(W), wv(w & 3),
           mode((f.mode & rsp::kFlowTickets) ? 2 : (f.mode & rsp::kFlowClaims) ? 1 : 0), L(l) {}
-    __device__ int ticket() const {
-        return (int)(__hip_atomic_fetch_add(fc.claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base);
+    __device__ unsigned long long claim() const {
+        return __hip_atomic_fetch_add(fc.claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __device__ int ticket() const { return (int)(claim() - base); }
     __device__ int rounds() const { return (it1 - it0 + 3) >> 2; }
     __device__ static int lds_ld(const int *p) {
         return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -519,16 +526,17 @@ struct FlowClaims {
     // other wave is past the round that slot held)
     __device__ void service() {
         if (cr > 0) {
-            __hip_atomic_store(&L->tk[cr % kTicketRing], cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int t = (int)(cv - base);
+            __hip_atomic_store(&L->tk[cr % kTicketRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
             __hip_atomic_store(&L->pub[cr % kTicketRing], cr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            claiming = cv < rounds();
+            claiming = t < rounds();
             cr = 0;
         }
         if (claiming && nclaimed <= r + kTicketAhead) {
             const int lo = min(lds_ld(&L->cur[1]), min(lds_ld(&L->cur[2]), lds_ld(&L->cur[3])));
             if (lo > nclaimed - kTicketRing) {
-                cv = ticket();
+                cv = claim();
                 cr = nclaimed++;
             }
         }
@@ -556,10 +564,16 @@ struct FlowClaims {
             __hip_atomic_store(&L->cur[wv], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     // tickets: the last workgroup to finish restores the counter (every
-    // thread calls it after its loop; thread 0 acts)
+    // thread calls it after its loop; thread 0 acts). Relaxed: thread 0's
+    // claims have all RETURNED before its exit count is issued (the pending
+    // one is consumed first), so they are performed at the counter before
+    // the last workgroup can see every exit; an acquire / release pair here
+    // would write back and invalidate the L2 once per workgroup (gfx950 agent
+    // scope), which cost a flow launch ~200 us.
     __device__ void finish() {
         if (mode != 2 || threadIdx.x != 0) return;
-        const int e = __hip_atomic_fetch_add(fc.exits, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (cr > 0) __builtin_amdgcn_s_waitcnt(0), cr = cv != ~0ull ? 0 : cr;  // the claim in flight has returned
+        const int e = __hip_atomic_fetch_add(fc.exits, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e == (int)gridDim.x - 1) {
             __hip_atomic_store(fc.claim, base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(fc.exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
