@@ -178,15 +178,10 @@ class Slice:
     """One matrix's share on this rank: its rows [r0, r1) (nnz-balanced split),
     generated locally, with the column layout of the chosen exchange."""
 
-    def __init__(self, name, rank, world, handle, device, exchange, overlap=False):
+    def __init__(self, name, rank, world, handle, device, exchange, overlap=False, meta=None):
         self.name = name
-        m = csr.surrogate_rows(name)
-        lens = csr.surrogate_rowlens(name)
-        rowptr = np.zeros(m + 1, np.int64)
-        np.cumsum(lens, out=rowptr[1:])
+        m, self.nnz_global, self.bounds = meta if meta is not None else partition_meta([name], world)[0]
         self.m, self.n = m, m
-        self.nnz_global = int(rowptr[-1])
-        self.bounds = csr.partition_rows(rowptr.astype(np.int32), world)
         r0, r1 = int(self.bounds[rank]), int(self.bounds[rank + 1])
         self.r0, self.r1 = r0, r1
         self.m_local = r1 - r0
@@ -246,6 +241,30 @@ class Slice:
         replicated x for the all-gather, local + halo for the halo exchange),
         y write."""
         return (elem + 4) * self.nnz_local + 4 * (self.m_local + 1) + elem * self.n_x + elem * self.m_local
+
+
+def partition_meta(names, world, rank=0, device=None):
+    """Per matrix (m, stored nnz, nnz-balanced row bounds for `world` ranks).
+    The bounds need every row's length: rank 0 generates them and broadcasts
+    the result (world > 1), so the ranks' setup does not repeat the
+    whole-matrix pass — each rank then generates only its own rows (Slice)."""
+    meta = None
+    if rank == 0:
+        meta = []
+        for name in names:
+            m = csr.surrogate_rows(name)
+            rowptr = np.zeros(m + 1, np.int64)
+            np.cumsum(csr.surrogate_rowlens(name), out=rowptr[1:])
+            meta.append((m, int(rowptr[-1]), csr.partition_rows(rowptr.astype(np.int32), world)))
+    if world == 1 or not dist.is_initialized():
+        return meta
+    flat = torch.zeros(len(names) * (world + 3), dtype=torch.int64)
+    if rank == 0:
+        flat.copy_(torch.tensor([v for m, nnz, b in meta for v in (m, nnz, *map(int, b))], dtype=torch.int64))
+    on = flat.to(device) if dist.get_backend() == "nccl" else flat
+    dist.broadcast(on, 0)
+    rows = on.cpu().view(len(names), world + 3).numpy()
+    return [(int(r[0]), int(r[1]), r[2:].astype(np.int32)) for r in rows]
 
 
 def workload_names(w):
@@ -366,7 +385,9 @@ class Workload:
     def __init__(self, names, rank, world, handle, device, args, batch=True):
         self.world, self.device = world, device
         self.overlap = overlap = world > 1 and args.exchange == "halo" and not args.no_overlap
-        self.slices = slices = [Slice(n, rank, world, handle, device, args.exchange, overlap) for n in names]
+        meta = partition_meta(names, world, rank, device)
+        self.slices = slices = [Slice(n, rank, world, handle, device, args.exchange, overlap, mt)
+                                for n, mt in zip(names, meta)]
         self.exchanges64, self.exchanges32 = [], []
         if world > 1 and args.exchange == "halo":
             groups = [[i] for i in range(len(slices))] if args.no_bucket else [list(range(len(slices)))]
@@ -727,8 +748,9 @@ def main():
         W5.ramp(20.0, device)
         el5, _, _ = W5.timed(args.steps, args.warmup)
         f5, b5 = W5.totals()
+        backend = "RCCL" if args.dist_backend == "nccl" else f"{args.dist_backend} (rehearsal)"
         config5 = {"workload": "Serena only, CSR SpMV fp64"
-                               + (f", row-partitioned x{world} + RCCL {args.exchange} exchange of x"
+                               + (f", row-partitioned x{world} + {backend} {args.exchange} exchange of x"
                                   if world > 1 else ", 1 GPU"),
                    "value": round(f5 * args.steps / el5 / 1e9, 2), "unit": "GFLOP/s",
                    "ms_per_step": round(el5 / args.steps * 1e3, 4),

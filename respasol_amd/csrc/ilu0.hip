@@ -416,27 +416,10 @@ __device__ __forceinline__ int flow_item(unsigned long long c, unsigned long lon
 }
 
 // One wave's walk over the items [it0, it1) of a flow launch (rsp::FlowCtl):
-//   for (fq.first(); fq.more(); fq.next()) { const int it = fq.item(); if (it < it1) ... }
-// Start tickets (kFlowTickets, the default): the workgroup takes TICKETS in
-// the order it runs — thread 0 alone, agent-scope fetch_adds on the flow
-// counter, so its tickets increase with its rounds — and in round r each
-// wave runs item 4 t_r + (its wave) of that round's ticket. Thread 0 claims
-// kTicketAhead rounds ahead and publishes each ticket in an LDS ring
-// (kTicketRing slots, with the round it belongs to); a wave entering round r
-// waits (in LDS) for round r's ticket, so the waves of a workgroup run
-// independently up to the lookahead — no workgroup barrier per round.
-// Thread 0 never runs more than kTicketRing - kTicketAhead rounds ahead of
-// the slowest wave (its ring slot would be reused).
-// Progress: an item waits only on items of lower tickets. Let u be the
-// lowest unfinished item, in round r of workgroup X; X's earlier rounds hold
-// lower tickets, so they are finished and u's wave is in round r or entering
-// it, whose ticket wave 0 published kTicketAhead - 1 rounds earlier (wave 0's
-// own round-r item is below u or is u). Every ticket is held by a workgroup
-// that has started: progress needs no co-residency, only that a started
-// workgroup keeps running.
-// The counter is restored at the end of the launch (the last workgroup to
-// exit, counted on fc.exits, stores `base` back), so a ticket launch leaves
-// the host mirror unchanged.
+//   for (fq.first(); fq.more(); fq.next()) { const int it = fq.item(); ... }
+// A wait inside an item that returns true (fq.expire(), tickets only) makes
+// the item yield: it runs through on what it has but stores nothing, and
+// fq.item_end(it, true) has next() run it again or walk a grown ticket list.
 // Static (RSP_ILU_FLOW_MODE=0): w, w + W, ... (the whole grid must be resident).
 // Claimed (kFlowClaims): in start order, TWO items ahead — the claim for item
 // j + 2 is issued during item j, behind its first loads (claim_ahead), and
@@ -446,138 +429,300 @@ __device__ __forceinline__ int flow_item(unsigned long long c, unsigned long lon
 // unfinished item is always some running wave's CURRENT item (a wave's
 // claimed items are above its current one), so progress needs no
 // co-residency.
-#ifndef RSP_TICKET_AHEAD
-#define RSP_TICKET_AHEAD 4
-#endif
-constexpr int kTicketRing = 4 * RSP_TICKET_AHEAD, kTicketAhead = RSP_TICKET_AHEAD;
+// Start tickets (kFlowTickets, the default): thread 0 takes the workgroup's
+// ticket t — from one of eight counters (blockIdx % 8; counter q hands out
+// q, q + 8, ..., so the G start claims do not queue on one address) of the
+// launch's counter slot (base & 1; block 0 zeroes the other slot for the
+// next launch, the previous launch's, which has ended) — and each wave walks
+// the static items of t, it0 + 4 t + wave + k W: a resident grid runs
+// exactly the static walk. A workgroup whose counter is spent owns nothing.
+// Steals: a wait past kFlowStealUs (2 us once its workgroup has stolen)
+// asks expire(): with every counter spent and the owned list unchanged
+// (calm) it waits on; else the item yields — it runs through on what it
+// has, stores nothing — and next() claims another ticket for the workgroup
+// (under an LDS lock, inserted so that own[] stays ascending) unless none
+// is left, then runs the item again — unless the list has grown (by this
+// steal or another wave's): then the wave walks again from the start:
+// rounds k = 0, 1, ..., in each the owned tickets in list order — the
+// merged index order of its items — skipping the items it has finished
+// (those of the start ticket below the round it had reached, and those
+// marked with the call's epoch in fc.done since).
+// A wave out of items waits in the workgroup until all four are (the list
+// could still grow), counted with the list length in one LDS word.
+// Progress: let u be the lowest unfinished item. If its ticket is owned,
+// its owner's wave for u has walked every owned item below u (finished) and
+// is at u, or waits on a higher item or for its siblings and sees the list
+// grow once u's ticket joined it: it comes to u, whose operands are lower
+// items, finished. If u's ticket is unclaimed, every started wave that
+// cannot go on waits, and either steals (a ticket is claimed) or its
+// workgroup ends (a new one starts and claims). Every wait is bounded by
+// fc.ticks; nothing needs co-residency.
 struct FlowTicketLds {
-    int tk[kTicketRing];   // ticket of the round in pub[] (ring slot r % kTicketRing)
-    int pub[kTicketRing];  // the round whose ticket the slot holds
-    int cur[4];            // the round each wave is in
+    int own[rsp::kFlowOwnMax];  // the workgroup's tickets, ascending (own[0] the start ticket until a steal)
+    int state;                  // tickets owned | waves out of items << 16
+    int lock;                   // a steal is in progress
+    int dry;                    // every counter is spent: no ticket left to steal
 };
+template <bool TK>  // TK: start tickets (kFlowTickets); else static or claimed (fc.mode)
 struct FlowClaims {
     const rsp::FlowCtl &fc;
     unsigned long long base, c1 = 0, c2 = 0;
     int it0, it1, cur, stride, wv;
-    int mode;  // 0 static, 1 claims, 2 tickets
+    int mode;  // 0 static, 1 claims, 2 tickets (TK)
     FlowTicketLds *L;
-    int A = 0, r = 0;
-    // thread 0 (tickets): the claim in flight (raw counter value cv for round
-    // cr > 0, or cr == 0: none; base is subtracted when it is published, not
-    // at the claim, so nothing waits for the atomic until then), the next
-    // round to claim, whether claims go on
-    unsigned long long cv = 0;
-    int cr = 0, nclaimed = 0;
-    bool claiming = false;
+    // tickets: the owned list as this wave last read it, its position
+    // (round k, list index j), the round its fast walk reached (start ticket
+    // items below it are finished), whether it walks with done checks
+    int nseen = 0, k = 0, j = 0, fast_k = 0, t0 = 0;
+    // a wait this long (100 MHz ticks) may steal: kFlowStealUs, 2 us after a steal
+    unsigned long long steal_at = 100ull * rsp::kFlowStealUs;
+    bool scan = false, redo = false, over = false;
     __device__ FlowClaims(const rsp::FlowCtl &f, unsigned long long b, int i0, int i1, int w, int W,
                           FlowTicketLds *l)
         : fc(f), base(b), it0(i0), it1(i1), cur(i0 + w), stride(W), wv(w & 3),
-          mode((f.mode & rsp::kFlowTickets) ? 2 : (f.mode & rsp::kFlowClaims) ? 1 : 0), L(l) {}
-    __device__ unsigned long long claim() const {
-        return __hip_atomic_fetch_add(fc.claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          mode(TK ? 2 : (f.mode & rsp::kFlowClaims) ? 1 : 0), L(l) {}
+    // tickets: counter q of this launch's slot hands out q, q + 8, q + 16, ...
+    // (eight counters, so the G start claims do not queue on one address)
+    __device__ unsigned *ctr() const { return fc.tickets + rsp::kFlowTicketCtrs * (int)(base & 1); }
+    __device__ int take(int q) const {
+        return q + rsp::kFlowTicketCtrs * (int)__hip_atomic_fetch_add(ctr() + q, 1u, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT);
     }
-    __device__ int ticket() const { return (int)(claim() - base); }
-    __device__ int rounds() const { return (it1 - it0 + 3) >> 2; }
+    __device__ bool spent(int q) const {  // counter q has no ticket < G left
+        return q + rsp::kFlowTicketCtrs * (long long)__hip_atomic_load(ctr() + q, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT) >= (long long)gridDim.x;
+    }
     __device__ static int lds_ld(const int *p) {
         return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     }
-    // LDS-only acquire / release (the "local" address-space fences): a
-    // workgroup-scope acquire or release on a plain atomic would also wait
-    // for the wave's outstanding GLOBAL accesses (s_waitcnt vmcnt(0)), here
-    // the item's y / value stores still in flight
+    // LDS-only acquire (the "local" address-space fence): a workgroup-scope
+    // acquire on a plain atomic would also wait for the wave's outstanding
+    // GLOBAL accesses (s_waitcnt vmcnt(0))
     __device__ static int lds_acq(const int *p) {
-        const int v = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const int v = lds_ld(p);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         return v;
     }
     __device__ void first() {
-        if (mode == 0) return;
-        if (mode == 1) {
-            const unsigned long long c0 = flow_claim(fc);
-            c1 = flow_claim(fc);
-            cur = flow_item(c0, base, it0, it1);
+        if constexpr (!TK) {
+            if (mode == 1) {
+                const unsigned long long c0 = flow_claim(fc);
+                c1 = flow_claim(fc);
+                cur = flow_item(c0, base, it0, it1);
+            }
             return;
         }
-        if (threadIdx.x == 0) {  // rounds 0 .. kTicketAhead - 1 (the atomics overlap)
-            int t[kTicketAhead];
-#pragma unroll
-            for (int k = 0; k < kTicketAhead; ++k) t[k] = ticket();
-#pragma unroll
-            for (int k = 0; k < kTicketAhead; ++k) L->tk[k] = t[k];
-            claiming = t[kTicketAhead - 1] < rounds();
-            nclaimed = kTicketAhead;
+        if (threadIdx.x == 0) {
+            if (blockIdx.x == 0)  // the next launch's slot (the previous launch's: it has ended)
+                for (int q = 0; q < rsp::kFlowTicketCtrs; ++q)
+                    __hip_atomic_store(fc.tickets + rsp::kFlowTicketCtrs * (int)((base + 1) & 1) + q, 0u,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int t = take(blockIdx.x % rsp::kFlowTicketCtrs);
+            L->own[0] = t;
+            L->state = t < (int)gridDim.x ? 1 : 0;
+            L->lock = 0;
+            L->dry = t >= (int)gridDim.x;
         }
-        if (threadIdx.x < kTicketRing) L->pub[threadIdx.x] = threadIdx.x < kTicketAhead ? (int)threadIdx.x : -1;
-        if (threadIdx.x < 4) L->cur[threadIdx.x] = 0;
         __syncthreads();  // (once, at the start)
-        A = lds_ld(&L->tk[0]);
+        nseen = lds_ld(&L->state) & 0xffff;
+        t0 = lds_ld(&L->own[0]);
+        settle();
     }
-    __device__ bool more() const { return mode == 2 ? A < rounds() : cur < it1; }
-    __device__ int item() const { return mode == 2 ? it0 + 4 * A + wv : cur; }
+    __device__ bool more() const { return TK ? !over : cur < it1; }
+    __device__ int item() const { return cur; }
     __device__ void claim_ahead() {
         __builtin_amdgcn_sched_barrier(0);
         if (mode == 1) c2 = flow_claim(fc);
         __builtin_amdgcn_sched_barrier(0);
     }
-    // thread 0: publish the claim in flight (issued at least a round ago, so
-    // its value is back), then claim round `nclaimed` if it is at most
-    // kTicketAhead past this wave's round and its ring slot is free (every
-    // other wave is past the round that slot held)
-    __device__ void service() {
-        if (cr > 0) {
-            const int t = (int)(cv - base);
-            __hip_atomic_store(&L->tk[cr % kTicketRing], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            __hip_atomic_store(&L->pub[cr % kTicketRing], cr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            claiming = t < rounds();
-            cr = 0;
-        }
-        if (claiming && nclaimed <= r + kTicketAhead) {
-            const int lo = min(lds_ld(&L->cur[1]), min(lds_ld(&L->cur[2]), lds_ld(&L->cur[3])));
-            if (lo > nclaimed - kTicketRing) {
-                cv = claim();
-                cr = nclaimed++;
+    // tickets: from position (k, j), the next item of this wave to run
+    // (cur), or none left in the workgroup (over)
+    __device__ void settle() {
+        if (!scan && nseen == 1) {  // the start ticket alone: the static walk
+            const int it = it0 + 4 * t0 + wv + k * stride;
+            if (it < it1) {
+                cur = it;
+                return;
             }
         }
+        for (;;) {
+            if (j >= nseen && nseen > 0) {
+                ++k;
+                j = 0;
+            }
+            if (nseen > 0) {
+                const int tj = lds_ld(&L->own[j]);
+                const int it = it0 + 4 * tj + wv + k * stride;
+                if (it < it1) {
+                    const bool fin = scan && ((tj == t0 && k < fast_k) ||
+                                              __hip_atomic_load(fc.done + it, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_WAVEFRONT) == (int)fc.epoch);
+                    if (!fin) {
+                        cur = it;
+                        return;
+                    }
+                    ++j;
+                    continue;
+                }
+                if (j > 0) {  // the rest of round k is past it1 too
+                    ++k;
+                    j = 0;
+                    continue;
+                }
+            }
+            const int s = idle();  // out of items
+            if (s < 0) {
+                over = true;
+                cur = it1;
+                return;
+            }
+            rescan(s);
+        }
+    }
+    // walk again from the start over an owned list of s tickets
+    __device__ void rescan(int s) {
+        if (!scan) fast_k = k;  // (the fast walk was at round k of the start ticket)
+        scan = true;
+        steal_at = 200;
+        nseen = s;
+        k = j = 0;
+    }
+    // out of items: wait until the owned list grows (its new length) or all
+    // four waves are out (-1)
+    __device__ int idle() {
+        const int me = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63));
+        int r = -1;
+        if ((int)(threadIdx.x & 63) == me) {
+            int s = __hip_atomic_fetch_add(&L->state, 1 << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) +
+                    (1 << 16);
+            for (;;) {
+                if ((s & 0xffff) != nseen) {
+                    __hip_atomic_fetch_add(&L->state, -(1 << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    r = s & 0xffff;
+                    break;
+                }
+                if ((s >> 16) == 4) break;
+                __builtin_amdgcn_s_sleep(2);
+                s = __hip_atomic_load(&L->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        r = __builtin_amdgcn_readfirstlane(r);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");  // own[] entries up to r
+        return r;
+    }
+    // a wait that began at wall clock t0 runs until this deadline, then
+    // expire() tells it to give up or (tickets) to yield the item to next(),
+    // which may steal, then runs the item again or walks a grown list; the
+    // give-up bound counts from the wait's start (one compare per poll, as
+    // without tickets; nothing written, so a wait of one lane is fine). An
+    // item yields only while a steal can follow (not calm), fewer than G + 1
+    // times per wave, so no item escapes the bound by yielding.
+    __device__ unsigned long long deadline(unsigned long long t0) const {
+        if constexpr (!TK) return t0 + fc.ticks;
+#ifdef RSP_TK_NOSTEAL
+        return t0 + fc.ticks;
+#endif
+        return t0 + min(fc.ticks, steal_at);
+    }
+    // a wait past its deadline: 0 give up, 1 yield, 2 wait on until the new
+    // deadline dl (tickets: nothing to steal and the owned list as this wave
+    // knows it — every ticket is claimed, a grown list would have had a
+    // steal succeed first)
+    __device__ int expire(unsigned long long now, unsigned long long t0, unsigned long long &dl) const {
+        if (TK && now <= t0 + fc.ticks) {
+            if (!calm()) return 1;
+            dl = t0 + fc.ticks;
+            return 2;
+        }
+        flow_give_up(fc);
+        return 0;
+    }
+    // tickets: no steal can succeed (LDS dry, set here once the counter
+    // shows all G tickets claimed) and the owned list has not grown past nseen
+    __device__ bool calm() const {
+        if constexpr (!TK) return true;
+        if (!__hip_atomic_load(&L->dry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            for (int q = 0; q < rsp::kFlowTicketCtrs; ++q)
+                if (!spent(q)) return false;
+            __hip_atomic_store(&L->dry, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return (__hip_atomic_load(&L->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 0xffff) == nseen;
+    }
+    // next() after a yield: the owned list's length if it has grown past
+    // nseen (maybe by a steal made here), else 0
+    __device__ int steal() {
+        const int me = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63));
+        int r = 0;
+        if ((int)(threadIdx.x & 63) == me) {
+            const int s = __hip_atomic_load(&L->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((s & 0xffff) != nseen)
+                r = s & 0xffff;
+            else if (!__hip_atomic_load(&L->dry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                int z = 0;
+                if (__hip_atomic_compare_exchange_strong(&L->lock, &z, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                    const int n = __hip_atomic_load(&L->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
+                                  0xffff;
+                    if (n != nseen)
+                        r = n;
+                    else if (n < rsp::kFlowOwnMax) {
+                        int t = (int)gridDim.x;
+                        for (int d = 0; d < rsp::kFlowTicketCtrs && t >= (int)gridDim.x; ++d) {
+                            const int q = (int)(blockIdx.x + d) % rsp::kFlowTicketCtrs;
+                            if (!spent(q)) t = take(q);
+                        }
+                        if (t < (int)gridDim.x) {  // insert, keeping own[] ascending
+                            int x = n;
+                            for (; x > 0 && L->own[x - 1] > t; --x) L->own[x] = L->own[x - 1];
+                            L->own[x] = t;
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                            __hip_atomic_fetch_add(&L->state, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            r = n + 1;
+                        } else
+                            __hip_atomic_store(&L->dry, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    __hip_atomic_store(&L->lock, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        }
+        r = __builtin_amdgcn_readfirstlane(r);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");  // own[] entries up to r
+        return r;
+    }
+    // the item is finished: after a steal its index is marked with the epoch
+    __device__ void done(int it) const {
+        if (TK && scan && (threadIdx.x & 63) == 0)
+            __hip_atomic_store(fc.done + it, (int)fc.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    // the item ends: finished, or (yl) yielded — then next() runs it again
+    // unless the owned list grows
+    __device__ void item_end(int it, bool yl) {
+        if constexpr (!TK) return;
+        if (yl)
+            redo = true;
+        else
+            done(it);
     }
     __device__ void next() {
-        if (mode == 0) {
-            cur += stride;
+        if constexpr (!TK) {
+            if (mode == 0) {
+                cur += stride;
+            } else {
+                cur = flow_item(c1, base, it0, it1);
+                c1 = c2;
+            }
             return;
         }
-        if (mode == 1) {
-            cur = flow_item(c1, base, it0, it1);
-            c1 = c2;
-            return;
-        }
-        const bool lead = wv == 0 && (threadIdx.x & 63) == 0;
-        if (lead) service();
-        ++r;
-        const int *pub = &L->pub[r % kTicketRing];
-        while (lds_acq(pub) != r) {  // (wave 0 publishes the round itself if it is not yet)
-            if (lead) service();
-            __builtin_amdgcn_s_sleep(1);
-        }
-        A = lds_ld(&L->tk[r % kTicketRing]);
-        if ((threadIdx.x & 63) == 0)
-            __hip_atomic_store(&L->cur[wv], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // tickets: the last workgroup to finish restores the counter (every
-    // thread calls it after its loop; thread 0 acts). Relaxed: thread 0's
-    // claims have all RETURNED before its exit count is issued (the pending
-    // one is consumed first), so they are performed at the counter before
-    // the last workgroup can see every exit; an acquire / release pair here
-    // would write back and invalidate the L2 once per workgroup (gfx950 agent
-    // scope), which cost a flow launch ~200 us.
-    __device__ void finish() {
-        if (mode != 2 || threadIdx.x != 0) return;
-        if (cr > 0) __builtin_amdgcn_s_waitcnt(0), cr = cv != ~0ull ? 0 : cr;  // the claim in flight has returned
-        const int e = __hip_atomic_fetch_add(fc.exits, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (e == (int)gridDim.x - 1) {
-            __hip_atomic_store(fc.claim, base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(fc.exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (redo) {  // the item yielded: it runs again unless the owned list grows
+            redo = false;
+            const int n = steal();
+            if (n == 0) return;
+            rescan(n);
+        } else if (!scan && nseen == 1)
+            ++k;
+        else
+            ++j;
+        settle();
     }
 };
 
@@ -593,10 +738,10 @@ __device__ __forceinline__ void flow_store(T *p, T v) {
 
 // Re-read this lane's operand words [0, n) that are still kNotYet until none
 // of the wave's is (wave-uniform loop; the pause between polls doubles up to
-// max_sleep s_sleep units of 64 clocks).
-template <typename T, int NB>
-__device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], const int (&id)[NB], int n,
-                                          const T *y, const rsp::FlowCtl &fc, int max_sleep) {
+// max_sleep s_sleep units of 64 clocks). True: the item yields (FlowClaims::expire).
+template <typename T, int NB, typename FQ>
+__device__ __forceinline__ bool flow_wait(typename FlowWord<T>::U (&w)[NB], const int (&id)[NB], int n,
+                                          const T *y, FQ &fq, int max_sleep, bool skip = false) {
     constexpr auto kNot = FlowWord<T>::kNotYet;
     auto pending = [&] {
         bool p = false;
@@ -604,17 +749,19 @@ __device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], cons
         for (int b = 0; b < NB; ++b) p |= b < n && w[b] == kNot;
         return p;
     };
-    if (!__ballot(pending())) return;
+    if (!__ballot(pending())) return false;
     const unsigned long long t0 = wall_clock64();
+    unsigned long long dl = skip ? 0ull : fq.deadline(t0);  // (skip: the item has yielded)
     for (int sl = 1;; sl = min(2 * sl, max_sleep)) {
         for (int q = 0; q < sl; ++q) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
             if (b < n && w[b] == kNot) w[b] = flow_load(y + id[b]);
-        if (!__ballot(pending())) return;
-        if (wall_clock64() - t0 > fc.ticks) {
-            flow_give_up(fc);
-            return;
+        if (!__ballot(pending())) return false;
+        const unsigned long long now = wall_clock64();
+        if (now > dl) {
+            const int r = fq.expire(now, t0, dl);
+            if (r != 2) return r != 0;
         }
     }
 }
@@ -626,13 +773,13 @@ __device__ __forceinline__ void flow_wait(typename FlowWord<T>::U (&w)[NB], cons
 // poll one word instead of a word per operand (the operand polls alone, up to
 // 8 per lane, slowed the loads on the critical path). Row g's item has a
 // lower index, so the gate cannot deadlock.
-template <typename T>
-__device__ __forceinline__ void flow_gate(int g, const T *y, const rsp::FlowCtl &fc, int max_sleep) {
-    if (g < 0) return;
+template <typename T, typename FQ>
+__device__ __forceinline__ bool flow_gate(int g, const T *y, FQ &fq, int max_sleep) {
+    if (g < 0) return false;
     typename FlowWord<T>::U w[1] = {0};
     int id[1] = {g};
     if ((threadIdx.x & 63) == 0) w[0] = flow_load(y + g);
-    flow_wait<T, 1>(w, id, (threadIdx.x & 63) == 0 ? 1 : 0, y, fc, max_sleep);
+    return flow_wait<T, 1>(w, id, (threadIdx.x & 63) == 0 ? 1 : 0, y, fq, max_sleep);
 }
 
 // Fat level in the slot layout (rsp::FacSlotLevel): the row's structure is
@@ -708,10 +855,10 @@ __global__ __launch_bounds__(64) void ilu0_level_slot(IluArgs a, const int *__re
 
 // Re-read this lane's operand words that are still kNotYet (need[b] set)
 // until none of the wave's is (wave-uniform loop, bounded like flow_wait).
-template <typename T, int NB>
-__device__ __forceinline__ void tagged_wait(typename FlowWord<T>::U (&w)[NB], const int (&pos)[NB],
-                                            const bool (&need)[NB], const T *vals, const rsp::FlowCtl &fc,
-                                            int max_sleep) {
+template <typename T, int NB, typename FQ>
+__device__ __forceinline__ bool tagged_wait(typename FlowWord<T>::U (&w)[NB], const int (&pos)[NB],
+                                            const bool (&need)[NB], const T *vals, FQ &fq,
+                                            int max_sleep, bool skip) {
     constexpr auto kNot = FlowWord<T>::kNotYet;
     auto pending = [&] {
         bool p = false;
@@ -719,17 +866,19 @@ __device__ __forceinline__ void tagged_wait(typename FlowWord<T>::U (&w)[NB], co
         for (int b = 0; b < NB; ++b) p |= need[b] && w[b] == kNot;
         return p;
     };
-    if (!__ballot(pending())) return;
+    if (!__ballot(pending())) return false;
     const unsigned long long t0 = wall_clock64();
+    unsigned long long dl = skip ? 0ull : fq.deadline(t0);  // (skip: the item has yielded)
     for (int sl = 1;; sl = min(2 * sl, max_sleep)) {
         for (int q = 0; q < sl; ++q) __builtin_amdgcn_s_sleep(1);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
             if (need[b] && w[b] == kNot) w[b] = flow_load(vals + pos[b]);
-        if (!__ballot(pending())) return;
-        if (wall_clock64() - t0 > fc.ticks) {
-            flow_give_up(fc);
-            return;
+        if (!__ballot(pending())) return false;
+        const unsigned long long now = wall_clock64();
+        if (now > dl) {
+            const int r = fq.expire(now, t0, dl);
+            if (r != 2) return r != 0;
         }
     }
 }
@@ -787,7 +936,7 @@ __global__ __launch_bounds__(256) void ilu0_flow_prep(IluArgs a, int nitems) {
 // write-back and an L2 invalidate per row) took 116 ms. Structure and
 // arithmetic as ilu0_level_slot (the level's rm / qm at run time, budgets
 // KR / KQ at their maximum): the same bits.
-template <typename T>
+template <typename T, bool TK>
 __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, unsigned long long base) {
     constexpr int R = rsp::kFacRow, Q = rsp::kFacPairs, KR = R / 64, KQ = Q / 64;
     typedef typename FlowWord<T>::U U;
@@ -801,8 +950,8 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, un
     unsigned short *pl = pl_[wv];
     T *vals = (T *)a.vals;
     const T *orig = (const T *)a.forig;
-    __shared__ FlowTicketLds tl;
-    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4, &tl);
+    __shared__ std::conditional_t<TK, FlowTicketLds, int> tl_;  // (tickets only)
+    FlowClaims<TK> fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4, reinterpret_cast<FlowTicketLds *>(&tl_));
     for (fq.first(); fq.more(); fq.next()) {
         const int it = fq.item();
         if (it >= it1) continue;  // (tickets: a last round's spare waves)
@@ -837,12 +986,18 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, un
                 const int x = min(lane + 64 * k, max(nr - 1, 0));
                 av[k] = x < nlo ? vals[rs + x] : orig[rs + x];
             }
+        // yl: a wait yielded (tickets, FlowClaims::expire): the item still
+        // runs through on what it has, but stores nothing and runs again
+        // later — no branch out of the polling loops (the structured control
+        // flow of such an exit cost the factor ~9 %, config-3 FEM subset)
+        int gate_yl = 0;
         if (lane == 0 && gp >= 0 && gp < ge) {
             U gw[1] = {flow_load(vals + gp)};
             const int gpos[1] = {gp};
             const bool gn[1] = {true};
-            tagged_wait<T, 1>(gw, gpos, gn, vals, a.fc, a.flow_sleep);
+            gate_yl = tagged_wait<T, 1>(gw, gpos, gn, vals, fq, a.flow_sleep, false);
         }
+        bool yl = __builtin_amdgcn_readfirstlane(gate_yl) != 0;
         // operands: divisors u_kk of the lower entries, u_kj of the update pairs
         U dw[KR], uw[KQ];
         int dp[KR], upos[KQ];
@@ -859,8 +1014,8 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, un
             upos[k] = 64 * k < qm ? pr[k].x : 0;
             uw[k] = 64 * k < qm ? flow_load(vals + upos[k]) : U(0);
         }
-        tagged_wait<T, KR>(dw, dp, dn, vals, a.fc, a.flow_sleep);
-        tagged_wait<T, KQ>(uw, upos, un, vals, a.fc, a.flow_sleep);
+        if (tagged_wait<T, KR>(dw, dp, dn, vals, fq, a.flow_sleep, yl)) yl = true;
+        if (tagged_wait<T, KQ>(uw, upos, un, vals, fq, a.flow_sleep, yl)) yl = true;
         if (nr > 0) {
 #pragma unroll
             for (int k = 0; k < KR; ++k) {
@@ -882,11 +1037,14 @@ __global__ __launch_bounds__(256) void ilu0_flow(IluArgs a, int it0, int it1, un
                     pu[u] = __builtin_bit_cast(T, uw[k]);
                 }
             }
+            // (after a yield: a zero pivot found here is real — a pivot built
+            // from a kNotYet operand is a NaN — and the rerun finds it again)
             row_lds_factor<T>(rv, dv, pu, up, lo, le, pl, nlo, nr, lane, hasdiag, i, a.zero_pivot);
-            for (int x = lane; x < nr; x += 64) flow_store(vals + rs + x, flow_publishable(rv[x]));
+            if (!yl)
+                for (int x = lane; x < nr; x += 64) flow_store(vals + rs + x, flow_publishable(rv[x]));
         }
+        fq.item_end(it, yl);
     }
-    fq.finish();
 }
 
 // The whole factor of a pattern without update pairs (IluArgs::fac_one: a
@@ -1434,7 +1592,7 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
 // expected) gives up and records the call in *fc.status (rsp_trsv_zero_pivot
 // then returns EXECUTION_FAILED) instead of hanging the GPU.
 // Same terms, same order, same fma chain as trsv_level: the same bits.
-template <typename T, int KIND>
+template <typename T, int KIND, bool TK>
 __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, unsigned long long base) {
     typedef typename FlowWord<T>::U U;
     constexpr int F = rsp::kFatLongTerms;
@@ -1449,8 +1607,8 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, u
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     };
-    __shared__ FlowTicketLds tl;
-    FlowClaims fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4, &tl);
+    __shared__ std::conditional_t<TK, FlowTicketLds, int> tl_;  // (tickets only)
+    FlowClaims<TK> fq(a.fc, base, it0, it1, blockIdx.x * 4 + wv, (int)gridDim.x * 4, reinterpret_cast<FlowTicketLds *>(&tl_));
     // claims are issued behind each item's first loads (task, term values and sources)
     for (fq.first(); fq.more(); fq.next()) {
         const int it = fq.item();
@@ -1481,28 +1639,30 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, u
             }
             T s = sx[x];
             fq.claim_ahead();
-            flow_gate<T>(f.gate, y, a.fc, a.flow_sleep);
+            // yl: a wait yielded (as in ilu0_flow: the item runs through and stores nothing)
+            bool yl = flow_gate<T>(f.gate, y, fq, a.flow_sleep);
             U w[F];
 #pragma unroll
             for (int b = 0; b < F; ++b) w[b] = b < n ? flow_load(y + id[b]) : U(0);
-            flow_wait<T, F>(w, id, n, y, a.fc, a.flow_sleep);
+            if (flow_wait<T, F>(w, id, n, y, fq, a.flow_sleep, yl)) yl = true;
 #pragma unroll
             for (int b = 0; b < F; ++b)
                 if (b < n) s = fma_t(-v[b], __builtin_bit_cast(T, w[b]), s);
             if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
-            if (lane < f.n) flow_store(y + t.i, s);
+            if (lane < f.n && !yl) flow_store(y + t.i, s);
+            fq.item_end(it, yl);
         } else {  // one row of more terms: a wave, 64 terms at a time on LDS broadcast operands
             const int x = f.x0;
             const rsp::RowTask t = a.plan.tasks[x];
             T s = sx[x];
             fq.claim_ahead();
-            flow_gate<T>(f.gate, y, a.fc, a.flow_sleep);
+            bool yl = flow_gate<T>(f.gate, y, fq, a.flow_sleep);
             for (int base = t.t0; base < t.t1; base += 64) {
                 const int k = min(base + lane, t.t1 - 1);
                 const T v = sval[k];
                 int id[1] = {src[k]};
                 U w[1] = {flow_load(y + id[0])};
-                flow_wait<T, 1>(w, id, 1, y, a.fc, a.flow_sleep);
+                if (flow_wait<T, 1>(w, id, 1, y, fq, a.flow_sleep, yl)) yl = true;
                 fwv[wv][lane] = v;
                 fwy[wv][lane] = __builtin_bit_cast(T, w[0]);
                 wave_sync();
@@ -1522,10 +1682,10 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, u
                 wave_sync();  // this group's reads before the next group's stores
             }
             if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
-            if (lane == 0) flow_store(y + t.i, s);
+            if (lane == 0 && !yl) flow_store(y + t.i, s);
+            fq.item_end(it, yl);
         }
     }
-    fq.finish();
 }
 
 // Thin run (levels cut into LDS-staged chunks [c0, c1)), one 1024-thread
@@ -2326,21 +2486,24 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
 // caps the requested grid.
 template <auto KERNEL>
 static int flow_grid(const rsp::FlowCtl &fc, int want, int cus, int items) {
-    (void)fc;  // (start tickets need no residency; the same grid keeps the polling load of the static walk)
     static int occ = 0;  // per kernel
     if (occ == 0) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KERNEL, 256, 0) != hipSuccess) nb = 1;
         occ = max(nb - 1, 1);
     }
-    return max(1, min(min(want, cus * occ), (items + 3) / 4));
+    // (start tickets need no residency: the same grid keeps the walk of the
+    // static one; tests oversubscribe it, RSP_ILU_FLOW_GRID_X, so that
+    // workgroups wait for others to end and steals carry the launch)
+    const int g = min(want, cus * occ) * ((fc.mode & rsp::kFlowTickets) ? fc.grid_x : 1);
+    return max(1, min(min(g, rsp::kFlowOwnMax), (items + 3) / 4));
 }
 
 // A flow launch of `items` items on `grid` 4-wave workgroups: its claim base,
 // and the host mirror advanced by the claims it will make (rsp::FlowCtl).
 static unsigned long long flow_claims(const rsp::FlowCtl &fc, int items, int grid) {
     const unsigned long long base = *fc.claim_host;
-    if (fc.mode & rsp::kFlowTickets) return base;  // the launch restores the counter (FlowClaims::finish)
+    if (fc.mode & rsp::kFlowTickets) return (*fc.tk_seq)++;  // the launch's counter slot (FlowClaims)
     if (!(fc.mode & rsp::kFlowClaims)) return base;  // static items: no claims
     *fc.claim_host = base + (unsigned long long)items + 2ull * 4ull * (unsigned long long)grid;
     return base;
@@ -2369,9 +2532,14 @@ static hipError_t launch_factor(const IluArgs &a, hipStream_t s) {
             while (fr < a.nfruns && a.fruns[fr].lb < l) ++fr;
             if (a.flow && fr < a.nfruns && a.fruns[fr].lb == l) {  // flow run: one persistent launch
                 const rsp::FacFlowRun r = a.fruns[fr];
-                const int grid = flow_grid<ilu0_flow<T>>(a.fc, a.flow_grid, a.flow_cus, r.c1 - r.c0);
+                const bool tk = a.fc.mode & rsp::kFlowTickets;
+                const int grid = tk ? flow_grid<ilu0_flow<T, true>>(a.fc, a.flow_grid, a.flow_cus, r.c1 - r.c0)
+                                    : flow_grid<ilu0_flow<T, false>>(a.fc, a.flow_grid, a.flow_cus, r.c1 - r.c0);
                 const unsigned long long base = flow_claims(a.fc, r.c1 - r.c0, grid);
-                hipLaunchKernelGGL((ilu0_flow<T>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, base);
+                if (tk)
+                    hipLaunchKernelGGL((ilu0_flow<T, true>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, base);
+                else
+                    hipLaunchKernelGGL((ilu0_flow<T, false>), dim3(grid), dim3(256), 0, s, a, r.c0, r.c1, base);
                 ++flow_launched;
                 l = r.le - 1;
                 continue;
@@ -2432,9 +2600,14 @@ static hipError_t launch_solve(const TrsvArgs &a, hipStream_t s) {
             continue;
         }
         if (a.flow && sg.c1 > sg.c0) {  // flow segment: one persistent launch
-            const int grid = flow_grid<trsv_flow<T, KIND>>(a.fc, a.flow_grid, a.flow_cus, sg.c1 - sg.c0);
+            const bool tk = a.fc.mode & rsp::kFlowTickets;
+            const int grid = tk ? flow_grid<trsv_flow<T, KIND, true>>(a.fc, a.flow_grid, a.flow_cus, sg.c1 - sg.c0)
+                                : flow_grid<trsv_flow<T, KIND, false>>(a.fc, a.flow_grid, a.flow_cus, sg.c1 - sg.c0);
             const unsigned long long base = flow_claims(a.fc, sg.c1 - sg.c0, grid);
-            hipLaunchKernelGGL((trsv_flow<T, KIND>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1, base);
+            if (tk)
+                hipLaunchKernelGGL((trsv_flow<T, KIND, true>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1, base);
+            else
+                hipLaunchKernelGGL((trsv_flow<T, KIND, false>), dim3(grid), dim3(256), 0, s, a, sg.c0, sg.c1, base);
             continue;
         }
         for (int l = sg.lb; l < sg.le; ++l) {

@@ -89,10 +89,13 @@ struct rsp_ilu0_info {
     int *d_upd_ptr, *d_upd_l, *d_upd_u, *d_lord, *d_lend, *d_udiv;
     // d_zero: [0] numerical zero pivot (atomicMin), [1] generation of the
     // last factor call whose flow wait gave up, [2..4] the same for the L,
-    // L^T and U solves (rsp::FlowCtl), [5] the finished workgroups of a
-    // ticket launch, [6..7] the flow claim counter
+    // L^T and U solves (rsp::FlowCtl), [6..7] the flow claim counter
     int *d_zero;
     unsigned long long claim_host = 0;  // flow claims issued (rsp::FlowCtl)
+    int *d_fdone = nullptr;             // ticket flow launches: per item, the epoch that finished it (rsp::FlowCtl)
+    unsigned *d_tk = nullptr;           // ticket flow launches: two slots of counters (rsp::FlowCtl::tickets)
+    unsigned long long tk_seq = 0;      // ticket flow launches enqueued (rsp::FlowCtl::tk_seq)
+    unsigned flow_epoch = 0;            // epochs handed out (rsp::FlowCtl)
     int solve_gen[3] = {0, 0, 0};       // per solve kind: generation of the last call
     long long n_updates;
     // one level set per DAG: L (factor + L solve), L^T, U
@@ -1198,7 +1201,8 @@ static void ilu_free_device(rsp_ilu0_info *f) {
     f->d_arena = f->d_arena_u = nullptr;
     f->d_usval = nullptr;
     f->d_fslots = nullptr;
-    f->d_dpos = f->d_hasdiag = f->d_zero = nullptr;
+    f->d_dpos = f->d_hasdiag = f->d_zero = f->d_fdone = nullptr;
+    f->d_tk = nullptr;
     f->d_upd_ptr = f->d_upd_l = f->d_upd_u = f->d_lord = f->d_lend = f->d_udiv = nullptr;
     f->d_sval = f->d_sx = f->d_sdg = nullptr;
     f->fslev.clear();
@@ -1804,6 +1808,9 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     ar.space(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
     ar.space(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
     ar.space((void **)&f->d_zero, 8 * sizeof(int));  // zero pivot, flow give-ups, claim counter
+    // flow items (factor rows; solve items hold >= 1 row each, U's included) <= n
+    ar.space((void **)&f->d_fdone, (size_t)std::max(n, 1) * sizeof(int));
+    ar.space((void **)&f->d_tk, 2 * rsp::kFlowTicketCtrs * sizeof(unsigned));
     int4 *d_desc = nullptr;
     long long *d_offs = nullptr;
     if (!hp->slot_desc.empty()) {
@@ -1828,8 +1835,12 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     }
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero + 1, 0, 7);
+    if (e == hipSuccess) e = hipMemsetD32(f->d_fdone, 0, (size_t)std::max(n, 1));
+    if (e == hipSuccess) e = hipMemsetD32(f->d_tk, 0, 2 * rsp::kFlowTicketCtrs);
+    f->tk_seq = 0;
     f->fac_gen = 0;
     f->claim_host = 0;
+    f->flow_epoch = 0;
     f->solve_gen[0] = f->solve_gen[1] = f->solve_gen[2] = 0;
     // fat factor slots, written on the device from the uploaded symbolic
     // arrays; the layout is an optimisation: without its memory, or if the
@@ -2168,9 +2179,15 @@ static rsp::FlowCtl flow_ctl(rsp_ilu0_info *f, int word, int gen) {
     const long long us = std::max(env_int("RSP_ILU_FLOW_TIMEOUT_US", 200000), 0);
     c.ticks = (unsigned long long)us * 100ull;  // 100 MHz wall clock
     c.claim = reinterpret_cast<unsigned long long *>(f->d_zero + 6);
-    c.exits = f->d_zero + 5;
     c.claim_host = &f->claim_host;
     c.mode = env_int("RSP_ILU_FLOW_MODE", rsp::kFlowTickets);
+    c.done = f->d_fdone;
+    c.tickets = f->d_tk;
+    c.grid_x = std::max(env_int("RSP_ILU_FLOW_GRID_X", 1), 1);
+    c.tk_seq = &f->tk_seq;
+    // (2^32 calls of one info before an epoch repeats; 0 is the array's initial value)
+    if (++f->flow_epoch == 0) f->flow_epoch = 1;
+    c.epoch = f->flow_epoch;
     return c;
 }
 

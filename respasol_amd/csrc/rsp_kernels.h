@@ -298,17 +298,20 @@ struct FacFlowRun {
 // Flow launches (ilu0_flow, trsv_flow): one launch over a run of work items
 // in level order; an item waits only for items of lower index.
 // Item assignment (FlowCtl::mode):
-//  * start tickets (kFlowTickets, the default, RSP_ILU_FLOW_MODE=2): the
-//    workgroups take tickets in the order they run (ONE agent-scope
-//    fetch_add per workgroup per round of four items, claimed a round ahead;
-//    ilu0.hip FlowClaims) and a ticket's waves run its four items. An item
-//    waits only on items of lower tickets, all held by workgroups that have
-//    started: the lowest unfinished item always belongs to a running
-//    workgroup, and a workgroup that cannot be scheduled yet holds no ticket
-//    anybody waits on. Progress needs no co-residency at all (a co-running
-//    kernel that holds all but a few CUs only slows the launch down). A
-//    launch of G workgroups over T = ceil(items / 4) tickets advances the
-//    counter by exactly T + 2 G (flow_claims on the host);
+//  * start tickets (kFlowTickets, the default, RSP_ILU_FLOW_MODE=2): each
+//    workgroup takes ONE ticket t when it starts (one agent-scope fetch_add)
+//    and its waves walk the static items of t (4 t + wave, + W, ...), so a
+//    resident grid runs exactly the static walk. A wave that has waited
+//    long (kFlowStealUs) while tickets < G are still unclaimed — some
+//    workgroups never started: a co-running kernel holds their CUs — claims
+//    one more ticket for its workgroup (a steal) and the workgroup's waves
+//    walk all its tickets' items in index order, restarting an item whose
+//    wait they abandon (a flow item writes nothing before its waits).
+//    Every ticket is then held by a workgroup that has started, and the
+//    lowest unfinished item is its owner's next: progress needs no
+//    co-residency (ilu0.hip FlowClaims). The tickets come from eight
+//    counters of one of two slots (launch sequence number & 1), zeroed by
+//    the launch before;
 //  * static (RSP_ILU_FLOW_MODE=0): wave w of the grid takes items w, w + W, ... Progress
 //    needs every workgroup of the grid resident together: the grid is sized
 //    from the occupancy query (one 4-wave workgroup per CU by default), and
@@ -333,12 +336,22 @@ struct FlowCtl {
     int gen;                          // this call's generation (>= 1)
     unsigned long long ticks;         // give-up bound (RSP_ILU_FLOW_TIMEOUT_US)
     unsigned long long *claim;        // device claim counter
-    int *exits;                       // device: workgroups of a ticket launch that have finished (0 between launches)
     unsigned long long *claim_host;   // host: claims issued by the launches enqueued so far
     int mode;                         // RSP_ILU_FLOW_MODE: 0 static items, kFlowClaims claimed items, kFlowTickets start tickets
+    unsigned *tickets;                // tickets: two slots of kFlowTicketCtrs counters (launch seq & 1)
+    unsigned long long *tk_seq;       // host: ticket launches enqueued so far (a launch's `base`)
+    int *done;                        // tickets: per item, the epoch of the call that finished it (after a steal)
+    int grid_x;                       // tickets, tests: grid x this past the resident one (RSP_ILU_FLOW_GRID_X)
+    unsigned epoch;                   // this call's epoch (unique per call of the info, >= 1)
 };
 constexpr int kFlowClaims = 1;
 constexpr int kFlowTickets = 2;
+constexpr int kFlowTicketCtrs = 8;    // tickets: start-claim counters per launch
+constexpr int kFlowOwnMax = 1024;     // tickets: the most one workgroup can own (>= the largest flow grid)
+#ifndef RSP_TK_STEAL_US
+#define RSP_TK_STEAL_US 50
+#endif
+constexpr int kFlowStealUs = RSP_TK_STEAL_US;      // tickets: a wait this long may steal (2 us once the workgroup has)
 
 
 struct IluArgs {

@@ -91,3 +91,45 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "WORLD_SIZE is 1" in r.stderr
+
+
+def _meta_worker(rank, world, port, names, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        bench._import_product()
+        q.put((rank, bench.partition_meta(names, world, rank)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_partition_meta_is_rank0s_broadcast():
+    """the whole-matrix row-length pass runs on rank 0 only;
+    every rank receives the same (m, nnz, bounds) as a single process computes
+    (gloo, world 2, small surrogate matrices)."""
+    import socket
+    import numpy as np
+    import torch.multiprocessing as mp
+    from respasol_amd import csr
+    names = ["ASIC_320ks", "ecology2"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_meta_worker, args=(r, 2, port, names, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for name, *per_rank in zip(names, got[0], got[1]):
+        m = csr.surrogate_rows(name)
+        rowptr = np.zeros(m + 1, np.int64)
+        np.cumsum(csr.surrogate_rowlens(name), out=rowptr[1:])
+        want = csr.partition_rows(rowptr.astype(np.int32), 2)
+        for mm, nnz, b in per_rank:
+            assert mm == m and nnz == int(rowptr[-1]) and np.array_equal(b, want)

@@ -467,6 +467,24 @@ def test_flow_segments(handle, monkeypatch, flow, wpc, mode, name, scale):
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
+@pytest.mark.parametrize("grid_x", [4, 16])
+@pytest.mark.parametrize("name,scale", [("xenon2", 0.3), ("offshore", 0.2), ("ss1", 0.2)])
+def test_flow_tickets_oversubscribed(handle, monkeypatch, grid_x, name, scale):
+    """Start tickets with a flow grid grid_x times the resident one
+    (RSP_ILU_FLOW_GRID_X, capped at 1024 workgroups): workgroups start only
+    as others end, so the launches finish only through steals (a waiting
+    workgroup claims the tickets of those not started) and the rerun of
+    yielded items — with recovery off and the oracle's bits."""
+    monkeypatch.setenv("RSP_ILU_FLOW", "1")
+    monkeypatch.setenv("RSP_ILU_FLOW_MODE", "2")
+    monkeypatch.setenv("RSP_ILU_FLOW_RECOVER", "0")
+    monkeypatch.setenv("RSP_ILU_FLOW_GRID_X", str(grid_x))
+    A = csr.surrogate(name, scale)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float64, handle, x=x)
+    compare(A, torch.float32, handle, x=x, true_lu=True)
+
+
 def test_flow_give_up_is_reported(handle, monkeypatch):
     """A persistent (flow) launch whose dependency wait gives up is reported,
     not silent, when recovery is off
