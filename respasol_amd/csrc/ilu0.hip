@@ -517,7 +517,11 @@ struct FlowClaims {
                 for (int q = 0; q < rsp::kFlowTicketCtrs; ++q)
                     __hip_atomic_store(fc.tickets + rsp::kFlowTicketCtrs * (int)((base + 1) & 1) + q, 0u,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef RSP_TK_BLOCKIDX
+            const int t = blockIdx.x;
+#else
             const int t = take(blockIdx.x % rsp::kFlowTicketCtrs);
+#endif
             L->own[0] = t;
             L->state = t < (int)gridDim.x ? 1 : 0;
             L->lock = 0;
@@ -713,14 +717,16 @@ struct FlowClaims {
             }
             return;
         }
-        if (redo) {  // the item yielded: it runs again unless the owned list grows
+        if (__builtin_expect(!redo && !scan && nseen == 1, 1)) {  // the static walk of the start ticket
+            cur += stride;
+            ++k;
+            if (cur < it1) return;
+        } else if (redo) {  // the item yielded: it runs again unless the owned list grows
             redo = false;
             const int n = steal();
             if (n == 0) return;
             rescan(n);
-        } else if (!scan && nseen == 1)
-            ++k;
-        else
+        } else
             ++j;
         settle();
     }

@@ -2360,10 +2360,12 @@ static rsp::TrsvArgs trsv_args(rsp_handle_t h, rsp_ilu0_info *f, const void *alp
     a.narrow_pairs = env_int("RSP_ILU_NARROW_PAIRS", -1);  // -1: by the DAG's level width (launcher)
     a.loaders = env_int("RSP_ILU_LOADERS", 1);
     a.flow = env_int("RSP_ILU_FLOW", 1) != 0;
-    // every workgroup of a flow launch must be resident at once (an item waits
-    // for items of lower index only, and workgroups take items in index
-    // order): 256-thread workgroups, RSP_ILU_FLOW_WPC (default 4) waves per CU
-    a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 4), 4), 16) / 4;
+    // 256-thread workgroups, RSP_ILU_FLOW_WPC waves per CU: 8 for the solves
+    // (config 3, start tickets: solve 34.34 -> 33.95 ms against 4; the
+    // factor's flow stays at 4: 40.11 vs 40.15 ms); no residency is needed
+    // with start tickets, the static walk (RSP_ILU_FLOW_MODE=0) needs the
+    // whole grid resident (flow_grid caps it by the occupancy query)
+    a.flow_grid = h->num_cus * std::min(std::max(env_int("RSP_ILU_FLOW_WPC", 8), 4), 16) / 4;
     a.flow_cus = h->num_cus;
     a.flow_sleep = std::min(std::max(env_int("RSP_ILU_FLOW_SLEEP", 1), 1), 64);
     return a;
