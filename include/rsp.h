@@ -148,10 +148,13 @@ rsp_status_t rsp_destroy_ilu0_info(rsp_ilu0_info_t info);
 rsp_status_t rsp_ilu0_buffer_size(rsp_handle_t handle, int n, int nnz, rsp_datatype_t value_type,
                                   rsp_ilu0_info_t info, size_t *buffer_size);
 
-/* cusparse?csrilu02_analysis + both csrsv2_analysis (GPU/ilu0.cu:203-252):
- * diagonal positions, structural-zero detection, level sets of the lower
- * triangle (factor + L-solve) and of its transpose (L^T-solve), and the
- * transposed strict-lower index map. `nnz` may exceed offsets[n] (the
+/* cusparse?csrilu02_analysis (GPU/ilu0.cu:203-217, the reference's timed
+ * "Symbolic"): diagonal positions, structural-zero detection, the symbolic
+ * factor, level sets of the lower triangle (factor + L-solve) and of its
+ * transpose (L^T-solve), and the factor plan. The two solve plans (the
+ * csrsv2_analysis half, rsp_trsv_analysis below) are started on a worker
+ * thread as soon as the levels exist and left running when this call
+ * returns. `nnz` may exceed offsets[n] (the
  * reference passes A.nnz, GPU/ilu0.cu:166); offsets[n] is what is analysed.
  * Each row's column indices must be strictly increasing (sorted, no
  * duplicates — as csrilu02 requires); otherwise INVALID_VALUE. The reference
@@ -160,6 +163,13 @@ rsp_status_t rsp_ilu0_buffer_size(rsp_handle_t handle, int n, int nnz, rsp_datat
  * Host-blocking (reads the pattern once). */
 rsp_status_t rsp_ilu0_analysis(rsp_handle_t handle, int n, int nnz, const int *d_row_offsets,
                                const int *d_col_ind, rsp_ilu0_info_t info);
+
+/* cusparse?csrsv2_analysis for the L (op NON_TRANSPOSE) or L^T (op
+ * TRANSPOSE) solve of an analysed info (GPU/ilu0.cu:228-252, untimed there):
+ * waits for the solve plans rsp_ilu0_analysis started and uploads them (the
+ * first call does both kinds; later calls return at once). Optional — the
+ * first solve does it if it was not called. Host-blocking. */
+rsp_status_t rsp_trsv_analysis(rsp_handle_t handle, rsp_operation_t op, rsp_ilu0_info_t info);
 
 /* cusparseXcsrilu02_zeroPivot (GPU/ilu0.cu:222,278). Host-blocking. Returns
  * RSP_STATUS_ZERO_PIVOT and *position = j (0-based) when A(j,j) is

@@ -105,6 +105,7 @@ RSP_PROTOS = {
     "rsp_trsv_upper": (i32, [vp, vp, vp, i32, vp, vp, vp]),
     "rsp_ilu0_levels": (i32, [vp, ip, ip]),
     "rsp_ilu0_solve_blocks": (i32, [vp, ip, ip]),
+    "rsp_trsv_analysis": (i32, [vp, i32, vp]),
     "rsp_gather": (i32, [vp, i32, i64, vp, vp, vp]),
     "rsp_scatter": (i32, [vp, i32, i64, vp, vp, vp]),
     "rsp_spmat_set_local_cols": (i32, [vp, i64]),

@@ -57,6 +57,35 @@ using rsp::TrsvArgs;
 __device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+// x / d, the IEEE quotient rounded to T. The FTZ build's float division
+// switches the denormal mode on and off around its Newton steps (two
+// s_setreg per division: the only difference between ilu0_rounds<float> in
+// rsp_k and rsp_k_ftz, found in their ISA), serialising the wave on every
+// l_ik = a_ik / u_kk. Here the FTZ build takes a float quotient in double,
+// rounded once to float: double has >= 2 * 24 + 2 bits, so that is the
+// correctly rounded float quotient for every operand, with fp32 denormals
+// flushed by the mode as the oracle's DAZ/FTZ (same bits as the float
+// division). Measured on dc1, matrix-new_3, xenon2, ASIC_320ks, crashbasis
+// (FTZ factor, ms): float division 25.32, this 24.89; the float Newton
+// sequence without the mode switch is 24.06 but loses the correct rounding
+// when a residual is denormal (numerators near 2^-103, divisors >= 2^126),
+// and guarding it (range checks + rescaling, 26.33; a fallback branch,
+// 27.88) costs more than it saves: the division is on the factor's
+// dependency chain (profiles/r06_ftz_division_ab.txt).
+template <typename T>
+__device__ __forceinline__ T qdiv(T x, T d) {
+#ifdef RSP_FTZ_BUILD
+    if constexpr (sizeof(T) == 4) {
+        // (the empty asm keeps the optimiser from folding the widened
+        // division back into a float one, a legal rewrite it makes)
+        double xd = x, dd = d;
+        asm volatile("" : "+v"(xd), "+v"(dd));
+        return (float)(xd / dd);
+    }
+#endif
+    return x / d;
+}
+
 
 // s - sum_p v_p y_p as a serial fma chain over p = p0 .. p1-1, ascending.
 // The operands of B consecutive terms are loaded together (clamped,
@@ -175,7 +204,7 @@ __device__ __forceinline__ void factor_row(const IluArgs &a, int i, int lane) {
             const int p = a.lord[x];
             const int k = a.colidx[p];
             const T ukk = a.hasdiag[k] ? vals[a.dpos[k]] : T(0);
-            vals[p] = factor_entry<T, B>(a, vals, p) / ukk;
+            vals[p] = qdiv<T>(factor_entry<T, B>(a, vals, p), ukk);
         }
         // this stage's l_ik visible to the next stage's lanes
         __threadfence_block();
@@ -318,7 +347,7 @@ __device__ __forceinline__ void row_lds_factor(T *rv, const T *dv, const T *pu, 
         for (int x = s + lane; x < e; x += 64) {
             const int r = lo[x];
             const T d = dv[r];  // read before the chain, not after it
-            rv[r] = entry(r) / d;
+            rv[r] = qdiv<T>(entry(r), d);
         }
         wave_sync();
         s = e;
@@ -1075,7 +1104,7 @@ __global__ __launch_bounds__(256) void ilu0_scale_lower(IluArgs a) {
     auto scale = [&](int p) {
         const int k = a.colidx[p];
         const T ukk = a.hasdiag[k] ? vals[a.dpos[k]] : T(0);
-        vals[p] = vals[p] / ukk;
+        vals[p] = qdiv<T>(vals[p], ukk);
     };
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < a.n) {
@@ -1227,7 +1256,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
             batch(u0);
             for (int u = u0 + 4; u < u1; u += 4) batch(u);
         }
-        if (r.z >= 0) v = v / dv;
+        if (r.z >= 0) v = qdiv<T>(v, dv);
         V[cb + it] = v;
         if constexpr (STORE) {
             vals[r.x] = v;
@@ -1319,7 +1348,7 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                     if (u + b < u1) v = fma_t(-l[b], w[b], v);
             }
         }
-        if (r.z >= 0) v = v / dv;
+        if (r.z >= 0) v = qdiv<T>(v, dv);
         V[cb + it] = v;
     };
     auto wave_order = [] {
@@ -1575,7 +1604,7 @@ __global__ __launch_bounds__(256) void trsv_level(TrsvArgs a, int off, int nrows
         }
         if ((threadIdx.x & 63) != 0) return;
     }
-    if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
+    if constexpr (KIND == 2) s = qdiv<T>(s, ((const T *)a.sdg)[x]);
     y[t.i] = s;
 }
 
@@ -1654,7 +1683,7 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, u
 #pragma unroll
             for (int b = 0; b < F; ++b)
                 if (b < n) s = fma_t(-v[b], __builtin_bit_cast(T, w[b]), s);
-            if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
+            if constexpr (KIND == 2) s = qdiv<T>(s, ((const T *)a.sdg)[x]);
             if (lane < f.n && !yl) flow_store(y + t.i, s);
             fq.item_end(it, yl);
         } else {  // one row of more terms: a wave, 64 terms at a time on LDS broadcast operands
@@ -1687,7 +1716,7 @@ __global__ __launch_bounds__(256) void trsv_flow(TrsvArgs a, int it0, int it1, u
                 for (; j < cnt; ++j) s = fma_t(-fwv[wv][j], fwy[wv][j], s);
                 wave_sync();  // this group's reads before the next group's stores
             }
-            if constexpr (KIND == 2) s = s / ((const T *)a.sdg)[x];
+            if constexpr (KIND == 2) s = qdiv<T>(s, ((const T *)a.sdg)[x]);
             if (lane == 0 && !yl) flow_store(y + t.i, s);
             fq.item_end(it, yl);
         }
@@ -2068,7 +2097,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             } else {
                 s = group_fma(cR.x, lval[g0], cI);
             }
-            if constexpr (KIND == 2) s = s / ldg[cr];
+            if constexpr (KIND == 2) s = qdiv<T>(s, ldg[cr]);
             put(cR.out, s);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
@@ -2232,7 +2261,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 if (__ballot(ng >= 3))
                     for (int g = 2; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
             }
-            if constexpr (KIND == 2) s = s / ldg[cr];
+            if constexpr (KIND == 2) s = qdiv<T>(s, ldg[cr]);
             put(R.out, s);
             lds_publish(&lds_done, L + 1, lane == 0);  // after the y stores
             if (a.trace && lane == 0 && L < a.trace_cap / 2)  // diagnostics: level end stamps
@@ -2314,7 +2343,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                         for (int g = 2; g < ng; ++g) s = group_fma(s, lval[g0 + g], lidx[g0 + g]);
                 }
             }
-            if constexpr (KIND == 2) s = s / ldg[cr];
+            if constexpr (KIND == 2) s = qdiv<T>(s, ldg[cr]);
             put(R.out, s);
             if (has2) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -2349,7 +2378,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                     if (__ballot(nh >= 2))
                         for (int g = 1; g < nh; ++g) t = group_fma(t, lval[h0 + g], lidx[h0 + g]);
                 }
-                if constexpr (KIND == 2) t = t / ldg[cr2];
+                if constexpr (KIND == 2) t = qdiv<T>(t, ldg[cr2]);
                 put(R2.out, t);
             }
             lds_publish(&lds_done, L + (has2 ? 2 : 1), lane == 0);  // after the y stores
@@ -2395,7 +2424,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
             if (tid < ns) {  // (ns <= kChunkRows <= NTH)
                 const ThinRow<T> r = lrow[off + tid];
                 T s = row_value(r);
-                if constexpr (KIND == 2) s = s / ldg[off + tid];
+                if constexpr (KIND == 2) s = qdiv<T>(s, ldg[off + tid]);
                 put(r.out, s);
             }
             for (int r = ns + (tid >> 6); r < cnt; r += NTH / 64) {  // long rows: a wave each
@@ -2410,7 +2439,7 @@ __global__ __launch_bounds__(rsp::kThinThreads) void trsv_thin_pf(TrsvArgs a, in
                 const int g0 = t.g & 0xffff, ng = t.g >> 16;
                 T s = ng > 0 ? groups_fma(t.x, g0, g0 + ng) : t.x;
 #endif
-                if constexpr (KIND == 2) s = s / ldg[off + r];
+                if constexpr (KIND == 2) s = qdiv<T>(s, ldg[off + r]);
                 if ((tid & 63) == 0) put(t.out, s);
             }
             lds_barrier();

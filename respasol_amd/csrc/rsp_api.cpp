@@ -152,8 +152,19 @@ struct rsp_ilu0_info {
     void *d_arena_pairs = nullptr;  // device analysis: upd_l, upd_u
     void *d_usval = nullptr;    // U solve term values (trsv_stream), in d_arena_u
     unsigned long long digest = 0;  // rsp_an::digest of the host plan
-    std::unique_ptr<rsp_an::IluHostPlan> host;  // kept for the U plan
+    std::unique_ptr<rsp_an::IluHostPlan> host;  // kept for the solve plans and the U plan
     rsp_an::hvec<int> host_rp, host_ci;
+    // The L and L^T solve plans (the reference's two csrsv2_analysis calls,
+    // GPU/ilu0.cu:228-252): built on a worker thread that rsp_ilu0_analysis
+    // starts once the levels exist and leaves running; ilu_solves_ready
+    // (rsp_trsv_analysis, or the first solve) joins it and uploads them.
+    // (Declared after host / host_rp / host_ci, which it reads: destroyed,
+    // i.e. joined, before them.)
+    std::unique_ptr<rsp_an::Task> solves_task;
+    bool solves_ready = false;
+    bool dev_terms = true;      // the per-term half of the solve plans is built on the device
+    void *d_arena_s = nullptr;  // the solve plans' allocation
+    rsp_handle_t han = nullptr; // the handle of the analysis (its stream uploads the solve plans)
     // Recovery of a call whose flow wait gave up (a co-running kernel kept
     // some of the flow launch's workgroups from being scheduled past the
     // give-up bound): rsp_ilu0_zero_pivot / rsp_trsv_zero_pivot re-run it
@@ -1186,6 +1197,10 @@ rsp_status_t rsp_scatter(rsp_handle_t h, rsp_datatype_t value_type, int64_t n, c
 /* --------------------------------------------------------------- ILU(0) */
 
 static void ilu_free_device(rsp_ilu0_info *f) {
+    f->solves_task.reset();  // (joins a solve planning still running)
+    f->solves_ready = false;
+    if (f->d_arena_s) (void)hipFree(f->d_arena_s);
+    f->d_arena_s = nullptr;
     // every array except the slot layout lives in the arenas
     if (f->d_arena) (void)hipFree(f->d_arena);
     if (f->d_arena_u) (void)hipFree(f->d_arena_u);
@@ -1309,8 +1324,10 @@ static void dag_upload(Arena &ar, rsp_ilu0_info::Dag &d, const rsp_an::DagHost &
     d.nwave = h.sp.nwave;
     d.sbase = h.sp.sbase;
     d.nterms = (int)h.sp.tpos.size();
-    ar.up(&d.d_rows, h.rows);
-    ar.up(&d.d_ptr, h.ptr);
+    if (!d.d_rows) {  // (L's levels may be in the factor's arena already)
+        ar.up(&d.d_rows, h.rows);
+        ar.up(&d.d_ptr, h.ptr);
+    }
     ar.up(&d.d_tasks, h.sp.tasks);
     ar.up(&d.d_nshort, h.sp.nshort);
     ar.up(&d.d_tpos, h.sp.tpos);
@@ -1361,8 +1378,10 @@ static void dag_upload_rows(Arena &ar, rsp_ilu0_info::Dag &d, const rsp_an::DagH
     const size_t nx = h.rows.size(), nch = h.sp.chunks.size();
     long long thin_terms = 0;
     for (const rsp::LevelChunk &ch : h.sp.chunks) thin_terms += ch.k1 - ch.k0;
-    ar.up(&d.d_rows, h.rows);
-    ar.up(&d.d_ptr, h.ptr);
+    if (!d.d_rows) {  // (L's levels may be in the factor's arena already)
+        ar.up(&d.d_rows, h.rows);
+        ar.up(&d.d_ptr, h.ptr);
+    }
     ar.up(&d.d_tasks, h.sp.tasks);
     ar.up(&d.d_nshort, h.sp.nshort);
     ar.space((void **)&d.d_tpos, (size_t)d.nterms * 4);
@@ -1701,28 +1720,32 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     const bool dev_terms = n > 0 && !env_int("RSP_ILU_HOST_TERMS", 0);
     // (declared after rp, ci, hp: destroyed - joined - before them if the
     // factor plan throws)
+    // the solve plans' thread outlives this call (rsp_ilu0_info::solves_task):
+    // it holds the buffers, which move into the info below, not the locals
     std::unique_ptr<rsp_an::Task> solves;
+    const int *rpd = rp.data(), *cid = ci.data();
+    rsp_an::IluHostPlan *H = hp.get();
     rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph, [&] {
-        solves.reset(new rsp_an::Task([&] {
+        solves.reset(new rsp_an::Task([rpd, cid, H, n, dev_terms] {
             // block-inverse plans of the deep DAGs, beside the row plans
             auto blk = [&](int kind) {
-                const rsp_an::DagHost &dg = kind == 0 ? hp->L : hp->LT;
+                const rsp_an::DagHost &dg = kind == 0 ? H->L : H->LT;
                 if (!rsp_an::blocks_wanted(n, (int)dg.ptr.size() - 1)) return;
-                bool &has = kind == 0 ? hp->has_lb : hp->has_ltb;
-                has = rsp_an::plan_blocks(kind, rp.data(), ci.data(), *hp, kind == 0 ? hp->Lb : hp->LTb);
+                bool &has = kind == 0 ? H->has_lb : H->has_ltb;
+                has = rsp_an::plan_blocks(kind, rpd, cid, *H, kind == 0 ? H->Lb : H->LTb);
             };
             rsp_an::Task bl([&] { blk(0); }), bt([&] { blk(1); });
             if (dev_terms)
-                rsp_an::plan_solves_rows(rp.data(), ci.data(), *hp);
+                rsp_an::plan_solves_rows(rpd, cid, *H);
             else
-                rsp_an::plan_solves(rp.data(), ci.data(), *hp);
+                rsp_an::plan_solves(rpd, cid, *H);
             bl.join();
             bt.join();
         }));
     });
     if (st == RSP_STATUS_SUCCESS) rsp_an::plan_factor(rp.data(), ci.data(), slot_cap_ints(), *hp);
-    if (solves) solves->join();  // rethrows the solve plans' exception
     if (st != RSP_STATUS_SUCCESS) {
+        solves.reset();  // (joined before the buffers it reads go)
         ilu_free_device(f);
         return st;
     }
@@ -1771,42 +1794,16 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     f->fac_scale = hp->fac_scale;
     if (hp->fac_one) {
         f->F.ptr = hp->F.ptr;
-        f->F.group = hp->L.group;
-        f->F.batch = hp->L.batch;
         ar.up(&f->F.d_rows, hp->F.rows);
         ar.up(&f->F.d_ptr, hp->F.ptr);
+    } else {  // the factor walks L's levels (the solve plans add the rest of L at ilu_solves_ready)
+        f->L.ptr = hp->L.ptr;
+        ar.up(&f->L.d_rows, hp->L.rows);
+        ar.up(&f->L.d_ptr, hp->L.ptr);
     }
+    f->LT.ptr = hp->LT.ptr;  // (level count, rsp_ilu0_levels)
     // flow runs: the saved upper input values of their rows (ilu0_flow_prep)
     if (!hp->fruns.empty()) ar.space(&f->d_forig, (size_t)std::max(hp->nnz_s, 1) * sizeof(double));
-    rsp_k::SolveTermsArgs tl{}, tt{};
-    if (dev_terms) {
-        dag_upload_rows(ar, f->L, hp->L, n, tl);
-        dag_upload_rows(ar, f->LT, hp->LT, n, tt);
-        tl.kind = 0;
-        tl.rp = d_row_offsets;
-        tl.ci = d_col_ind;
-        // the split term order (rsp_an::split_terms); none (nullptr) for the
-        // reference's order
-        if (!hp->lpos.empty()) {
-            ar.up((int **)&tl.lpos, hp->lpos);
-            ar.up((int **)&tl.ne, hp->ne_l);
-            ar.up((int **)&tt.ne, hp->ne_lt);
-        }
-        tt.kind = 1;
-        ar.up((int **)&tt.ltp, hp->ltp);
-        ar.up((int **)&tt.lts, hp->lts);
-        ar.up((int **)&tt.ltc, hp->ltc);
-    } else {
-        dag_upload(ar, f->L, hp->L);
-        dag_upload(ar, f->LT, hp->LT);
-    }
-    if (hp->has_lb) blk_upload(ar, f->Lb, hp->Lb);
-    if (hp->has_ltb) blk_upload(ar, f->LTb, hp->LTb);
-    // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
-    const size_t nt = (size_t)std::max({f->L.nterms, f->LT.nterms, 1});
-    ar.space(&f->d_sval, nt * sizeof(double));
-    ar.space(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
-    ar.space(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
     ar.space((void **)&f->d_zero, 8 * sizeof(int));  // zero pivot, flow give-ups, claim counter
     // flow items (factor rows; solve items hold >= 1 row each, U's included) <= n
     ar.space((void **)&f->d_fdone, (size_t)std::max(n, 1) * sizeof(int));
@@ -1820,19 +1817,6 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     up_step("arena build");
     hipError_t e = ar.commit(&f->d_arena, h->stream);
     up_step("commit (H2D)");
-    if (e == hipSuccess && dev_terms) {
-        tl.dpos = f->d_dpos;
-        e = dag_build_terms(f->L, tl, h->stream);
-        if (e == hipSuccess) e = dag_build_terms(f->LT, tt, h->stream);
-    }
-    up_step("solve terms");
-    if (e == hipSuccess && env_int("RSP_ILU_DIGEST", 0)) {  // tests only
-        if (dev_terms) {
-            e = dag_download_terms(f->L, tl, hp->L, h->stream);
-            if (e == hipSuccess) e = dag_download_terms(f->LT, tt, hp->LT, h->stream);
-        }
-        f->digest = e == hipSuccess && f->digest ? rsp_an::digest(*hp) : 0;
-    }
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero, INT_MAX, 1);
     if (e == hipSuccess) e = hipMemsetD32(f->d_zero + 1, 0, 7);
     if (e == hipSuccess) e = hipMemsetD32(f->d_fdone, 0, (size_t)std::max(n, 1));
@@ -1877,6 +1861,100 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
         ilu_free_device(f);
         return e == hipErrorOutOfMemory ? RSP_STATUS_ALLOC_FAILED : RSP_STATUS_EXECUTION_FAILED;
     }
+    // (the buffers keep their addresses: the solve plans' thread reads them on)
+    f->host_rp.swap(rp);
+    f->host_ci.swap(ci);
+    f->host = std::move(hp);
+    f->solves_task = std::move(solves);
+    f->dev_terms = dev_terms;
+    f->han = h;
+    f->n = n;
+    f->nnz_s = nnz_s;
+    f->rowptr = d_row_offsets;
+    f->colidx = d_col_ind;
+    f->analysed = 1;
+    return RSP_STATUS_SUCCESS;
+}
+
+// The L and L^T solve plans (rsp_trsv_analysis, or the first solve): wait
+// for their thread (started by rsp_ilu0_analysis) and upload them — the row
+// plans, the block-inverse plans of deep DAGs, the solve streams — and build
+// their per-term half on the device. Once per analysis.
+static rsp_status_t ilu_solves_ready(rsp_handle_t h, rsp_ilu0_info *f) {
+    if (f->solves_ready) return RSP_STATUS_SUCCESS;
+    if (!f->analysed || !f->host || !h) return RSP_STATUS_INVALID_VALUE;
+    if (f->solves_task) {
+        std::unique_ptr<rsp_an::Task> t = std::move(f->solves_task);
+        t->join();  // rethrows the solve plans' exception (guarded: an error status)
+    }
+    rsp_an::IluHostPlan *hp = f->host.get();
+    const int n = f->n;
+    const bool dev_terms = f->dev_terms;
+    const int *d_row_offsets = f->rowptr, *d_col_ind = f->colidx;
+    const bool tm3 = env_int("RSP_ILU_TIMING", 0) >= 3;  // diagnostics
+    auto t_up = std::chrono::steady_clock::now();
+    auto up_step = [&](const char *what) {
+        if (!tm3) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "rsp_trsv_analysis n=%d     upload: %-16s %8.2f ms\n", n, what,
+                std::chrono::duration<double, std::milli>(t - t_up).count());
+        t_up = t;
+    };
+    Arena ar;
+    rsp_k::SolveTermsArgs tl{}, tt{};
+    if (dev_terms) {
+        dag_upload_rows(ar, f->L, hp->L, n, tl);
+        dag_upload_rows(ar, f->LT, hp->LT, n, tt);
+        tl.kind = 0;
+        tl.rp = d_row_offsets;
+        tl.ci = d_col_ind;
+        // the split term order (rsp_an::split_terms); none (nullptr) for the
+        // reference's order
+        if (!hp->lpos.empty()) {
+            ar.up((int **)&tl.lpos, hp->lpos);
+            ar.up((int **)&tl.ne, hp->ne_l);
+            ar.up((int **)&tt.ne, hp->ne_lt);
+        }
+        tt.kind = 1;
+        ar.up((int **)&tt.ltp, hp->ltp);
+        ar.up((int **)&tt.lts, hp->lts);
+        ar.up((int **)&tt.ltc, hp->ltc);
+    } else {
+        dag_upload(ar, f->L, hp->L);
+        dag_upload(ar, f->LT, hp->LT);
+    }
+    if (hp->has_lb) blk_upload(ar, f->Lb, hp->Lb);
+    if (hp->has_ltb) blk_upload(ar, f->LTb, hp->LTb);
+    // solve streams: values per flat term, alpha x and u_ii per level-order slot (fp64 size)
+    const size_t nt = (size_t)std::max({f->L.nterms, f->LT.nterms, 1});
+    ar.space(&f->d_sval, nt * sizeof(double));
+    ar.space(&f->d_sx, (size_t)std::max(n, 1) * sizeof(double));
+    ar.space(&f->d_sdg, (size_t)std::max(n, 1) * sizeof(double));
+    up_step("arena build");
+    hipError_t e = ar.commit(&f->d_arena_s, h->stream);
+    up_step("commit (H2D)");
+    if (e == hipSuccess && dev_terms) {
+        tl.dpos = f->d_dpos;
+        e = dag_build_terms(f->L, tl, h->stream);
+        if (e == hipSuccess) e = dag_build_terms(f->LT, tt, h->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    up_step("solve terms");
+    if (e == hipSuccess && env_int("RSP_ILU_DIGEST", 0)) {  // tests only
+        if (dev_terms) {
+            e = dag_download_terms(f->L, tl, hp->L, h->stream);
+            if (e == hipSuccess) e = dag_download_terms(f->LT, tt, hp->LT, h->stream);
+        }
+        f->digest = e == hipSuccess && f->digest ? rsp_an::digest(*hp) : 0;
+    }
+    if (e != hipSuccess) {
+        if (f->d_arena_s) (void)hipFree(f->d_arena_s);
+        f->d_arena_s = nullptr;
+        f->L = f->LT = rsp_ilu0_info::Dag();
+        f->Lb = f->LTb = rsp_ilu0_info::BlkDag();
+        f->analysed = 0;  // (the factor's L levels went with L: analyse again)
+        return e == hipErrorOutOfMemory ? RSP_STATUS_ALLOC_FAILED : RSP_STATUS_EXECUTION_FAILED;
+    }
     // host copies kept for the U plan, built on first use (rsp_trsv_upper)
     hp->sym = rsp_an::IluSymbolic();
     hp->fplan = rsp_an::FacPlan();
@@ -1892,14 +1970,7 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     hp->frow.clear();
     hp->slot_desc.clear();
     hp->slot_offs.clear();
-    f->host_rp.swap(rp);
-    f->host_ci.swap(ci);
-    f->host = std::move(hp);
-    f->n = n;
-    f->nnz_s = nnz_s;
-    f->rowptr = d_row_offsets;
-    f->colidx = d_col_ind;
-    f->analysed = 1;
+    f->solves_ready = true;
     return RSP_STATUS_SUCCESS;
 }
 
@@ -1998,13 +2069,18 @@ static rsp_status_t rsp_spmv_plan_host_impl(int m, const int *rp, const int *ci,
 }
 
 rsp_status_t rsp_ilu0_plan_digest(rsp_ilu0_info_t f, uint64_t *digest) {
-    if (!f || !digest || !f->analysed || !f->digest) return RSP_STATUS_INVALID_VALUE;
+    if (!f || !digest || !f->analysed) return RSP_STATUS_INVALID_VALUE;
+    const rsp_status_t st = ilu_solves_ready(f->han, f);  // (the digest covers the solve plans)
+    if (st != RSP_STATUS_SUCCESS) return st;
+    if (!f->digest) return RSP_STATUS_INVALID_VALUE;
     *digest = f->digest;
     return RSP_STATUS_SUCCESS;
 }
 
 rsp_status_t rsp_ilu0_solve_blocks(rsp_ilu0_info_t f, int *blocks_lower, int *blocks_upper) {
     if (!f || !blocks_lower || !blocks_upper || !f->analysed) return RSP_STATUS_INVALID_VALUE;
+    const rsp_status_t st = ilu_solves_ready(f->han, f);
+    if (st != RSP_STATUS_SUCCESS) return st;
     *blocks_lower = f->Lb.on ? f->Lb.nb : 0;
     *blocks_upper = f->LTb.on ? f->LTb.nb : 0;
     return RSP_STATUS_SUCCESS;
@@ -2408,6 +2484,10 @@ static rsp_status_t rsp_trsv_lower_unit_impl(rsp_handle_t h, rsp_operation_t op,
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
     if (op != RSP_OPERATION_NON_TRANSPOSE && op != RSP_OPERATION_TRANSPOSE) return RSP_STATUS_INVALID_VALUE;
+    {
+        const rsp_status_t st = ilu_solves_ready(h, f);  // (rsp_trsv_analysis not called: done here)
+        if (st != RSP_STATUS_SUCCESS) return st;
+    }
     remember_solve(h, f, op == RSP_OPERATION_NON_TRANSPOSE ? RSP_TRSV_L : RSP_TRSV_LT, op, alpha, value_type,
                    d_values, d_x, d_y);
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
@@ -2497,7 +2577,9 @@ static rsp_status_t rsp_trsv_upper_impl(rsp_handle_t h, const void *alpha, rsp_i
     if (!f || !f->analysed || !alpha) return RSP_STATUS_INVALID_VALUE;
     if (value_type != RSP_R_64F && value_type != RSP_R_32F) return RSP_STATUS_INVALID_VALUE;
     if (f->n > 0 && (!d_x || !d_y || d_x == d_y)) return RSP_STATUS_INVALID_VALUE;
-    rsp_status_t st = ilu_plan_u(h, f);  // planned on first use
+    rsp_status_t st = ilu_solves_ready(h, f);  // (the solve streams)
+    if (st != RSP_STATUS_SUCCESS) return st;
+    st = ilu_plan_u(h, f);  // planned on first use
     if (st != RSP_STATUS_SUCCESS) return st;
     remember_solve(h, f, RSP_TRSV_U, RSP_OPERATION_NON_TRANSPOSE, alpha, value_type, d_values, d_x, d_y);
     rsp::TrsvArgs a = trsv_args(h, f, alpha, value_type, d_values, d_x, d_y);
@@ -2579,6 +2661,15 @@ rsp_status_t rsp_ilu0_analysis_host(int n, const int *row_offsets, const int *co
 rsp_status_t rsp_ilu0_factor(rsp_handle_t h, rsp_ilu0_info_t f, rsp_datatype_t value_type,
                              void *d_values) {
     return guarded([&] { return rsp_ilu0_factor_impl(h, f, value_type, d_values); }, [] {});
+}
+
+rsp_status_t rsp_trsv_analysis(rsp_handle_t h, rsp_operation_t op, rsp_ilu0_info_t f) {
+    return guarded([&] {
+        if (!h) return RSP_STATUS_NOT_INITIALIZED;
+        if (!f || !f->analysed) return RSP_STATUS_INVALID_VALUE;
+        if (op != RSP_OPERATION_NON_TRANSPOSE && op != RSP_OPERATION_TRANSPOSE) return RSP_STATUS_INVALID_VALUE;
+        return ilu_solves_ready(h, f);
+    }, [] {});
 }
 
 rsp_status_t rsp_trsv_lower_unit(rsp_handle_t h, rsp_operation_t op, const void *alpha,

@@ -8,8 +8,9 @@
  *
  * Flow (GPU/ilu0.cu:29-342): load with outputbase 0 (:42-44); fp32 demotion
  * under --prec=fp32 (`#define FLOAT`, :55-63); x = 1 (:63,74); H2D;
- * bufferSize x3 (:165-194); [timed "Symbolic"] analysis (:196-217);
+ * bufferSize x3 (:165-194); [timed "Symbolic"] ILU analysis (:196-217);
  * structural zero pivot -> "A(%d,%d) is missing" and exit 0 (:221-226);
+ * the two trsv analyses, untimed (:228-252);
  * [timed "Numeric"] factorisation (:257-275); numerical zero pivot ->
  * "L(%d,%d) is zero" and exit 0 (:278-282); [timed "Solve"] L z = x then
  * L^T y = z with the unit-lower descriptor (:284-310 — the reference never
@@ -117,6 +118,9 @@ int main(int argc, char **argv) {
         printf("A(%d,%d) is missing\n", structural_zero, structural_zero);
         return 0;
     }
+    /* the two csrsv2_analysis calls (:228-252), untimed as there */
+    rspErrCheck(rsp_trsv_analysis(handle, RSP_OPERATION_NON_TRANSPOSE, info));
+    rspErrCheck(rsp_trsv_analysis(handle, RSP_OPERATION_TRANSPOSE, info));
 
     hipEventRecord(start, NULL);
     rspErrCheck(rsp_ilu0_factor(handle, info, dt, d_v));

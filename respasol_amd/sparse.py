@@ -246,8 +246,15 @@ class Ilu0:
         check(rsp.rsp_create_ilu0_info(C.byref(self._info)), "rsp_create_ilu0_info")
 
     def analysis(self) -> None:
+        """cusparse?csrilu02_analysis (rsp_ilu0_analysis): the solve plans
+        are finished by trsv_analysis() or the first solve."""
         check(rsp.rsp_ilu0_analysis(self.handle.ptr, self.n, self.nnz, _ptr(self.rowptr),
                                     _ptr(self.colidx), self._info), "rsp_ilu0_analysis")
+
+    def trsv_analysis(self, transpose: bool = False) -> None:
+        """cusparse?csrsv2_analysis (rsp_trsv_analysis) for the L (or L^T) solve."""
+        op = _lib.OP_T if transpose else _lib.OP_N
+        check(rsp.rsp_trsv_analysis(self.handle.ptr, op, self._info), "rsp_trsv_analysis")
 
     def zero_pivot(self) -> int:
         """-1 if none, else the 0-based row (cusparseXcsrilu02_zeroPivot)."""

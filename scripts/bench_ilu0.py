@@ -6,9 +6,11 @@ the oracle's sequential CPU time beside it and a bitwise parity check.
 
     python scripts/bench_ilu0.py [--set moderate] [--reps 3] [--json out.json]
 
-Times (ms): analysis (host-side level sets, wall clock), factor and solve
-(L then L^T, the reference's "Solve", GPU/ilu0.cu:284-310) as HIP event
-pairs, median of --reps.
+Times (ms): analysis (rsp_ilu0_analysis = csrilu02_analysis, the
+reference's timed "Symbolic", wall clock) and the two trsv analyses
+(rsp_trsv_analysis = csrsv2_analysis, untimed in the reference, wall clock),
+factor and solve (L then L^T, the reference's "Solve", GPU/ilu0.cu:284-310)
+as HIP event pairs, median of --reps.
 """
 from __future__ import annotations
 
@@ -36,9 +38,13 @@ def run_one(h, A, dt, ftz, reps):
     rp, ci, va0 = upload_csr(A.rowptr, A.colidx, A.values, dt)
     il = Ilu0(h, rp, ci)
     t0 = time.perf_counter()
-    il.analysis()
+    il.analysis()  # csrilu02_analysis: the reference's timed "Symbolic" (GPU/ilu0.cu:196-217)
     t_an = (time.perf_counter() - t0) * 1e3
     assert il.zero_pivot() == -1
+    t0 = time.perf_counter()
+    il.trsv_analysis()  # the two csrsv2_analysis (:228-252), untimed there
+    il.trsv_analysis(transpose=True)
+    t_tan = (time.perf_counter() - t0) * 1e3
     lev = il.levels()
     x = torch.ones(A.n, dtype=dt, device="cuda")
     tf, ts = [], []
@@ -79,7 +85,7 @@ def run_one(h, A, dt, ftz, reps):
     fbytes = 20 * nnz_s + 4 * (m + 1) + 4 * m
     sbytes = 2 * (12 * nnz_l + 4 * (m + 1) + 16 * m)
     fac, sol = statistics.median(tf), statistics.median(ts)
-    return {"analysis_ms": round(t_an, 3), "factor_ms": round(fac, 4),
+    return {"analysis_ms": round(t_an, 3), "trsv_analysis_ms": round(t_tan, 3), "factor_ms": round(fac, 4),
             "solve_ms": round(sol, 4), "levels_L": lev[0], "levels_LT": lev[1],
             "factor_gbps": round(fbytes / (fac * 1e6), 1), "solve_gbps": round(sbytes / (sol * 1e6), 1),
             "cpu_factor_ms": round(t_cf, 3), "cpu_solve_ms": round(t_cs, 3), "bitwise_ok": bool(ok)}
@@ -119,6 +125,8 @@ def main():
           f"fp32 factor {tot('factor_ms', 'fp32'):.2f} solve {tot('solve_ms', 'fp32'):.2f}; "
           f"fp32+ftz factor {tot('factor_ms', 'fp32_ftz'):.2f} solve {tot('solve_ms', 'fp32_ftz'):.2f}; "
           f"cpu(1 thread) factor {tot('cpu_factor_ms', 'fp64'):.1f} solve {tot('cpu_solve_ms', 'fp64'):.1f}")
+    print(f"ANALYSIS fp64 ilu (Symbolic) {tot('analysis_ms', 'fp64'):.1f} ms; trsv (untimed in the reference) "
+          f"{tot('trsv_analysis_ms', 'fp64'):.1f} ms")
     if args.json:
         json.dump(out, open(args.json, "w"), indent=1)
 

@@ -467,6 +467,20 @@ def test_flow_segments(handle, monkeypatch, flow, wpc, mode, name, scale):
     compare(A, torch.float32, handle, x=x, true_lu=True)
 
 
+@pytest.mark.parametrize("exp2", [0, 70, -70, 100])
+@pytest.mark.parametrize("name,scale", [("dc1", 0.05), ("xenon2", 0.1)])
+def test_ftz_division_any_exponent(handle, exp2, name, scale):
+    """FTZ build divisions (ilu0.hip qdiv): operands within [2^-60, 2^60] run
+    the float Newton sequence without the denormal-mode switch, others the
+    double quotient rounded once; with the matrix scaled by 2^exp2 both
+    branches meet the oracle's DAZ/FTZ bits (factor and solves, fp32)."""
+    import dataclasses
+    A = csr.surrogate(name, scale)
+    A = dataclasses.replace(A, values=A.values * (2.0 ** exp2))
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    compare(A, torch.float32, handle, ftz=True, x=x)
+
+
 @pytest.mark.parametrize("grid_x", [4, 16])
 @pytest.mark.parametrize("name,scale", [("xenon2", 0.3), ("offshore", 0.2), ("ss1", 0.2)])
 def test_flow_tickets_oversubscribed(handle, monkeypatch, grid_x, name, scale):
