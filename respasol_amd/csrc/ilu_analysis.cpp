@@ -1240,31 +1240,38 @@ static void split_terms(const int *rp, const int *ci, IluHostPlan &hp) {
     });
 }
 
-void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
+// The lower DAG's levels (factor + L solve): the longest path ending at each
+// row (each row needs its producers'). rsp_ilu0_analysis waits for these only.
+void plan_levels_lower(const int *rp, const int *ci, IluHostPlan &hp) {
+    const int n = hp.n;
+    const hvec<int> &dpos = hp.dpos;
+    const double t0 = now_ms();
+    hvec<int> &lv = hp.lev_l;
+    lv.assign((size_t)n, 0);
+    int nl = n > 0 ? 1 : 0;
+    for (int i = 0; i < n; i++) {
+        int l = 0;
+        for (int p = rp[i]; p < dpos[(size_t)i]; p++) l = std::max(l, lv[(size_t)ci[p]] + 1);
+        lv[(size_t)i] = l;
+        nl = std::max(nl, l + 1);
+    }
+    group_levels(lv, nl, hp.L.ptr, hp.L.rows);
+    if (env_int("RSP_ILU_TIMING", 0) >= 3)
+        fprintf(stderr, "rsp_ilu0_analysis n=%d     levels: L %.2f ms\n", n, now_ms() - t0);
+}
+
+// The solves-only half of the level analysis: the L^T DAG's levels and the
+// transposed strict lower part (two independent passes, run concurrently:
+// each is memory-latency bound), then the split term order. Round 6: started
+// by the solve plans' thread, so the analysis proper (the reference's
+// csrilu02_analysis) no longer waits for it. The split order reads the L
+// levels too: with split = false it is left to the caller (plan_levels).
+void plan_levels_upper(const int *rp, const int *ci, IluHostPlan &hp, bool split) {
     const int n = hp.n;
     hp.split = env_int("RSP_ILU_SPLIT", 0) != 0;
     const hvec<int> &dpos = hp.dpos;
-    // three independent sequential passes over the strict lower part, run
-    // concurrently (each is memory-latency bound; splitting one over threads
-    // measured slower on the box): the L levels, the transposed lower part,
-    // the L^T levels; each level set then grouped (counting sort).
-    // levels of the lower DAG (factor + L solve): the longest path ending at
-    // each row (each row needs its producers')
     const double t0 = now_ms();
-    double t_l = 0, t_lt = 0, t_tr = 0;  // diagnostics (RSP_ILU_TIMING >= 3): each pass's wall time
-    Task tl([&] {
-        hvec<int> &lv = hp.lev_l;
-        lv.assign((size_t)n, 0);
-        int nl = n > 0 ? 1 : 0;
-        for (int i = 0; i < n; i++) {
-            int l = 0;
-            for (int p = rp[i]; p < dpos[(size_t)i]; p++) l = std::max(l, lv[(size_t)ci[p]] + 1);
-            lv[(size_t)i] = l;
-            nl = std::max(nl, l + 1);
-        }
-        group_levels(lv, nl, hp.L.ptr, hp.L.rows);
-        t_l = now_ms() - t0;
-    });
+    double t_lt = 0, t_tr = 0;  // diagnostics (RSP_ILU_TIMING >= 3): each pass's wall time
     // levels of the L^T DAG: row i waits for every j > i with l_ji != 0
     Task tt([&] {
         hvec<int> &lvt = hp.lev_lt;
@@ -1335,13 +1342,20 @@ void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
         }
     });
     t_tr = now_ms() - t0;
-    tl.join();
     tt.join();
     const double t_j = now_ms() - t0;
-    split_terms(rp, ci, hp);
+    if (split) split_terms(rp, ci, hp);
     if (env_int("RSP_ILU_TIMING", 0) >= 3)
-        fprintf(stderr, "rsp_ilu0_analysis n=%d     levels: L %.2f LT %.2f transpose %.2f joined %.2f split %.2f ms\n",
-                n, t_l, t_lt, t_tr, t_j, now_ms() - t0 - t_j);
+        fprintf(stderr, "rsp_ilu0_analysis n=%d     levels: LT %.2f transpose %.2f joined %.2f split %.2f ms\n",
+                n, t_lt, t_tr, t_j, now_ms() - t0 - t_j);
+}
+
+void plan_levels(const int *rp, const int *ci, IluHostPlan &hp) {
+    hp.split = env_int("RSP_ILU_SPLIT", 0) != 0;
+    Task tl([&] { plan_levels_lower(rp, ci, hp); });
+    plan_levels_upper(rp, ci, hp, false);
+    tl.join();
+    split_terms(rp, ci, hp);
 }
 
 rsp_status_t plan_symbolic(const int *rpp, const int *cip, IluHostPlan &hp) {

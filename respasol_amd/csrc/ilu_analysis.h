@@ -184,7 +184,10 @@ rsp_status_t plan_validate(int n, const int *rp, const int *ci, IluHostPlan &hp)
 // The rows of the L DAG's levels the factor runs thin (needs the levels and
 // sym.upd_ptr): the only rows whose update pairs the factor plan reads.
 hvec<int> factor_thin_rows(const int *rp, const IluHostPlan &hp);
-void plan_levels(const int *rp, const int *ci, IluHostPlan &hp);
+void plan_levels(const int *rp, const int *ci, IluHostPlan &hp);        // both halves below
+void plan_levels_lower(const int *rp, const int *ci, IluHostPlan &hp);  // L levels (the factor's)
+void plan_levels_upper(const int *rp, const int *ci, IluHostPlan &hp,  // L^T levels, transposed lower,
+                       bool split = true);                             // split order (needs L levels)
 rsp_status_t plan_symbolic(const int *rp, const int *ci, IluHostPlan &hp);
 void plan_solves(const int *rp, const int *ci, IluHostPlan &hp);
 // ... their per-row half only (SolvePlan without tpos / src / trow / sid /

@@ -1539,7 +1539,8 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
         hp.structural_zero = szero.load() == INT_MAX ? -1 : szero.load();
     }
     sub("host check + dpos");
-    rsp_an::Task levels([&] { rsp_an::plan_levels(rp.data(), ci.data(), hp); });
+    // (the L levels: the factor's; L^T's are the solve plans' thread's first step)
+    rsp_an::Task levels([&] { rsp_an::plan_levels_lower(rp.data(), ci.data(), hp); });
     size_t scan_bytes = 0;
     RSP_CHECK_HIP(rsp_k::ilu_an_scan(nullptr, nullptr, nnz_s + 1, nullptr, &scan_bytes, s));
     Arena ar;
@@ -1727,6 +1728,7 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     rsp_an::IluHostPlan *H = hp.get();
     rsp_status_t st = ilu_symbolic_device(h, f, d_row_offsets, d_col_ind, rp, ci, *hp, ph, [&] {
         solves.reset(new rsp_an::Task([rpd, cid, H, n, dev_terms] {
+            rsp_an::plan_levels_upper(rpd, cid, *H);  // L^T levels, the transposed lower part
             // block-inverse plans of the deep DAGs, beside the row plans
             auto blk = [&](int kind) {
                 const rsp_an::DagHost &dg = kind == 0 ? H->L : H->LT;
@@ -1801,7 +1803,6 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
         ar.up(&f->L.d_rows, hp->L.rows);
         ar.up(&f->L.d_ptr, hp->L.ptr);
     }
-    f->LT.ptr = hp->LT.ptr;  // (level count, rsp_ilu0_levels)
     // flow runs: the saved upper input values of their rows (ilu0_flow_prep)
     if (!hp->fruns.empty()) ar.space(&f->d_forig, (size_t)std::max(hp->nnz_s, 1) * sizeof(double));
     ar.space((void **)&f->d_zero, 8 * sizeof(int));  // zero pivot, flow give-ups, claim counter
@@ -2088,6 +2089,10 @@ rsp_status_t rsp_ilu0_solve_blocks(rsp_ilu0_info_t f, int *blocks_lower, int *bl
 
 rsp_status_t rsp_ilu0_levels(rsp_ilu0_info_t f, int *levels_lower, int *levels_upper) {
     if (!f || !f->analysed) return RSP_STATUS_INVALID_VALUE;
+    if (levels_upper) {  // (the L^T levels come with the solve plans)
+        const rsp_status_t st = ilu_solves_ready(f->han, f);
+        if (st != RSP_STATUS_SUCCESS) return st;
+    }
     if (levels_lower) *levels_lower = (int)f->L.ptr.size() - 1;
     if (levels_upper) *levels_upper = (int)f->LT.ptr.size() - 1;
     return RSP_STATUS_SUCCESS;
