@@ -1886,7 +1886,12 @@ static rsp_status_t ilu_solves_ready(rsp_handle_t h, rsp_ilu0_info *f) {
     if (!f->analysed || !f->host || !h) return RSP_STATUS_INVALID_VALUE;
     if (f->solves_task) {
         std::unique_ptr<rsp_an::Task> t = std::move(f->solves_task);
-        t->join();  // rethrows the solve plans' exception (guarded: an error status)
+        try {
+            t->join();
+        } catch (...) {  // the plans are incomplete: the info needs a new analysis
+            f->analysed = 0;
+            throw;  // (guarded: an error status)
+        }
     }
     rsp_an::IluHostPlan *hp = f->host.get();
     const int n = f->n;

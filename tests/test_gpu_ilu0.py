@@ -293,6 +293,45 @@ def test_empty_matrix(handle):
     assert A.n == 0
 
 
+def test_trsv_analysis_lifecycle(handle):
+    """Round 6: rsp_ilu0_analysis leaves the solve plans running on a worker
+    thread; rsp_trsv_analysis joins them (either op, repeatable), the first
+    solve does it otherwise, and destroying or re-analysing the info while
+    they still run is safe. Bad arguments are INVALID_VALUE."""
+    from respasol_amd import _lib
+    from respasol_amd._lib import rsp
+    A = csr.surrogate("dc1", 0.3)
+    rp, ci, va = upload_csr(A.rowptr, A.colidx, A.values)
+    # destroyed with the plans still running (the destructor joins them)
+    for _ in range(3):
+        il = Ilu0(handle, rp, ci, nnz=A.nnz)
+        il.analysis()
+        del il
+    il = Ilu0(handle, rp, ci, nnz=A.nnz)
+    # not analysed yet / a bad op
+    assert rsp.rsp_trsv_analysis(handle.ptr, _lib.OP_N, il._info) == _lib.STATUS_INVALID_VALUE
+    il.analysis()
+    assert rsp.rsp_trsv_analysis(handle.ptr, 7, il._info) == _lib.STATUS_INVALID_VALUE
+    il.analysis()  # re-analysis while the first analysis' plans may still run
+    il.trsv_analysis(transpose=True)
+    il.trsv_analysis()  # (already done: returns at once)
+    x, _ = csr.dlarnv(2, [0, 0, 0, 1], A.n)
+    il.factor(va)
+    xx = torch.from_numpy(x).cuda()
+    z = il.solve_lower(va, xx)
+    y = il.solve_lower(va, z, transpose=True)
+    rv, _, _ = ob.ilu0(A.rowptr, A.colidx, A.values)
+    assert np.array_equal(va.cpu().numpy(), rv)
+    assert np.array_equal(z.cpu().numpy(), ob.trsv("lower_n", A.rowptr, A.colidx, rv, x))
+    assert np.array_equal(y.cpu().numpy(), ob.trsv("lower_t", A.rowptr, A.colidx, rv, z.cpu().numpy()))
+    # n = 0: both analyses succeed
+    z0 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    e = Ilu0(handle, z0, z0, nnz=0)
+    e.analysis()
+    e.trsv_analysis()
+    e.trsv_analysis(transpose=True)
+
+
 @pytest.mark.parametrize("thin_solve", [1024, 0])
 def test_fp32_fma_single_rounding(handle, monkeypatch, thin_solve):
     """fp32 solves fuse in fp32 (one rounding, fmaf), not in double: for
