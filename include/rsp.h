@@ -177,9 +177,11 @@ rsp_status_t rsp_trsv_analysis(rsp_handle_t handle, rsp_operation_t op, rsp_ilu0
  * factorisation); the smallest such j is reported. Otherwise SUCCESS, -1. */
 rsp_status_t rsp_ilu0_zero_pivot(rsp_handle_t handle, rsp_ilu0_info_t info, int *position);
 /* Flow launches (one launch over a run of fat levels) take their work items by
- * start tickets (the default since round 6): a workgroup waits only on items
- * of workgroups that started before it, so progress never depends on other
- * kernels leaving CUs free and no wait gives up in normal operation. The
+ * start tickets (the default since round 6): a workgroup owns the items of the
+ * ticket it claimed when it started, and a workgroup that has waited long
+ * while some tickets are still unclaimed (their workgroups have not started:
+ * another kernel holds the CUs) claims those too, so progress never depends on
+ * other kernels leaving CUs free and no wait gives up in normal operation. The
  * bounded wait (RSP_ILU_FLOW_TIMEOUT_US, default 0.2 s) stays as a backstop,
  * and it is what the older static item walk (RSP_ILU_FLOW_MODE=0) needs: a
  * factor whose flow wait gave up is RECOVERED here — its input values (kept
