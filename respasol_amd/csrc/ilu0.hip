@@ -1137,6 +1137,9 @@ __global__ __launch_bounds__(256) void ilu0_scale_lower(IluArgs a) {
 // in flight. Rounds of <= 64 items run on wave 0 alone, consecutive narrow
 // rounds without workgroup barriers (in-order LDS of one wave); wider rounds
 // use every thread and an LDS-only barrier.
+#ifndef RSP_FAC_PRE3
+#define RSP_FAC_PRE3 1
+#endif
 template <typename T>
 __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, int c1) {
     constexpr int NTH = kThinThreads, K = rsp::kRndItems, S = rsp::kRndStaged;
@@ -1372,8 +1375,18 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 const int b0 = lrnd[s0], n0 = lrnd[s0 + 1] - b0;
                 const bool has1 = s0 + 1 < s1;
                 const int b1 = has1 ? lrnd[s0 + 1] : b0, n1 = has1 ? lrnd[s0 + 2] - b1 : 0;
+#if RSP_FAC_PRE3
+                // (a third round's records too: levels of three rounds are
+                // common on the deep circuits, dc1 2.7 rounds per level)
+                const bool has2 = s0 + 2 < s1;
+                const int b2 = has2 ? lrnd[s0 + 2] : b0, n2 = has2 ? lrnd[s0 + 3] - b2 : 0;
+#endif
                 const ItemPre p0 = item_pre(b0 + min(lane, n0 - 1), cb);
                 const ItemPre p1 = item_pre(b1 + min(lane, max(n1 - 1, 0)), cb);
+#if RSP_FAC_PRE3
+                const ItemPre p2 = item_pre(b2 + min(lane, max(n2 - 1, 0)), cb);
+                const bool sh2 = !__ballot(lane < n2 && (p2.r.y >> 16) > 2);
+#endif
                 const bool sh0 = !__ballot(lane < n0 && (p0.r.y >> 16) > 2);
                 const bool sh1 = !__ballot(lane < n1 && (p1.r.y >> 16) > 2);
                 if (s0 > q) lds_wait_geq(&lds_rdone, ch.r0 + s0, ch.r0 + sp);
@@ -1382,7 +1395,15 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 if (has1) {
                     if (lane < n1) item_post(b1 + lane, cb, p1, sh1);
                     wave_order();
+#if RSP_FAC_PRE3
+                    if (has2) {
+                        if (lane < n2) item_post(b2 + lane, cb, p2, sh2);
+                        wave_order();
+                    }
+                    for (int qq = s0 + 3; qq < s1; ++qq) {  // levels of more than three rounds
+#else
                     for (int qq = s0 + 2; qq < s1; ++qq) {  // levels of more than two rounds
+#endif
                         const int bq = lrnd[qq];
                         if (bq + lane < lrnd[qq + 1]) process(bq + lane, cb, std::false_type());
                         wave_order();

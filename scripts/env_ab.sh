@@ -13,7 +13,7 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
         name=${spec%%:*}; envs=${spec#*:}
         env $envs timeout -k 10 300 python scripts/bench_ilu0.py --set "$SET" --fp64-only --reps 5 \
             > "$O/${name}_$r.txt" 2> "$O/${name}_$r.err" || { tail -20 "$O/${name}_$r.err"; exit 1; }
-        echo "$name round $r: $(tail -1 "$O/${name}_$r.txt" | cut -c1-60)"
+        echo "$name round $r: $(grep TOTAL "$O/${name}_$r.txt" | cut -c1-60)"
         cut -c1-16,50-68 "$O/${name}_$r.txt" | sed -n '2,$p' | grep -v "^median\|^TOTAL"
     done
 done
