@@ -1140,6 +1140,9 @@ __global__ __launch_bounds__(256) void ilu0_scale_lower(IluArgs a) {
 #ifndef RSP_FAC_PRE3
 #define RSP_FAC_PRE3 1
 #endif
+#ifndef RSP_FAC_PRE3C
+#define RSP_FAC_PRE3C 1
+#endif
 template <typename T>
 __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, int c1) {
     constexpr int NTH = kThinThreads, K = rsp::kRndItems, S = rsp::kRndStaged;
@@ -1384,7 +1387,12 @@ __global__ __launch_bounds__(kThinThreads) void ilu0_rounds(IluArgs a, int c0, i
                 const ItemPre p0 = item_pre(b0 + min(lane, n0 - 1), cb);
                 const ItemPre p1 = item_pre(b1 + min(lane, max(n1 - 1, 0)), cb);
 #if RSP_FAC_PRE3
+#if RSP_FAC_PRE3C
+                ItemPre p2{};
+                if (has2) p2 = item_pre(b2 + min(lane, max(n2 - 1, 0)), cb);  // (wave-uniform: levels of >= 3 rounds)
+#else
                 const ItemPre p2 = item_pre(b2 + min(lane, max(n2 - 1, 0)), cb);
+#endif
                 const bool sh2 = !__ballot(lane < n2 && (p2.r.y >> 16) > 2);
 #endif
                 const bool sh0 = !__ballot(lane < n0 && (p0.r.y >> 16) > 2);
