@@ -546,11 +546,7 @@ struct FlowClaims {
                 for (int q = 0; q < rsp::kFlowTicketCtrs; ++q)
                     __hip_atomic_store(fc.tickets + rsp::kFlowTicketCtrs * (int)((base + 1) & 1) + q, 0u,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef RSP_TK_BLOCKIDX
-            const int t = blockIdx.x;
-#else
             const int t = take(blockIdx.x % rsp::kFlowTicketCtrs);
-#endif
             L->own[0] = t;
             L->state = t < (int)gridDim.x ? 1 : 0;
             L->lock = 0;
@@ -652,9 +648,6 @@ struct FlowClaims {
     // times per wave, so no item escapes the bound by yielding.
     __device__ unsigned long long deadline(unsigned long long t0) const {
         if constexpr (!TK) return t0 + fc.ticks;
-#ifdef RSP_TK_NOSTEAL
-        return t0 + fc.ticks;
-#endif
         return t0 + min(fc.ticks, steal_at);
     }
     // a wait past its deadline: 0 give up, 1 yield, 2 wait on until the new
