@@ -42,28 +42,19 @@ __device__ __forceinline__ int lower_bound_dev(const int *__restrict__ ci, int l
     return lo;
 }
 
-// Validation + diagonal positions + structural zero, one thread per row.
-// flags[0] |= 1 for a column out of range or a row not strictly increasing;
-// flags[1] = min row without a diagonal (INT_MAX = none).
+// Diagonal positions + structural zero, one thread per row (binary search:
+// O(log len) even on a circuit's hub rows). The pattern was validated on the
+// host before this launch (columns in range, rows strictly increasing:
+// rsp_api.cpp ilu_symbolic_device returns INVALID_VALUE first), so flags[0]
+// is never set here (round 6: the per-row validation loop held one thread
+// for a hub row's whole length, ~1 ms on ASIC_320ks); flags[1] = min row
+// without a diagonal (INT_MAX = none).
 __global__ __launch_bounds__(kAnThreads) void an_rows(int n, const int *__restrict__ rp,
                                                        const int *__restrict__ ci, int *__restrict__ dpos,
                                                        int *__restrict__ hasdiag, int *__restrict__ flags) {
     const int i = blockIdx.x * kAnThreads + threadIdx.x;
     if (i >= n) return;
     const int rs = rp[i], re = rp[i + 1];
-    bool bad = false;
-    int prev = -1;
-    for (int p = rs; p < re; p++) {
-        const int c = ci[p];
-        bad |= c < 0 || c >= n || c <= prev;
-        prev = c;
-    }
-    if (bad) {
-        atomicOr(flags, 1);
-        dpos[i] = rs;
-        hasdiag[i] = 0;
-        return;
-    }
     const int d = lower_bound_dev(ci, rs, re, i);
     const int hd = (d < re && ci[d] == i) ? 1 : 0;
     dpos[i] = d;
@@ -127,6 +118,85 @@ __global__ __launch_bounds__(64) void an_pairs(const int *__restrict__ rows, con
         for (int t = rs + lane; t < re; t += 64) cnt_or_ptr[t] = cur[t];
 }
 
+// The same lists for the rows of <= `cap` entries, with row i's columns
+// staged in LDS beside its counters (dynamic LDS: 2 cap ints): the search for
+// each column of row k in row i is an LDS binary search instead of a chain of
+// global loads, row i's lower positions' k, row k's upper range are gathered
+// 64 at a time (one lane each, then read lane by lane), and the column load of
+// the next step is issued before the current step's search (round 6: the
+// circuits' rows of hundreds of lower positions, several of them into hub
+// rows, held a wave ~1 ms per pass). Same traversal, same order: the (p, q)
+// steps run in ascending p, then q, as an_pairs.
+template <bool FILL>
+__global__ __launch_bounds__(64) void an_pairs_lds(const int *__restrict__ rows, int cap, const int *__restrict__ rp,
+                                                   const int *__restrict__ ci, const int *__restrict__ dpos,
+                                                   const int *__restrict__ hasdiag, int *__restrict__ cnt_or_ptr,
+                                                   int *__restrict__ upd_l, int *__restrict__ upd_u) {
+    extern __shared__ int an_lds[];
+    int *cur = an_lds, *cols = an_lds + cap;  // indexed by position - rs
+    const int lane = threadIdx.x;
+    const int i = rows[blockIdx.x];
+    const int rs = rp[i], re = rp[i + 1], di = dpos[i], len = re - rs;
+    for (int t = lane; t < len; t += 64) {
+        cur[t] = FILL ? cnt_or_ptr[rs + t] : 0;
+        cols[t] = ci[rs + t];
+    }
+    __syncthreads();
+    for (int pb = rs; pb < di; pb += 64) {
+        const int np = min(64, di - pb);
+        int qs = 0, qe = 0;  // lane j: row k = ci[pb + j]'s upper range
+        if (lane < np) {
+            const int k = cols[pb + lane - rs];
+            qs = dpos[k] + hasdiag[k];
+            qe = rp[k + 1];
+        }
+        int j = 0, qb = 0, qend = 0;
+        for (; j < np; j++) {
+            qb = __builtin_amdgcn_readlane(qs, j);
+            qend = __builtin_amdgcn_readlane(qe, j);
+            if (qb < qend) break;
+        }
+        int col = (j < np && qb + lane < qend) ? ci[qb + lane] : -1;
+        while (j < np) {
+            // the next step (j2, qb2), its column load in flight under this step's search
+            int j2 = j, qb2 = qb + 64, qe2 = qend;
+            if (qb2 >= qe2)
+                for (j2 = j + 1; j2 < np; j2++) {
+                    qb2 = __builtin_amdgcn_readlane(qs, j2);
+                    qe2 = __builtin_amdgcn_readlane(qe, j2);
+                    if (qb2 < qe2) break;
+                }
+            const int coln = (j2 < np && qb2 + lane < qe2) ? ci[qb2 + lane] : -1;
+            if (col >= 0) {
+                const int p = pb + j;
+                int lo = p + 1 - rs, hi = len;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (cols[mid] < col)
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                if (lo < len && cols[lo] == col) {
+                    const int m = cur[lo];
+                    cur[lo] = m + 1;
+                    if (FILL) {
+                        upd_l[m] = p;
+                        upd_u[m] = qb + lane;
+                    }
+                }
+            }
+            j = j2;
+            qb = qb2;
+            qend = qe2;
+            col = coln;
+        }
+    }
+    __syncthreads();
+    if (!FILL)
+        for (int t = lane; t < len; t += 64) cnt_or_ptr[rs + t] = cur[t];
+}
+
 // Per row (one thread): intra-row stages of the lower positions (stage(t) =
 // 1 + max stage of the l_ik its pairs read, 0 without pairs; positions in
 // ascending order, so every read stage is final), the stable order of the
@@ -177,6 +247,112 @@ __global__ __launch_bounds__(kAnThreads) void an_stages(int n, int maxlen, const
     }
 }
 
+// an_stages for one row per wave (the rows of (thread-kernel maxlen, 1024]
+// entries, listed in `rows`): the same stage, udiv, lord, lend. Stages in
+// LDS; a lower position's pairs read by the lanes (the next position's pair
+// loads issued before this one's max-reduce: upd_l does not depend on the
+// stages); the stable counting sort by stage as a wave: LDS histogram, scan,
+// then positions placed 64 at a time in position order, each lane counting
+// the lanes before it of its own stage (round 6: one thread per such row
+// walked its pairs and sort through dependent global loads, ~0.6-1 ms per
+// pass on the circuits).
+__global__ __launch_bounds__(64) void an_stages_wave(const int *__restrict__ rows, const int *__restrict__ rp,
+                                                      const int *__restrict__ ci, const int *__restrict__ dpos,
+                                                      const int *__restrict__ hasdiag,
+                                                      const int *__restrict__ ptr,
+                                                      const int *__restrict__ upd_l, int *__restrict__ stage,
+                                                      int *__restrict__ lord, int *__restrict__ lend,
+                                                      int *__restrict__ udiv) {
+    __shared__ int st[1024], base[1024], pl[1024];
+    const int lane = threadIdx.x;
+    const int i = rows[blockIdx.x];
+    const int rs = rp[i], di = dpos[i], re = rp[i + 1], nl = di - rs;
+    for (int t = di + lane; t < re; t += 64) {
+        stage[t] = 0;
+        udiv[t] = -1;
+        lord[t] = 0;
+        lend[t] = 0;
+    }
+    for (int x = lane; x < nl; x += 64) {
+        const int k = ci[rs + x];
+        udiv[rs + x] = hasdiag[k] ? dpos[k] : -1;
+        base[x] = 0;
+    }
+    if (nl == 0) return;
+    // stages, position by position; u ranges read 63 positions at a time
+    // (lane x: the start of position xb + x's pairs, lane nx: the last end)
+    int smax = 0;
+    for (int xb = 0; xb < nl; xb += 63) {
+        const int nx = min(63, nl - xb);
+        const int u0l = lane <= nx ? ptr[rs + xb + lane] : 0;
+        int u0 = __builtin_amdgcn_readlane(u0l, 0);
+        int u1 = __builtin_amdgcn_readlane(u0l, 1);
+        int v = u0 + lane < u1 ? upd_l[u0 + lane] : -1;
+        for (int x = 0; x < nx; x++) {
+            int s = 0;
+            for (int u = u0;;) {
+                const int un = u + 64;
+                // the next load: this position's next 64 pairs, else the next position's first
+                int vn = -1, u0n = u0, u1n = u1;
+                if (un < u1) {
+                    vn = un + lane < u1 ? upd_l[un + lane] : -1;
+                } else if (x + 1 < nx) {
+                    u0n = u1;
+                    u1n = __builtin_amdgcn_readlane(u0l, x + 2);
+                    vn = u0n + lane < u1n ? upd_l[u0n + lane] : -1;
+                }
+                if (v >= 0) s = max(s, st[v - rs] + 1);
+                v = vn;
+                if (un >= u1) {
+                    u0 = u0n;
+                    u1 = u1n;
+                    break;
+                }
+                u = un;
+            }
+            // wave max (every lane ends with the row's value)
+            for (int o = 32; o > 0; o >>= 1) s = max(s, __shfl_xor(s, o));
+            st[xb + x] = s;  // every lane writes the same value, and reads only its own writes
+            stage[rs + xb + x] = s;
+            smax = max(smax, s);
+        }
+    }
+    // histogram of the stages (< nl), exclusive scan into base
+    __syncthreads();
+    for (int x = lane; x < nl; x += 64) atomicAdd(&base[st[x]], 1);
+    __syncthreads();
+    int carry = 0;
+    for (int sb = 0; sb <= smax; sb += 64) {
+        const int sx = sb + lane;
+        const int c = sx <= smax ? base[sx] : 0;
+        int incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (sx <= smax) base[sx] = carry + incl - c;
+        carry += __builtin_amdgcn_readlane(incl, 63);
+    }
+    __syncthreads();
+    // stable placement, 64 positions at a time in position order
+    for (int xb = 0; xb < nl; xb += 64) {
+        const int x = xb + lane;
+        const int s = x < nl ? st[x] : -1;
+        int before = 0;
+        for (int l = 0; l < 64; l++) before += (l < lane && __builtin_amdgcn_readlane(s, l) == s) ? 1 : 0;
+        if (s >= 0) {
+            const int pos = base[s] + before;
+            pl[x] = pos;
+            lord[rs + pos] = rs + x;
+        }
+        __syncthreads();
+        if (s >= 0) atomicAdd(&base[s], 1);
+        __syncthreads();
+    }
+    // base[s] is now the end of stage s's group
+    for (int x = lane; x < nl; x += 64) lend[rs + pl[x]] = rs + base[st[x]];
+}
+
 inline unsigned grid_of(long long count) { return (unsigned)((count + kAnThreads - 1) / kAnThreads); }
 
 }  // namespace
@@ -197,11 +373,12 @@ hipError_t ilu_an_rows(int n, const int *rp, const int *ci, int *dpos, int *hasd
 // wave), <= 16384 (64 KB), longer (global cursors). rows_c*: the rows of each
 // class (device), counts n_c*.
 template <bool FILL>
-static hipError_t an_pairs_launch(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+static hipError_t an_pairs_launch(const int *const rows_c[3], const int n_c[3], int cap0, const int *rp, const int *ci,
                                   const int *dpos, const int *hasdiag, int *cnt_or_ptr, int *gcur, int *upd_l,
                                   int *upd_u, hipStream_t s) {
     if (n_c[0] > 0)
-        an_pairs<FILL, 1024><<<n_c[0], 64, 0, s>>>(rows_c[0], rp, ci, dpos, hasdiag, cnt_or_ptr, gcur, upd_l, upd_u);
+        an_pairs_lds<FILL><<<n_c[0], 64, 2 * cap0 * sizeof(int), s>>>(rows_c[0], cap0, rp, ci, dpos, hasdiag,
+                                                                    cnt_or_ptr, upd_l, upd_u);
     if (n_c[1] > 0)
         an_pairs<FILL, 16384><<<n_c[1], 64, 0, s>>>(rows_c[1], rp, ci, dpos, hasdiag, cnt_or_ptr, gcur, upd_l, upd_u);
     if (n_c[2] > 0)
@@ -209,9 +386,9 @@ static hipError_t an_pairs_launch(const int *const rows_c[3], const int n_c[3], 
     return hipGetLastError();
 }
 
-hipError_t ilu_an_count(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+hipError_t ilu_an_count(const int *const rows_c[3], const int n_c[3], int cap0, const int *rp, const int *ci,
                         const int *dpos, const int *hasdiag, int *cnt, int *gcur, hipStream_t s) {
-    return an_pairs_launch<false>(rows_c, n_c, rp, ci, dpos, hasdiag, cnt, gcur, nullptr, nullptr, s);
+    return an_pairs_launch<false>(rows_c, n_c, cap0, rp, ci, dpos, hasdiag, cnt, gcur, nullptr, nullptr, s);
 }
 
 // Exclusive prefix sum of `count` ints (cnt -> ptr) in three passes: block
@@ -300,19 +477,21 @@ hipError_t ilu_an_scan(const int *cnt, int *ptr, int count, void *temp, size_t *
     return hipGetLastError();
 }
 
-hipError_t ilu_an_fill(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+hipError_t ilu_an_fill(const int *const rows_c[3], const int n_c[3], int cap0, const int *rp, const int *ci,
                        const int *dpos, const int *hasdiag, const int *ptr, int *gcur, int *upd_l, int *upd_u,
                        hipStream_t s) {
-    return an_pairs_launch<true>(rows_c, n_c, rp, ci, dpos, hasdiag, const_cast<int *>(ptr), gcur, upd_l, upd_u,
+    return an_pairs_launch<true>(rows_c, n_c, cap0, rp, ci, dpos, hasdiag, const_cast<int *>(ptr), gcur, upd_l, upd_u,
                                  s);
 }
 
 hipError_t ilu_an_stages(int n, int maxlen, const int *rp, const int *ci, const int *dpos, const int *hasdiag,
                          const int *ptr, const int *upd_l, int *stage, int *lord, int *lend, int *udiv,
-                         int *scratch, hipStream_t s) {
+                         int *scratch, const int *wrows, int nwrows, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     an_stages<<<grid_of(n), kAnThreads, 0, s>>>(n, maxlen, rp, ci, dpos, hasdiag, ptr, upd_l, stage, lord, lend,
                                                 udiv, scratch);
+    if (nwrows > 0)
+        an_stages_wave<<<nwrows, 64, 0, s>>>(wrows, rp, ci, dpos, hasdiag, ptr, upd_l, stage, lord, lend, udiv);
     return hipGetLastError();
 }
 

@@ -1471,6 +1471,9 @@ static long long slot_cap_ints() {
 // host (rsp_an::symbolic_rows) and their ranges uploaded. Fills hp (levels
 // included).
 static constexpr int kAnDevRow = 1024;
+// device rows longer than this get one wave each for their stages (the
+// thread-per-row kernel takes the rest; RSP_AN_WAVE_ROW overrides, A/B)
+static constexpr int kAnWaveRow = 128;
 static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const int *d_rp, const int *d_ci,
                                         const rsp_an::hvec<int> &rp, rsp_an::hvec<int> &ci, rsp_an::IluHostPlan &hp,
                                         rsp_an::Phases &ph, const std::function<void()> &after_levels) {
@@ -1485,9 +1488,18 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
                 std::chrono::duration<double, std::milli>(t - t_last).count());
         t_last = t;
     };
-    rsp_an::hvec<int> dev_rows, long_rows;
-    for (int i = 0; i < n; i++)
-        if (rp[(size_t)i + 1] - rp[(size_t)i] > kAnDevRow) long_rows.push_back(i);
+    rsp_an::hvec<int> dev_rows, long_rows, wave_rows;
+    const int wave_row = (int)env_int("RSP_AN_WAVE_ROW", kAnWaveRow);
+    int cap0 = 1;  // the longest device row: the pair kernel's LDS per row
+    for (int i = 0; i < n; i++) {
+        const int len = rp[(size_t)i + 1] - rp[(size_t)i];
+        if (len > kAnDevRow) {
+            long_rows.push_back(i);
+        } else {
+            cap0 = std::max(cap0, len);
+            if (len > wave_row) wave_rows.push_back(i);
+        }
+    }
     dev_rows.resize((size_t)(n - (int)long_rows.size()));
     if (long_rows.empty()) {  // every row (FEM / stencil patterns): 0 .. n-1 in parallel
         rsp_an::parallel_for(n, 1 << 16, [&](long long a, long long b) {
@@ -1558,6 +1570,8 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     ar.space((void **)&d_scratch, (size_t)std::max(nnz_s, 1) * 4);
     ar.space(&d_scan, std::max<size_t>(scan_bytes, 16));
     ar.up(&d_rows, dev_rows);
+    int *d_wrows = nullptr;
+    ar.up(&d_wrows, wave_rows);
     sub("arena");
     RSP_CHECK_HIP(ar.commit(&f->d_arena_sym, s));
     // the device's diagonal positions and flags (its validation flags are not
@@ -1565,7 +1579,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     RSP_CHECK_HIP(rsp_k::ilu_an_rows(n, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_flags, s));
     const int n_c[3] = {(int)dev_rows.size(), 0, 0};
     const int *rows_c[3] = {d_rows, nullptr, nullptr};
-    RSP_CHECK_HIP(rsp_k::ilu_an_count(rows_c, n_c, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_cnt, d_scratch, s));
+    RSP_CHECK_HIP(rsp_k::ilu_an_count(rows_c, n_c, cap0, d_rp, d_ci, f->d_dpos, f->d_hasdiag, d_cnt, d_scratch, s));
     sub("rows + count kernels");
     // the long rows' counts on the host
     rsp_an::hvec<int> hcnt(long_rows.empty() ? 0 : (size_t)nnz_s);
@@ -1591,10 +1605,11 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     ap.space((void **)&f->d_upd_u, (size_t)std::max(total, 1) * 4);
     RSP_CHECK_HIP(ap.commit(&f->d_arena_pairs, s));
     sub("pairs arena");
-    RSP_CHECK_HIP(rsp_k::ilu_an_fill(rows_c, n_c, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, d_scratch,
+    RSP_CHECK_HIP(rsp_k::ilu_an_fill(rows_c, n_c, cap0, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, d_scratch,
                                      f->d_upd_l, f->d_upd_u, s));
-    RSP_CHECK_HIP(rsp_k::ilu_an_stages(n, kAnDevRow, d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, f->d_upd_l,
-                                       d_stage, f->d_lord, f->d_lend, f->d_udiv, d_scratch, s));
+    RSP_CHECK_HIP(rsp_k::ilu_an_stages(n, std::min(wave_row, kAnDevRow), d_rp, d_ci, f->d_dpos, f->d_hasdiag, f->d_upd_ptr, f->d_upd_l,
+                                       d_stage, f->d_lord, f->d_lend, f->d_udiv, d_scratch, d_wrows,
+                                       (int)wave_rows.size(), s));
     // the level sets (host thread, started above) while the device fills the update lists
     levels.join();
     ph.mark("levels");

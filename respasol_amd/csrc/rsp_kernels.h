@@ -527,25 +527,26 @@ hipError_t trsv_blocks_f64(const rsp::BlkArgs &a, hipStream_t s);
 // desc[t] = {level-order slot x, rm, qm, 0}, offs[t] = its slot's offset.
 hipError_t ilu0_build_slots(const rsp::IluArgs &a, const int4 *desc, const long long *offs, int nrows,
                             int *slots, hipStream_t s);
-// ILU(0) analysis on the device (ilu_analysis.hip): validation + diagonal
-// positions + structural zero (flags[0] |= 1 if malformed, flags[1] = atomicMin
+// ILU(0) analysis on the device (ilu_analysis.hip): diagonal positions +
+// structural zero of a pattern the host has validated (flags[1] = atomicMin
 // of the rows without a diagonal); the symbolic factor's update lists (count,
 // exclusive scan, fill; rows_c / n_c: the rows of each length class, see
-// ilu_analysis.hip), then stages, stage order (lord / lend) and divisor
-// positions (udiv; scratch: one int per position) of the rows of <= maxlen
-// entries.
+// ilu_analysis.hip; cap0 >= the longest row of class 0, <= 1024), then
+// stages, stage order (lord / lend) and divisor positions (udiv; scratch: one
+// int per position) of the rows of <= maxlen entries, one thread each, and of
+// the nwrows rows listed in wrows (maxlen < length <= 1024), one wave each.
 hipError_t ilu_an_rows(int n, const int *rp, const int *ci, int *dpos, int *hasdiag, int *flags, hipStream_t s);
-hipError_t ilu_an_count(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+hipError_t ilu_an_count(const int *const rows_c[3], const int n_c[3], int cap0, const int *rp, const int *ci,
                         const int *dpos, const int *hasdiag, int *cnt, int *gcur, hipStream_t s);
 hipError_t ilu_an_scan(const int *cnt, int *ptr, int count, void *temp, size_t *temp_bytes, hipStream_t s);
 hipError_t ilu_an_gather_pairs(const int *rows, int nrows, const int *rp, const int *ptr, const int *cbase,
                                const int *upd_l, const int *upd_u, int *out_l, int *out_u, hipStream_t s);
-hipError_t ilu_an_fill(const int *const rows_c[3], const int n_c[3], const int *rp, const int *ci,
+hipError_t ilu_an_fill(const int *const rows_c[3], const int n_c[3], int cap0, const int *rp, const int *ci,
                        const int *dpos, const int *hasdiag, const int *ptr, int *gcur, int *upd_l, int *upd_u,
                        hipStream_t s);
 hipError_t ilu_an_stages(int n, int maxlen, const int *rp, const int *ci, const int *dpos, const int *hasdiag,
                          const int *ptr, const int *upd_l, int *stage, int *lord, int *lend, int *udiv,
-                         int *scratch, hipStream_t s);
+                         int *scratch, const int *wrows, int nwrows, hipStream_t s);
 // The per-term half of a solve plan (ilu_analysis.cpp solve_plan_terms, same
 // arrays bit for bit) from its per-row half already on the device: flat term
 // positions and y sources, the thin runs' window remap, row records, y

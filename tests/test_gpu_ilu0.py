@@ -418,7 +418,32 @@ def test_device_analysis_same_plan_as_host(handle, monkeypatch, name, scale):
     il.close()
 
 
-@pytest.mark.parametrize("knobs", [{"RSP_ILU_THIN_SOLVE": "0"}, {"RSP_ILU_THIN_SOLVE": "1"},
+@pytest.mark.parametrize("wave_row", ["0", "8"])
+@pytest.mark.parametrize("name,scale", [("dc1", 0.5), ("stomach", 0.05), ("crashbasis", 0.2), ("G2_circuit", 0.2)])
+def test_device_analysis_wave_stages(handle, monkeypatch, wave_row, name, scale):
+    """The one-wave-per-row stages kernel (an_stages_wave: stages, stable
+    stage order, group ends, divisors) forced onto every row longer than
+    RSP_AN_WAVE_ROW entries: the plan digest equals the host analysis'."""
+    import ctypes as C
+    from respasol_amd._lib import rsp
+    monkeypatch.setenv("RSP_ILU_DIGEST", "1")
+    monkeypatch.setenv("RSP_AN_WAVE_ROW", wave_row)
+    A = csr.surrogate(name, scale)
+    rp, ci, _ = upload_csr(A.rowptr, A.colidx, A.values)
+    il = Ilu0(handle, rp, ci)
+    il.analysis()
+    dev = C.c_uint64()
+    assert rsp.rsp_ilu0_plan_digest(il._info, C.byref(dev)) == 0
+    lo, up, hst = C.c_int(), C.c_int(), C.c_uint64()
+    r = np.ascontiguousarray(A.rowptr, np.int32)
+    c = np.ascontiguousarray(A.colidx, np.int32)
+    assert rsp.rsp_ilu0_analysis_host(A.n, r.ctypes.data, c.ctypes.data, C.byref(lo), C.byref(up),
+                                      C.byref(hst), None) == 0
+    assert dev.value == hst.value
+    il.close()
+
+
+@pytest.mark.parametrize("knobs",[{"RSP_ILU_THIN_SOLVE": "0"}, {"RSP_ILU_THIN_SOLVE": "1"},
                                    {"RSP_ILU_GROUP": "2"}, {"RSP_ILU_FAT_PAD": "0"},
                                    {"RSP_ILU_THIN_TERMS": "64"}, {"RSP_ILU_FAT_LONG": "8"}])
 @pytest.mark.parametrize("name,scale", [("dc1", 0.3), ("stomach", 0.05), ("ecology2", 0.05)])
