@@ -25,6 +25,7 @@
 #include <stddef.h>
 
 #include <new>
+#include <type_traits>
 #include <vector>
 
 namespace rsp_an {
@@ -39,6 +40,23 @@ struct PoolAlloc {
     PoolAlloc() noexcept = default;
     template <typename U>
     PoolAlloc(const PoolAlloc<U> &) noexcept {}
+    // elements added by resize() / a size constructor are value-initialised
+    // (zeroed), unless resize_uninit (below) is on the stack of this thread
+    template <typename U, typename... A>
+    void construct(U *p, A &&...a) {
+        ::new ((void *)p) U(static_cast<A &&>(a)...);
+    }
+    template <typename U>
+    void construct(U *p) {
+        if (uninit_scope())
+            ::new ((void *)p) U;
+        else
+            ::new ((void *)p) U();
+    }
+    static bool &uninit_scope() {
+        static thread_local bool on = false;
+        return on;
+    }
     T *allocate(size_t n) {
         const size_t b = n * sizeof(T);
         if (b >= kPoolMin) return static_cast<T *>(pool_get(b));
@@ -60,6 +78,24 @@ struct PoolAlloc {
 // the analysis' vectors
 template <typename T>
 using hvec = std::vector<T, PoolAlloc<T>>;
+
+// v.resize(n) without zeroing the new elements (trivial T only): for arrays
+// that a transfer or a loop overwrites whole right after (round 6: zeroing
+// the downloaded pattern, update pointers and stages cost ~3 x 4 B per
+// stored entry of serial memset per analysis)
+template <typename T>
+void resize_uninit(hvec<T> &v, size_t n) {
+    static_assert(std::is_trivially_default_constructible<T>::value, "trivial types only");
+    bool &on = PoolAlloc<T>::uninit_scope();
+    on = true;
+    try {
+        v.resize(n);
+    } catch (...) {
+        on = false;
+        throw;
+    }
+    on = false;
+}
 
 }  // namespace rsp_an
 

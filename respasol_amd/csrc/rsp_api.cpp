@@ -1500,7 +1500,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
             if (len > wave_row) wave_rows.push_back(i);
         }
     }
-    dev_rows.resize((size_t)(n - (int)long_rows.size()));
+    rsp_an::resize_uninit(dev_rows, (size_t)(n - (int)long_rows.size()));
     if (long_rows.empty()) {  // every row (FEM / stencil patterns): 0 .. n-1 in parallel
         rsp_an::parallel_for(n, 1 << 16, [&](long long a, long long b) {
             for (long long i = a; i < b; i++) dev_rows[(size_t)i] = (int)i;
@@ -1526,8 +1526,8 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
         // kernel below computes the same arrays for the device, so nothing of
         // it is read back — round 5: two synchronisations fewer per analysis)
         std::atomic<int> bad{0}, szero{INT_MAX};
-        hp.dpos.resize((size_t)n);
-        hp.hasdiag.resize((size_t)n);
+        rsp_an::resize_uninit(hp.dpos, (size_t)n);
+        rsp_an::resize_uninit(hp.hasdiag, (size_t)n);
         rsp_an::parallel_for(n, 1 << 14, [&](long long r0, long long r1) {
             int sz = INT_MAX;
             for (long long i = r0; i < r1; i++) {
@@ -1591,7 +1591,7 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     sub("long-row counts");
     RSP_CHECK_HIP(hipMemsetAsync(d_cnt + nnz_s, 0, 4, s));
     RSP_CHECK_HIP(rsp_k::ilu_an_scan(d_cnt, f->d_upd_ptr, nnz_s + 1, d_scan, &scan_bytes, s));
-    hp.sym.upd_ptr.resize((size_t)nnz_s + 1);
+    rsp_an::resize_uninit(hp.sym.upd_ptr, (size_t)nnz_s + 1);
     RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_ptr.data(), f->d_upd_ptr, ((size_t)nnz_s + 1) * 4,
                                  hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
@@ -1620,8 +1620,10 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
     // rows (their lists are uploaded from full host arrays) or for the tests'
     // plan digest (which covers the full arrays).
     const bool pack = long_rows.empty() && !env_int("RSP_ILU_DIGEST", 0) && env_int("RSP_ILU_PACK_PAIRS", 1);
+    bool want_stage = true;  // the factor plan reads the stages of its thin rows only
     if (pack) {
         const rsp_an::hvec<int> trows = rsp_an::factor_thin_rows(rp.data(), hp);
+        want_stage = !trows.empty();
         rsp_an::hvec<int> cbase(trows.size() + 1, 0);
         for (size_t r = 0; r < trows.size(); r++) {
             const int i = trows[r];
@@ -1630,8 +1632,8 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
         const int packed = cbase.back();
         hp.sym.pair_base.assign((size_t)std::max(n, 1), 0);
         for (size_t r = 0; r < trows.size(); r++) hp.sym.pair_base[(size_t)trows[r]] = cbase[r];
-        hp.sym.upd_l.resize((size_t)packed);
-        hp.sym.upd_u.resize((size_t)packed);
+        rsp_an::resize_uninit(hp.sym.upd_l, (size_t)packed);
+        rsp_an::resize_uninit(hp.sym.upd_u, (size_t)packed);
         if (packed > 0) {
             Arena ag;
             int *d_trows = nullptr, *d_cbase = nullptr, *d_pl = nullptr, *d_pu = nullptr;
@@ -1650,15 +1652,15 @@ static rsp_status_t ilu_symbolic_device(rsp_handle_t h, rsp_ilu0_info *f, const 
             RSP_CHECK_HIP(e);
         }
     } else {
-        hp.sym.upd_l.resize((size_t)total);
-        hp.sym.upd_u.resize((size_t)total);
+        rsp_an::resize_uninit(hp.sym.upd_l, (size_t)total);
+        rsp_an::resize_uninit(hp.sym.upd_u, (size_t)total);
         if (total > 0) {
             RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_l.data(), f->d_upd_l, (size_t)total * 4, hipMemcpyDeviceToHost, s));
             RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.upd_u.data(), f->d_upd_u, (size_t)total * 4, hipMemcpyDeviceToHost, s));
         }
     }
-    hp.sym.stage.resize((size_t)nnz_s);
-    if (nnz_s > 0)
+    rsp_an::resize_uninit(hp.sym.stage, want_stage ? (size_t)nnz_s : 0);
+    if (nnz_s > 0 && want_stage)
         RSP_CHECK_HIP(hipMemcpyAsync(hp.sym.stage.data(), d_stage, (size_t)nnz_s * 4, hipMemcpyDeviceToHost, s));
     RSP_CHECK_HIP(hipStreamSynchronize(s));
     sub("D2H pairs + stages");
@@ -1724,7 +1726,8 @@ static rsp_status_t rsp_ilu0_analysis_impl(rsp_handle_t h, int n, int nnz, const
     if (nnz_s > 0 && !d_col_ind) return RSP_STATUS_INVALID_VALUE;
     if (nnz_s > nnz) return RSP_STATUS_INVALID_VALUE;  // entries past the declared arrays
     pre("D2H rowptr + checks");
-    rsp_an::hvec<int> ci((size_t)nnz_s);
+    rsp_an::hvec<int> ci;
+    rsp_an::resize_uninit(ci, (size_t)nnz_s);  // (downloaded whole below)
     std::unique_ptr<rsp_an::IluHostPlan> hp(new (std::nothrow) rsp_an::IluHostPlan());
     if (!hp) return RSP_STATUS_ALLOC_FAILED;
     hp->n = n;
