@@ -119,21 +119,26 @@ __global__ __launch_bounds__(64) void an_pairs(const int *__restrict__ rows, con
 }
 
 // The same lists for the rows of <= `cap` entries, with row i's columns
-// staged in LDS beside its counters (dynamic LDS: 2 cap ints): the search for
+// staged in LDS beside its counters (dynamic LDS: 3 cap ints): the search for
 // each column of row k in row i is an LDS binary search instead of a chain of
-// global loads, row i's lower positions' k, row k's upper range are gathered
-// 64 at a time (one lane each, then read lane by lane), and the column load of
-// the next step is issued before the current step's search (round 6: the
-// circuits' rows of hundreds of lower positions, several of them into hub
-// rows, held a wave ~1 ms per pass). Same traversal, same order: the (p, q)
-// steps run in ascending p, then q, as an_pairs.
+// global loads, and the (p, q) steps are FLATTENED: for 64 lower positions p
+// at a time, the upper parts of their rows k are concatenated (an exclusive
+// scan of their lengths) and the wave takes 64 consecutive (p, q) of that
+// sequence per step, the next step's column loads issued before this step's
+// searches (round 6: one step per p left a circuit row of hundreds of lower
+// positions, most with rows k of a few upper entries, at one dependent load
+// per p, ~0.5-0.9 ms per pass). Order: a step's lanes are in (p, q) order, so
+// two lanes of one step that hit the same target t are ranked by lane (the
+// lower lane has the smaller p) — the lists come out in ascending k as in the
+// one-p-per-step walk. Counting needs no order (LDS atomic adds).
 template <bool FILL>
 __global__ __launch_bounds__(64) void an_pairs_lds(const int *__restrict__ rows, int cap, const int *__restrict__ rp,
                                                    const int *__restrict__ ci, const int *__restrict__ dpos,
                                                    const int *__restrict__ hasdiag, int *__restrict__ cnt_or_ptr,
                                                    int *__restrict__ upd_l, int *__restrict__ upd_u) {
     extern __shared__ int an_lds[];
-    int *cur = an_lds, *cols = an_lds + cap;  // indexed by position - rs
+    int *cur = an_lds, *cols = an_lds + cap, *tag = an_lds + 2 * cap;  // indexed by position - rs
+    __shared__ int offs[64], qsl[64];
     const int lane = threadIdx.x;
     const int i = rows[blockIdx.x];
     const int rs = rp[i], re = rp[i + 1], di = dpos[i], len = re - rs;
@@ -144,31 +149,48 @@ __global__ __launch_bounds__(64) void an_pairs_lds(const int *__restrict__ rows,
     __syncthreads();
     for (int pb = rs; pb < di; pb += 64) {
         const int np = min(64, di - pb);
-        int qs = 0, qe = 0;  // lane j: row k = ci[pb + j]'s upper range
+        int qs = 0, nq = 0;  // lane j: row k = ci[pb + j]'s upper range
         if (lane < np) {
             const int k = cols[pb + lane - rs];
             qs = dpos[k] + hasdiag[k];
-            qe = rp[k + 1];
+            nq = max(0, rp[k + 1] - qs);
         }
-        int j = 0, qb = 0, qend = 0;
-        for (; j < np; j++) {
-            qb = __builtin_amdgcn_readlane(qs, j);
-            qend = __builtin_amdgcn_readlane(qe, j);
-            if (qb < qend) break;
+        int incl = nq;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
         }
-        int col = (j < np && qb + lane < qend) ? ci[qb + lane] : -1;
-        while (j < np) {
-            // the next step (j2, qb2), its column load in flight under this step's search
-            int j2 = j, qb2 = qb + 64, qe2 = qend;
-            if (qb2 >= qe2)
-                for (j2 = j + 1; j2 < np; j2++) {
-                    qb2 = __builtin_amdgcn_readlane(qs, j2);
-                    qe2 = __builtin_amdgcn_readlane(qe, j2);
-                    if (qb2 < qe2) break;
-                }
-            const int coln = (j2 < np && qb2 + lane < qe2) ? ci[qb2 + lane] : -1;
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        offs[lane] = incl - nq;  // lanes >= np: total
+        qsl[lane] = qs;
+        __syncthreads();
+        // flattened index f -> (j, q): the largest j with offs[j] <= f
+        auto locate = [&](int f, int &jj) {
+            int lo = 0, hi = 63;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (offs[mid] <= f)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+            jj = lo;
+            return qsl[lo] + f - offs[lo];
+        };
+        int j = 0, q = 0, col = -1;
+        if (lane < total) {
+            q = locate(lane, j);
+            col = ci[q];
+        }
+        for (int fb = 0; fb < total; fb += 64) {
+            int jn = 0, qn = 0, coln = -1;
+            if (fb + 64 + lane < total) {
+                qn = locate(fb + 64 + lane, jn);
+                coln = ci[qn];
+            }
+            const int p = pb + j;
+            int t = -1;
             if (col >= 0) {
-                const int p = pb + j;
                 int lo = p + 1 - rs, hi = len;
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
@@ -177,20 +199,47 @@ __global__ __launch_bounds__(64) void an_pairs_lds(const int *__restrict__ rows,
                     else
                         hi = mid;
                 }
-                if (lo < len && cols[lo] == col) {
-                    const int m = cur[lo];
-                    cur[lo] = m + 1;
-                    if (FILL) {
-                        upd_l[m] = p;
-                        upd_u[m] = qb + lane;
+                if (lo < len && cols[lo] == col) t = lo;
+            }
+            if (!FILL) {
+                if (t >= 0) atomicAdd(&cur[t], 1);
+            } else {
+                // lanes of this step sharing a target: ranked by lane
+                // (volatile: the read-backs must not be folded into this
+                // lane's own stores). One lane of a clashing group wins the
+                // tag; the others mark the target, so the whole group sees it;
+                // then one ballot per clashing group ranks its lanes
+                volatile int *vtag = tag;
+                if (t >= 0) vtag[t] = lane;
+                const bool lost = t >= 0 && vtag[t] != lane;
+                int rank = 0, last = 1;
+                if (__any(lost)) {
+                    if (lost) vtag[t] = 64;
+                    const bool grp = t >= 0 && vtag[t] == 64;
+                    unsigned long long todo = __ballot(grp);
+                    while (todo) {
+                        const int tl = __builtin_amdgcn_readlane(t, __builtin_ctzll(todo));
+                        const unsigned long long mask = __ballot(grp && t == tl);
+                        if (grp && t == tl) {
+                            rank = __popcll(mask & ((1ull << lane) - 1ull));
+                            last = (mask >> lane) == 1ull ? 1 : 0;
+                        }
+                        todo &= ~mask;
                     }
                 }
+                if (t >= 0) {
+                    const int m = cur[t] + rank;
+                    upd_l[m] = p;
+                    upd_u[m] = q;
+                    __builtin_amdgcn_wave_barrier();
+                    if (last) cur[t] = m + 1;
+                }
             }
-            j = j2;
-            qb = qb2;
-            qend = qe2;
+            j = jn;
+            q = qn;
             col = coln;
         }
+        __syncthreads();  // (offs / qsl rewritten by the next batch)
     }
     __syncthreads();
     if (!FILL)
@@ -285,11 +334,21 @@ __global__ __launch_bounds__(64) void an_stages_wave(const int *__restrict__ row
     for (int xb = 0; xb < nl; xb += 63) {
         const int nx = min(63, nl - xb);
         const int u0l = lane <= nx ? ptr[rs + xb + lane] : 0;
+        if (__builtin_amdgcn_readlane(u0l, 0) == __builtin_amdgcn_readlane(u0l, nx)) {
+            // no pairs in these positions: stage 0 each, in parallel
+            if (lane < nx) {
+                st[xb + lane] = 0;
+                stage[rs + xb + lane] = 0;
+            }
+            __syncthreads();  // (later positions read these slots from other lanes)
+            continue;
+        }
         int u0 = __builtin_amdgcn_readlane(u0l, 0);
         int u1 = __builtin_amdgcn_readlane(u0l, 1);
         int v = u0 + lane < u1 ? upd_l[u0 + lane] : -1;
         for (int x = 0; x < nx; x++) {
             int s = 0;
+            const bool any = u1 > u0;  // (uniform)
             for (int u = u0;;) {
                 const int un = u + 64;
                 // the next load: this position's next 64 pairs, else the next position's first
@@ -311,7 +370,8 @@ __global__ __launch_bounds__(64) void an_stages_wave(const int *__restrict__ row
                 u = un;
             }
             // wave max (every lane ends with the row's value)
-            for (int o = 32; o > 0; o >>= 1) s = max(s, __shfl_xor(s, o));
+            if (any)
+                for (int o = 32; o > 0; o >>= 1) s = max(s, __shfl_xor(s, o));
             st[xb + x] = s;  // every lane writes the same value, and reads only its own writes
             stage[rs + xb + x] = s;
             smax = max(smax, s);
@@ -377,7 +437,7 @@ static hipError_t an_pairs_launch(const int *const rows_c[3], const int n_c[3], 
                                   const int *dpos, const int *hasdiag, int *cnt_or_ptr, int *gcur, int *upd_l,
                                   int *upd_u, hipStream_t s) {
     if (n_c[0] > 0)
-        an_pairs_lds<FILL><<<n_c[0], 64, 2 * cap0 * sizeof(int), s>>>(rows_c[0], cap0, rp, ci, dpos, hasdiag,
+        an_pairs_lds<FILL><<<n_c[0], 64, 3 * cap0 * sizeof(int), s>>>(rows_c[0], cap0, rp, ci, dpos, hasdiag,
                                                                     cnt_or_ptr, upd_l, upd_u);
     if (n_c[1] > 0)
         an_pairs<FILL, 16384><<<n_c[1], 64, 0, s>>>(rows_c[1], rp, ci, dpos, hasdiag, cnt_or_ptr, gcur, upd_l, upd_u);
